@@ -1,0 +1,165 @@
+/*
+ * ppo_engine.h -- C-ABI of the MI355X (gfx950) PPO rollout-and-update engine.
+ *
+ * One shared object (mujoco_reinforcement_learning_amd/libppo_engine.so), plain pointers and
+ * sizes, no torch types.  Every pointer argument named *_d is a caller-owned DEVICE buffer
+ * (a PyTorch-ROCm tensor's data_ptr()), contiguous, in the dtype and layout documented at the
+ * function.  `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream);
+ * nothing in the library synchronises the host except ppo_ctx_create/destroy.
+ *
+ * Return codes: 0 = ok, PPO_EINVAL on a bad argument (shape, null, size), PPO_EHIP on a HIP
+ * runtime error; the message is in ppo_last_error() (thread-local).  The Python host raises
+ * RuntimeError with that message (mirroring the reference's RuntimeError/ValueError style).
+ *
+ * The reference has no FFI: its "plugin interface" is a set of duck-typed Python classes.  Each
+ * entry point below replaces the reference function cited next to it; the Python host
+ * (mujoco_reinforcement_learning_amd/) keeps the reference's class/method surface on top.
+ *
+ * Buffer layout.  The rollout buffer is TIME-major in HBM: element (n, t) of
+ * the reference's (N, T) TensorDict lives at storage row s = t*N + n, so one rollout step writes
+ * one contiguous row block and the GAE scan reads coalesced rows.  The reference's flat minibatch
+ * index f = n*T + t (memory.view(-1), ppo.py:99) is translated by ppo_perm_to_rows.
+ *
+ * Flat parameter layout: actor then critic, each in torch `Module.parameters()` order, i.e.
+ *   actor : actor_logstd[A], then per layer l: W_l[out][in] (row-major, torch Linear), b_l[out]
+ *   critic: per layer l: W_l[out][in], b_l[out]
+ * Gradients, Adam moments and split-K partial slabs use the same layout.
+ */
+#ifndef PPO_ENGINE_H
+#define PPO_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPO_ABI_VERSION 1
+#define PPO_EINVAL (-22)
+#define PPO_EHIP (-5)
+#define PPO_MAX_LAYERS 8
+
+/* NetworkConfig.activation_class (features.py:41-54; main.py uses ReLU). */
+enum { PPO_ACT_RELU = 0, PPO_ACT_TANH = 1, PPO_ACT_ELU = 2 };
+
+/* Shapes of the actor-critic (models/linear/actor.py:9-23, models/critic.py:6-20,
+ * network_block_creator.py:24-72).  The critic flattens the (N, W, O) state like the actor. */
+typedef struct ppo_net_cfg {
+  int32_t obs_dim;          /* NetworkConfig.input_shape (O) */
+  int32_t window;           /* EnvironmentConfig.window_length (W) */
+  int32_t act_dim;          /* NetworkConfig.output_shape (A), <= 32 */
+  int32_t activation;       /* PPO_ACT_* for every hidden layer */
+  int32_t actor_use_bias;   /* NetworkConfig.use_bias (critic always has biases, critic.py:20) */
+  int32_t n_actor_hidden;
+  int32_t actor_hidden[PPO_MAX_LAYERS];
+  int32_t n_critic_hidden;
+  int32_t critic_hidden[PPO_MAX_LAYERS];
+  float output_max_value;   /* NetworkConfig.output_max_value (actor.py:30) */
+  int32_t max_rows;         /* workspace rows = max(num_envs, minibatch) */
+} ppo_net_cfg;
+
+typedef struct ppo_ctx ppo_ctx;
+
+int ppo_abi_version(void);
+const char *ppo_last_error(void);
+
+/* Context: owns activation workspace and split-K grad slabs on `device`; caller owns params. */
+int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out);
+int ppo_ctx_destroy(ppo_ctx *ctx);
+/* net = 0 actor, 1 critic, -1 both: number of fp32 parameters in the flat layout. */
+int64_t ppo_param_count(const ppo_ctx *ctx, int net);
+/* Bind the flat fp32 parameter buffer (device, ppo_param_count(ctx,-1) floats). */
+int ppo_bind_params(ppo_ctx *ctx, float *params_d);
+
+/* ---- A1: observation window + per-sample standardisation -------------------------------------
+ * replaces EnvironmentHelper.step's window shift (running_gym_sequential_vectorized.py:120-125,
+ * helper.py:51-57) and get_state/normalize_state/_normalize (:61-92).
+ * window_d: (N, O, W) f64, the reference's timestep.observation.  obs_d: (N, O) new observation
+ * (f64 if obs_is_f64 else f32).  reset_d (nullable): u8 per env; 1 -> all W slots := obs
+ * (termination / reset), 0 -> shift left and append.  With reset_d == NULL and all_reset != 0
+ * every env is reset (helper.py:59-64). */
+int ppo_obs_window_push(double *window_d, const void *obs_d, int obs_is_f64,
+                        const uint8_t *reset_d, int all_reset, int n, int o, int w, void *stream);
+/* state_d: (N, W, O) f32 = permute(standardise_f64(window)).  bounds: n_bounds+1 ascending
+ * feature-slice edges already clipped to O (Humanoid table :70-80); normalize=0 -> plain cast. */
+int ppo_obs_normalize(const double *window_d, float *state_d, int n, int o, int w,
+                      const int32_t *bounds, int n_bounds, int normalize, void *stream);
+
+/* ---- A2-A4: rollout policy step -------------------------------------------------------------
+ * replaces PPOAgent.get_state_value / act / Normal.sample / log_prob (ppo.py:22-26,
+ * ppo_agent.py:24-43, linear/actor.py:25-30).  state_d: (n, W*O) f32.
+ * eps_d (nullable): (n, A) f32 standard normals drawn by the host in reference RNG order
+ * (parity mode); NULL -> counter-based Philox4x32-10 normals keyed by (seed, offset) (perf mode).
+ * Outputs (each nullable): action (n, A) = fl(fl(eps*std)+mean); logp (n,) = sum_a log_prob;
+ * value (n,) critic V(s); mean (n, A).  Only the networks whose outputs are requested run. */
+int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
+                    uint64_t offset, float *action_d, float *logp_d, float *value_d, float *mean_d,
+                    void *stream);
+
+/* ---- A6/A9: per-env standardisation over T (ppo.py:66-69 rewards, :81-88 advantage/target) ----
+ * x_d: time-major (T, N) (element (n,t) at t*N+n), f32 or f64 (is_f64).  x <- (x-mean_T)/std_T*scale
+ * with the unbiased std (torch.std), in place. */
+int ppo_normalize_rows(void *x_d, int is_f64, int n, int t, double scale, void *stream);
+
+/* ---- A7/A8: GAE + value target -------------------------------------------------------------
+ * replaces torchrl 0.6.0 generalized_advantage_estimate called at ppo.py:70-80.
+ * All arrays time-major (T, N).  value_d / next_value_d f32; reward_d f64 or f32 (reward_is_f64);
+ * done_d / terminated_d u8 (done_d nullable -> done = terminated); force_last_done=1 applies
+ * ppo.py:72 (done[:, -1] = True).  Recurrence carried in f64, stored f32 (bit-exact with the
+ * reference).  adv_d, vtarget_d: f32 outputs. */
+int ppo_gae(const float *value_d, const float *next_value_d, const void *reward_d,
+            int reward_is_f64, const uint8_t *done_d, const uint8_t *terminated_d,
+            int force_last_done, int n, int t, double gamma, double lmbda, float *adv_d,
+            float *vtarget_d, void *stream);
+
+/* ---- A10: minibatch rows ---------------------------------------------------------------------
+ * rows_d[j] = storage row of reference flat index perm_d[start + j] (f = n*T+t -> t*N+n), j < b.
+ * Replaces memory.view(-1)[torch.randperm(N*T)][i*B:(i+1)*B] (ppo.py:99-106).  With shard_lo <
+ * shard_hi only envs in [shard_lo, shard_hi) are kept (exact data-parallel):
+ * they are compacted in order and the count is written to count_d (device int32). */
+int ppo_perm_to_rows(const int64_t *perm_d, int64_t start, int b, int n_envs, int t,
+                     int shard_lo, int shard_hi, int32_t *rows_d, int32_t *count_d,
+                     void *stream);
+/* Perf-mode shuffle: rows of a keyed bijection (cycle-walking Feistel) of [0, n_envs*t). */
+int ppo_feistel_rows(uint64_t seed, uint64_t epoch, int64_t start, int b, int n_envs, int t,
+                     int32_t *rows_d, void *stream);
+
+/* ---- A11-A13: one minibatch loss + gradients -------------------------------------------------
+ * replaces ppo.py:109-135 (actor/critic forward, Normal log_prob/entropy, huber critic loss,
+ * clipped surrogate, both backward passes).  Buffers are time-major storage arrays indexed by
+ * rows_d (b rows, or *count_d if count_d != NULL): states (rows, W*O) f32, actions (rows, A),
+ * old_logp (rows,), adv (rows,), vtarget (rows,).  inv_b = 1/B_global, inv_ba = 1/(B_global*A)
+ * (data-parallel ranks pass the global minibatch so an all-reduce SUM gives the mean-loss grad).
+ * grad_d: flat fp32 gradient (layout above), overwritten.  loss_d: 2 floats, (actor, critic)
+ * loss contributions of these rows, overwritten. */
+int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                       const float *old_logp_d, const float *adv_d, const float *vtarget_d,
+                       const int32_t *rows_d, int b, const int32_t *count_d, float clip_lo,
+                       float clip_hi, float entropy_coef, float inv_b, float inv_ba,
+                       float *grad_d, float *loss_d, void *stream);
+
+/* ---- A15: fused Adam over the flat buffer (torch.optim.Adam single-tensor path) ----------------
+ * replaces optimizers['critic'].step() / optimizers['actor'].step() (ppo.py:122,135) and
+ * torch.optim.Adam defaults (ppo_agent.py:15-18).  Elements [0, n_actor) use neg_step_actor,
+ * [n_actor, n) use neg_step_critic.  Every scalar is computed by the host in double exactly as
+ * adam.py does and rounded to f32 the way torch wraps a python scalar: neg_step = -(lr/(1-b1^k)),
+ * one_minus_beta1 = 1-b1, one_minus_beta2 = 1-b2, bc2_sqrt = (1-b2^k)**0.5.  One launch updates
+ * p, m, v in place. */
+int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n, int64_t n_actor,
+             float neg_step_actor, float neg_step_critic, float one_minus_beta1, float beta2,
+             float one_minus_beta2, float bc2_sqrt, float eps, void *stream);
+
+/* ---- harness: synthetic VecEnv dynamics on device + Philox normals ---------------------------
+ * The bench/test environment (physics is out of scope): obs' = base_obs + 0.1*a[:, o % A],
+ * r = base_r - 0.01*sum_a a^2 (f64), terminated = base_term.  obs_out (N, O) f64, reward (N,) f64,
+ * terminated (N,) u8.  Mirrors oracle/ppo_ref.py RefSyntheticEnv. */
+int ppo_synthetic_env_step(const float *base_obs_d, const float *base_reward_d,
+                           const uint8_t *base_term_d, const float *action_d, int n, int o, int a,
+                           double *obs_out_d, double *reward_out_d, uint8_t *term_out_d,
+                           void *stream);
+int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, int64_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPO_ENGINE_H */

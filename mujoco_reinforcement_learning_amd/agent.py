@@ -1,0 +1,260 @@
+"""``PPOEngineAgent`` -- drop-in for the reference ``PPOAgent`` (ppo_agent.py:10-43, agent.py:14-72).
+
+Same surface: ``networks`` (ModuleDict 'actor'/'critic' with the reference state_dict keys),
+``optimizers`` / ``schedulers`` dicts with the same keys, ``act(state, return_dist, test_phase)``,
+``get_state_value(state)``, ``save()``, ``load()``.  Parameters, gradients and Adam moments are
+flat fp32 device buffers; the fused Adam kernel (ppo_adam) updates both networks in one launch.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from . import engine as E
+from .features import Run
+from .models import EngineActor, EngineCritic, move_to_flat
+
+_ACT_NAMES = {nn.ReLU: "relu", nn.Tanh: "tanh", nn.ELU: "elu"}
+
+
+class FlatAdam:
+    """``torch.optim.Adam`` facade over one segment of the engine's flat buffers.
+
+    ``step()`` runs the HIP Adam kernel on this segment with the scalars computed in double
+    exactly as adam.py ``_single_tensor_adam`` does; ``state_dict()`` / ``load_state_dict()`` use
+    torch's Adam format so optimizer_<name>.pth files interoperate with the reference.
+    """
+
+    def __init__(self, params, flat_p, flat_g, flat_m, flat_v, lo: int, hi: int, lr: float,
+                 betas=(0.9, 0.999), eps: float = 1e-8):
+        self.params = list(params)
+        self.lo, self.hi = lo, hi
+        self._p, self._g, self._m, self._v = (flat_p[lo:hi], flat_g[lo:hi], flat_m[lo:hi],
+                                              flat_v[lo:hi])
+        self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": 0,
+                              "amsgrad": False, "maximize": False, "foreach": None,
+                              "capturable": False, "differentiable": False, "fused": None,
+                              "initial_lr": lr}]
+        self.step_count = 0
+
+    @property
+    def lr(self) -> float:
+        return self.param_groups[0]["lr"]
+
+    def scalars(self, step: int):
+        """(neg_step_size, bc2_sqrt) for Adam step ``step`` (adam.py, python double math)."""
+        beta1, beta2 = self.param_groups[0]["betas"]
+        bias_correction1 = 1 - beta1 ** step
+        bias_correction2 = 1 - beta2 ** step
+        step_size = self.lr / bias_correction1
+        return -step_size, bias_correction2 ** 0.5
+
+    def zero_grad(self, set_to_none: bool = True):
+        self._g.zero_()
+
+    def step(self):
+        self.step_count += 1
+        beta1, beta2 = self.param_groups[0]["betas"]
+        neg, bc2 = self.scalars(self.step_count)
+        n = self.hi - self.lo
+        E.adam(self._p, self._g, self._m, self._v, n, neg, neg, 1 - beta1, beta2, 1 - beta2, bc2,
+               self.param_groups[0]["eps"])
+
+    def _views(self):
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            yield p, self._m[off:off + n].view(p.shape), self._v[off:off + n].view(p.shape)
+            off += n
+
+    def state_dict(self):
+        state = {}
+        if self.step_count > 0:
+            for i, (_, m, v) in enumerate(self._views()):
+                state[i] = {"step": torch.tensor(float(self.step_count)), "exp_avg": m.clone(),
+                            "exp_avg_sq": v.clone()}
+        group = dict(self.param_groups[0])
+        group["params"] = list(range(len(self.params)))
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, sd):
+        group = sd["param_groups"][0]
+        for k in ("lr", "betas", "eps", "initial_lr"):
+            if k in group:
+                self.param_groups[0][k] = group[k]
+        st = sd.get("state", {})
+        if not st:
+            self.step_count = 0
+            self._m.zero_()
+            self._v.zero_()
+            return
+        for i, (_, m, v) in enumerate(self._views()):
+            s = st[i] if i in st else st[str(i)]
+            m.copy_(s["exp_avg"].to(m.device))
+            v.copy_(s["exp_avg_sq"].to(v.device))
+            self.step_count = int(float(s["step"]))
+
+
+class ExponentialLRFacade:
+    """``torch.optim.lr_scheduler.ExponentialLR`` (gamma per ``step()``, chainable form)."""
+
+    def __init__(self, optimizer: FlatAdam, gamma: float):
+        self.optimizer = optimizer
+        self.gamma = gamma
+        self.last_epoch = 0
+
+    def step(self):
+        self.last_epoch += 1
+        for g in self.optimizer.param_groups:
+            g["lr"] = g["lr"] * self.gamma
+
+    def get_last_lr(self):
+        return [g["lr"] for g in self.optimizer.param_groups]
+
+    def state_dict(self):
+        return {"gamma": self.gamma, "last_epoch": self.last_epoch}
+
+    def load_state_dict(self, sd):
+        self.gamma = sd["gamma"]
+        self.last_epoch = sd["last_epoch"]
+
+
+class PPOEngineAgent:
+    """PPOAgent on the MI355X engine."""
+
+    def __init__(self, run: Optional[Run] = None, device: Optional[torch.device] = None,
+                 max_rows: Optional[int] = None):
+        run = run or Run.instance()
+        if run is None:
+            raise ValueError("PPOEngineAgent needs a Run (construct entities Run first)")
+        self.run = run
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        nc, ec = run.network_config, run.environment_config
+        act_cls = nc.activation_class
+        if act_cls not in _ACT_NAMES:
+            raise ValueError(f"activation {act_cls} not supported by the engine (ReLU/Tanh/ELU)")
+        hidden = list(nc.linear_hidden_shapes)[:nc.num_linear_layers]
+        critic_hidden = run.engine_config.critic_hidden_shapes or hidden
+        in_dim = nc.input_shape * ec.window_length
+        self.networks = nn.ModuleDict()
+        # PPOAgent.initialize_networks builds the actor first, then the critic (RNG order)
+        self.networks["actor"] = EngineActor(in_dim, hidden, nc.output_shape, act_cls,
+                                             nc.use_bias, nc.output_max_value)
+        self.networks["critic"] = EngineCritic(in_dim, critic_hidden, act_cls)
+        self.flat_params = move_to_flat(self.networks, self.device)
+        for m in (self.networks["actor"], self.networks["critic"]):
+            m._agent = self
+        rows = max_rows or max(ec.num_envs, int(run.training_config.batch_size))
+        self.engine = E.Engine(nc.input_shape, ec.window_length, nc.output_shape, hidden,
+                               critic_hidden, _ACT_NAMES[act_cls], nc.use_bias,
+                               nc.output_max_value, rows, self.device)
+        if self.engine.n_params != self.flat_params.numel():
+            raise RuntimeError(f"flat layout mismatch: engine {self.engine.n_params} vs modules "
+                               f"{self.flat_params.numel()}")
+        self.engine.bind(self.flat_params)
+        self.flat_grad = torch.zeros_like(self.flat_params)
+        self.flat_m = torch.zeros_like(self.flat_params)
+        self.flat_v = torch.zeros_like(self.flat_params)
+        na = self.engine.n_actor
+        lr = run.training_config.learning_rate
+        self.optimizers: Dict[str, FlatAdam] = {
+            "actor": FlatAdam(self.networks["actor"].parameters(), self.flat_params,
+                              self.flat_grad, self.flat_m, self.flat_v, 0, na, lr),
+            "critic": FlatAdam(self.networks["critic"].parameters(), self.flat_params,
+                               self.flat_grad, self.flat_m, self.flat_v, na,
+                               self.engine.n_params, lr),
+        }
+        self.schedulers = {k: ExponentialLRFacade(o, 0.999) for k, o in self.optimizers.items()}
+
+    # ---- fused optimizer step for both networks (ppo.py:122 + :135 in one launch) -------------
+    def step_both(self) -> None:
+        oa, oc = self.optimizers["actor"], self.optimizers["critic"]
+        oa.step_count += 1
+        oc.step_count += 1
+        beta1, beta2 = oa.param_groups[0]["betas"]
+        neg_a, bc2 = oa.scalars(oa.step_count)
+        neg_c, bc2c = oc.scalars(oc.step_count)
+        if bc2 != bc2c or oc.param_groups[0]["betas"] != (beta1, beta2):
+            oa.step_count -= 1
+            oc.step_count -= 1
+            oa.step()
+            oc.step()
+            return
+        E.adam(self.flat_params, self.flat_grad, self.flat_m, self.flat_v, self.engine.n_actor,
+               neg_a, neg_c, 1 - beta1, beta2, 1 - beta2, bc2, oa.param_groups[0]["eps"])
+
+    # ---- Agent API ---------------------------------------------------------------------------
+    def _as_state(self, state: torch.Tensor) -> torch.Tensor:
+        s = state.to(device=self.device, dtype=torch.float32)
+        return s.reshape(len(s), -1).contiguous()
+
+    def _actor_mean(self, state: torch.Tensor) -> torch.Tensor:
+        s = self._as_state(state)
+        mean = torch.empty(len(s), self.engine.act_dim, device=self.device)
+        self.engine.policy_step(s, mean=mean)
+        return mean
+
+    def get_state_value(self, state: torch.Tensor) -> torch.Tensor:
+        """ppo_agent.py:24-25 -> (n, 1)."""
+        s = self._as_state(state)
+        value = torch.empty(len(s), 1, device=self.device)
+        self.engine.policy_step(s, value=value)
+        return value
+
+    def act(self, state: torch.Tensor, return_dist: bool = False, test_phase: bool = False):
+        """ppo_agent.py:27-43.  Sampling noise: torch global CPU generator (rng="torch", the
+        reference's ``Normal.sample`` draws) or on-device Philox (rng="philox")."""
+        s = self._as_state(state)
+        n, a = len(s), self.engine.act_dim
+        mean = torch.empty(n, a, device=self.device)
+        std = self.networks["actor"].actor_logstd.detach().exp()
+        if test_phase:
+            self.engine.policy_step(s, mean=mean)
+            action = mean.reshape(-1)  # torch.cat([means[i] for i in range(n)])
+        else:
+            action = torch.empty(n, a, device=self.device)
+            if self.run.engine_config.rng == "torch":
+                eps = torch.randn(n, a).to(self.device)
+                self.engine.policy_step(s, eps=eps, action=action, mean=mean)
+            else:
+                self._act_offset = getattr(self, "_act_offset", 0)
+                self.engine.policy_step(s, seed=self.run.engine_config.seed ^ 0x5EED,
+                                        offset=self._act_offset, action=action, mean=mean)
+                self._act_offset += n * a
+        if return_dist:
+            dist = torch.distributions.Normal(mean, std[None, :].expand(n, a), validate_args=False)
+            return action, dist
+        return action
+
+    # ---- checkpoint (agent.py:47-72; same files and keys) ------------------------------------
+    def save(self):
+        run = Run.instance()
+        path = f"{run.experiment_path}/networks/{run.dynamic_config.current_episode}"
+        os.makedirs(path, exist_ok=True)
+        torch.save({k: v.detach().cpu() for k, v in self.networks.state_dict().items()},
+                   f"{path}/networks.pth")
+        for name, opt in self.optimizers.items():
+            sd = opt.state_dict()
+            sd["state"] = {i: {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in s.items()}
+                           for i, s in sd["state"].items()}
+            torch.save(sd, f"{path}/optimizer_{name}.pth")
+        run.save()
+
+    def load(self):
+        run = Run.instance()
+        base = run.experiment_path
+        ep = run.dynamic_config.current_episode
+        path = f"{base}/networks/{ep}"
+        if not os.path.exists(path):
+            path = f"{base}/networks/best_results/{ep}"
+        if not os.path.exists(path):
+            raise ValueError("the current iteration does not exist")
+        sd = torch.load(f"{path}/networks.pth", map_location="cpu", weights_only=True)
+        self.networks.load_state_dict(sd)
+        for name, opt in self.optimizers.items():
+            opt.load_state_dict(torch.load(f"{path}/optimizer_{name}.pth", map_location="cpu",
+                                           weights_only=True))

@@ -1,0 +1,203 @@
+"""``PPOEngine`` -- drop-in for the reference ``PPO`` algorithm (ppo.py:11-159, base_algorithm.py:14-61).
+
+Same surface: ``PPOEngine(environment_helper, agent)``, ``iterate()`` -> ``_iterate()`` ->
+``rollout()`` (returns the buffer), ``calculate_advantages(memory)`` (adds ``advantage`` and
+``current_state_value_target``), ``train(memory)``.  The Python here only sequences launches; all
+arithmetic runs in the engine's HIP kernels on the current stream, and the host reads back once
+per iteration (losses, mean reward) instead of twice per minibatch (ppo.py:139-140).
+
+RNG (``Run.engine_config.rng``):
+  "torch"  -- the reference's draws from the torch global CPU generator, in its order: per rollout
+              step one (N, A) ``Normal.sample`` (ppo.py:23-25), per epoch ``randperm(N*T)``
+              (ppo.py:103) and per minibatch the (B, A) sample that ppo.py:110 draws and drops.
+  "philox" -- on-device Philox normals and a keyed Feistel permutation (no host RNG, no H2D).
+Data parallel (``dist`` = torch.distributed initialised, backend RCCL): each rank owns its env
+shard; per optimizer step ONE all-reduce(SUM) of the flat actor+critic gradient, with every rank
+scaling its loss by the global minibatch size.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Optional
+
+import torch
+
+from . import engine as E
+from .buffer import RolloutBuffer
+from .features import Run
+
+
+def _default_log(msg: str) -> None:
+    print(msg, flush=True)
+
+
+class PPOEngine:
+    def __init__(self, environment_helper, agent, log: Optional[Callable[[str], None]] = None,
+                 process_group=None):
+        self.environment_helper = environment_helper
+        self.agent = agent
+        self.run: Run = environment_helper.run
+        self.log = log or _default_log
+        self.pg = process_group
+        self.world = 1
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            self.world = torch.distributed.get_world_size(process_group)
+        ec, nc = self.run.environment_config, self.run.network_config
+        self.buffer = RolloutBuffer(ec.num_envs, ec.maximum_timesteps, nc.input_shape,
+                                    ec.window_length, nc.output_shape, agent.device)
+        self.iteration = 0
+        self.last_losses = (float("nan"), float("nan"))
+        self.last_mean_reward = float("nan")
+        self.timings = {}
+        self._rows = None
+        self._loss_buf = None
+
+    # ---- helpers -----------------------------------------------------------------------------
+    def _rng(self) -> str:
+        return self.run.engine_config.rng
+
+    def _seed(self) -> int:
+        return int(self.run.engine_config.seed)
+
+    def _eps(self, n: int, a: int):
+        """(eps tensor or None, philox offset) for one (n, A) sampling draw."""
+        if self._rng() == "torch":
+            return torch.randn(n, a).to(self.agent.device, non_blocking=True), 0
+        return None, None
+
+    # ---- ppo.py:13-60 ----------------------------------------------------------------------
+    @torch.no_grad()
+    def rollout(self) -> RolloutBuffer:
+        helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
+        n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        helper.reset()
+        helper.reset_environment(test_phase=False)
+        # helpers that can write straight into the buffer (SyntheticVecEnvHelper) skip the copies
+        fast_state = fast_step = bool(getattr(helper, "writes_into_buffer", False))
+
+        def observe(slot: int):
+            if fast_state:
+                helper.get_state(test_phase=False, out=buf.states[slot])
+            else:
+                buf.states[slot].copy_(helper.get_state(test_phase=False).reshape(n, -1))
+
+        seed = self._seed() * 1_000_003 + 17
+        base_off = self.iteration * (t_len * n * a)
+        observe(0)
+        eps, _ = self._eps(n, a)
+        eng.policy_step(buf.states[0], eps=eps, seed=seed, offset=base_off, action=buf.actions[0],
+                        logp=buf.logp[0], value=buf.values[0])
+        for t in range(t_len):
+            if fast_step:
+                helper.step(buf.actions[t], reward_out=buf.reward[t], terminated_out=buf.terminated[t])
+            else:
+                helper.step(buf.actions[t])
+                ts = helper.environment.timestep
+                buf.reward[t].copy_(torch.as_tensor(ts.reward))
+                buf.terminated[t].copy_(torch.as_tensor(ts.terminated))
+                buf.truncated[t].copy_(torch.as_tensor(ts.truncated))
+            observe(t + 1)
+            if t + 1 < t_len:
+                eps, _ = self._eps(n, a)
+                eng.policy_step(buf.states[t + 1], eps=eps, seed=seed,
+                                offset=base_off + (t + 1) * n * a, action=buf.actions[t + 1],
+                                logp=buf.logp[t + 1], value=buf.values[t + 1])
+            else:
+                eng.policy_step(buf.states[t_len], value=buf.values[t_len])
+        return buf
+
+    # ---- ppo.py:62-91 ----------------------------------------------------------------------
+    @torch.no_grad()
+    def calculate_advantages(self, memory: RolloutBuffer) -> None:
+        run = self.run
+        buf = memory
+        t_len = buf.horizon
+        rewards = buf.reward
+        if run.normalize_rewards:
+            if buf.reward_work is None:
+                buf.reward_work = torch.empty_like(buf.reward)
+            buf.reward_work.copy_(buf.reward)
+            E.normalize_rows(buf.reward_work, run.ppo_config.advantage_scaler)
+            rewards = buf.reward_work
+        E.gae(buf.values[:t_len], buf.values[1:], rewards, buf.terminated, run.ppo_config.gamma,
+              run.ppo_config.lmbda, buf.advantage, buf.value_target, force_last_done=True)
+        if run.ppo_config.normalize_advantage:
+            E.normalize_rows(buf.advantage, run.ppo_config.advantage_scaler)
+            E.normalize_rows(buf.value_target, run.ppo_config.advantage_scaler)
+
+    # ---- ppo.py:93-154 ---------------------------------------------------------------------
+    def train(self, memory: RolloutBuffer):
+        run, agent, eng, buf = self.run, self.agent, self.agent.engine, memory
+        n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        bs = run.training_config.batch_size
+        epochs = int(run.training_config.epochs_per_iteration)
+        batches_per_epoch = int(t_len * n / bs)
+        if batches_per_epoch <= 0 or float(bs) != int(bs):
+            # ppo.py:142: an epoch without a full minibatch divides by len([]) == 0
+            raise ZeroDivisionError("division by zero")
+        b = int(bs)
+        dev = agent.device
+        if self._rows is None or self._rows.numel() < b:
+            self._rows = torch.empty(b, dtype=torch.int32, device=dev)
+        if self._loss_buf is None or self._loss_buf.shape != (epochs, batches_per_epoch, 2):
+            self._loss_buf = torch.empty(epochs, batches_per_epoch, 2, dtype=torch.float32,
+                                         device=dev)
+        ppo = run.ppo_config
+        clip_lo = 1.0 - ppo.clip_epsilon
+        clip_hi = 1.0 + ppo.clip_epsilon
+        b_global = b * self.world
+        inv_b = 1.0 / b_global
+        inv_ba = 1.0 / (b_global * a)
+        states = buf.states
+        for epoch in range(epochs):
+            if self._rng() == "torch":
+                perm = torch.randperm(n * t_len).to(dev, non_blocking=True)
+            for i in range(batches_per_epoch):
+                if self._rng() == "torch":
+                    torch.randn(b, a)  # ppo.py:110: agent.act draws a sample it never uses
+                    E.perm_to_rows(perm, i * b, b, n, t_len, self._rows)
+                else:
+                    E.feistel_rows(self._seed(), self.iteration * epochs + epoch, i * b, b, n,
+                                   t_len, self._rows)
+                eng.minibatch_grad(states, buf.actions, buf.logp, buf.advantage, buf.value_target,
+                                   self._rows, b, agent.flat_grad, self._loss_buf[epoch, i],
+                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba)
+                if self.world > 1:
+                    torch.distributed.all_reduce(agent.flat_grad, group=self.pg)
+                agent.step_both()
+        if run.dynamic_config.current_episode < 2500:
+            for scheduler in agent.schedulers.values():
+                scheduler.step()
+        return self._loss_buf
+
+    def _finish_logging(self, loss_buf: torch.Tensor) -> None:
+        losses = loss_buf.double().cpu()
+        if self.world > 1:
+            pass  # per-rank contributions; the rank-0 line reports its own shard
+        epoch_means = losses.mean(dim=1)
+        actor_loss = float(epoch_means[:, 0].mean())
+        critic_loss = float(epoch_means[:, 1].mean())
+        self.last_losses = (actor_loss, critic_loss)
+
+    # ---- ppo.py:156-159, base_algorithm.py:53-58 ----------------------------------------------
+    def _iterate(self):
+        memory = self.rollout()
+        self.calculate_advantages(memory)
+        loss_buf = self.train(memory)
+        self.iteration += 1
+        return memory, loss_buf
+
+    def iterate(self, verbose: bool = True):
+        t0 = time.perf_counter()
+        memory, loss_buf = self._iterate()
+        self._finish_logging(loss_buf)
+        self.last_mean_reward = float(memory.reward.mean())
+        run = self.run
+        if verbose:
+            ep = run.dynamic_config.current_episode
+            self.log(f"[iteration {ep}] total episode reward: {self.last_mean_reward}")
+            self.log(f"Actor Loss: {self.last_losses[0]} Critic Loss: {self.last_losses[1]} "
+                     f"Epoch Loss: {self.last_losses[0] + self.last_losses[1]}")
+            self.log(f"iterate took {time.perf_counter() - t0:.4f} s")
+        run.dynamic_config.next_episode()
+        return memory

@@ -1,0 +1,959 @@
+// Actor-critic MLP forward/backward on gfx950 MFMA + the PPO loss heads + split-K gradient
+// reduction, behind the ppo_ctx C-ABI (ppo_policy_step, ppo_minibatch_grad).
+//
+// Every dense fc-layer product is one MFMA GEMM template (v_mfma_f32_32x32x2_f32: exact f32
+// inputs, f32 accumulate -- the reference computes in f32, so parity keeps f32 operands):
+//   forward   Y  = act(X W^T + b)          A = X  [rows][in]  (optionally gathered by row index)
+//   input grad dX = (dY W) * act'(X)        A = dY [rows][out], B = W [out][in]
+//   weight grad dW = dY^T X  (split-K over the minibatch rows, per-split slabs, + bias colsums)
+// Operands are staged global -> registers -> LDS ([k][m] / [k][n], row stride +2 words: the
+// transposing store is conflict-free for 32-lane write groups, the MFMA fragment reads are
+// consecutive), double-buffered with one barrier per k-tile.  Actor and critic layers of equal
+// shape run in one launch (blockIdx.z = net).
+//
+// Heads (output widths A and 1) are wave-per-row VALU kernels: tanh/mean, sampling, log-prob,
+// clipped surrogate, Huber, and the head backward, with torch's formulas (SURVEY.md s8(a) A3-A4,
+// A11-A13).  Reductions are in a fixed order (split slabs summed 0..S-1), so results are
+// bit-reproducible run to run.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "common.h"
+
+namespace ppo {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { A_MK = 0, A_KM = 1 };
+enum { B_NK = 0, B_KN = 1 };
+enum { EPI_FWD = 0, EPI_DX = 1, EPI_PARTIAL = 2 };
+
+struct GemmProblem {
+  const float *a;
+  const int32_t *a_rows;  // gather on the stored matrix's row index
+  int64_t lda;
+  const float *b;
+  const int32_t *b_rows;
+  int64_t ldb;
+  float *c;
+  int64_t ldc;
+  const float *bias;   // EPI_FWD, nullable
+  const float *aux;    // EPI_DX: layer input activations (same layout as c; c may alias it)
+  float *colsum;       // EPI_PARTIAL: bias-gradient slab base, nullable
+  int m, n;
+};
+
+struct GemmBatch {
+  GemmProblem p[2];
+  int k;                   // reduction length (EPI_PARTIAL: rows)
+  const int32_t *rows_n;   // device row count: M for FWD/DX, K for PARTIAL (nullable)
+  int act;
+  int splits;              // EPI_PARTIAL
+  int64_t slab_stride;     // EPI_PARTIAL: floats between split slabs
+};
+
+template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = 32 * TM * WM;
+  constexpr int BN = 32 * TN * WN;
+  constexpr int SA = BM + 2;
+  constexpr int SB = BN + 2;
+  constexpr int A_PER = BM * BK / NT;
+  constexpr int B_PER = BN * BK / NT;
+  static_assert((BM * BK) % NT == 0 && (BN * BK) % NT == 0, "tile/thread mismatch");
+  static_assert(BK % 2 == 0, "BK must be even for 32x32x2");
+  __shared__ float lds[2 * BK * (SA + SB)];
+
+  const GemmProblem P = (blockIdx.z == 0) ? gb.p[0] : gb.p[1];
+  int M = P.m, N = P.n, K = gb.k;
+  if (gb.rows_n) {
+    if (EPI == EPI_PARTIAL) K = *gb.rows_n;
+    else M = *gb.rows_n;
+  }
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tile_m = blockIdx.x / tiles_n;
+  const int tile_n = blockIdx.x - tile_m * tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  if (m0 >= M || n0 >= N) return;  // uniform per block
+  int kbeg = 0, kend = K;
+  const int split = (EPI == EPI_PARTIAL) ? static_cast<int>(blockIdx.y) : 0;
+  if (EPI == EPI_PARTIAL) {
+    kbeg = static_cast<int>((static_cast<int64_t>(split) * K) / gb.splits);
+    kend = static_cast<int>((static_cast<int64_t>(split + 1) * K) / gb.splits);
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  float ra[A_PER], rb[B_PER];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int e = tid + i * NT;
+      int mm, kk;
+      if (AMODE == A_MK) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < M && gk < kend) {
+        if (AMODE == A_MK) {
+          const int64_t row = P.a_rows ? P.a_rows[gm] : gm;
+          v = P.a[row * P.lda + gk];
+        } else {
+          const int64_t row = P.a_rows ? P.a_rows[gk] : gk;
+          v = P.a[row * P.lda + gm];
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int e = tid + i * NT;
+      int nn, kk;
+      if (BMODE == B_NK) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
+      const int gn = n0 + nn, gk = k0 + kk;
+      float v = 0.f;
+      if (gn < N && gk < kend) {
+        if (BMODE == B_NK) {
+          const int64_t row = P.b_rows ? P.b_rows[gn] : gn;
+          v = P.b[row * P.ldb + gk];
+        } else {
+          const int64_t row = P.b_rows ? P.b_rows[gk] : gk;
+          v = P.b[row * P.ldb + gn];
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+    float *As = lds + buf * BK * (SA + SB);
+    float *Bs = As + BK * SA;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int e = tid + i * NT;
+      int mm, kk;
+      if (AMODE == A_MK) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
+      As[kk * SA + mm] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int e = tid + i * NT;
+      int nn, kk;
+      if (BMODE == B_NK) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
+      Bs[kk * SB + nn] = rb[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const bool do_colsum = (EPI == EPI_PARTIAL) && P.colsum && tile_n == 0 && tid < BM;
+  float colacc = 0.f;
+
+  const int ntiles = (kend - kbeg + BK - 1) / BK;
+  if (ntiles > 0) {
+    gload(kbeg);
+    lstore(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) gload(kbeg + (kt + 1) * BK);
+    const float *As = lds + cur * BK * (SA + SB);
+    const float *Bs = As + BK * SA;
+#pragma unroll
+    for (int kp = 0; kp < BK / 2; ++kp) {
+      const int kk = 2 * kp + (lane >> 5);
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = As[kk * SA + (wm * TM + i) * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[kk * SB + (wn * TN + j) * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (do_colsum) {
+      float s = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < BK; ++kk) s += As[kk * SA + tid];
+      colacc += s;
+    }
+    if (kt + 1 < ntiles) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue: 32x32 C map (row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31) ----------
+  float *cbase = P.c + (EPI == EPI_PARTIAL ? static_cast<int64_t>(split) * gb.slab_stride : 0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + (wn * TN + j) * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M && col < N) {
+          const int64_t off = static_cast<int64_t>(row) * P.ldc + col;
+          float v = acc[i][j][r];
+          if (EPI == EPI_FWD) {
+            if (P.bias) v = v + P.bias[col];
+            cbase[off] = act_forward(v, gb.act);
+          } else if (EPI == EPI_DX) {
+            cbase[off] = act_backward(v, P.aux[off], gb.act);
+          } else {
+            cbase[off] = v;
+          }
+        }
+      }
+    }
+  }
+  if (do_colsum && m0 + tid < M)
+    P.colsum[static_cast<int64_t>(split) * gb.slab_stride + m0 + tid] = colacc;
+}
+
+// ============================================================================================
+// Heads
+// ============================================================================================
+constexpr int kMaxAct = 32;
+
+struct PolicyHeadArgs {
+  const float *ha;   // actor last hidden (n, da) or null
+  const float *hc;   // critic last hidden (n, dc) or null
+  int da, dc, n, act_dim;
+  const float *wa, *ba, *logstd;  // actor head (A, da), (A) or null, (A)
+  const float *wc, *bc;           // critic head (1, dc), (1)
+  float omv;
+  const float *eps;               // (n, A) or null -> Philox(seed, offset + row*A + a)
+  uint64_t seed, offset;
+  float *action, *logp, *value, *mean;
+};
+
+// One wave per env row.  logp follows Normal.log_prob term by term:
+//   (-(x-mu)^2) / (2*var) - log(std) - log(sqrt(2*pi)),  var = std*std,  summed a = 0..A-1.
+template <int HPL>
+__global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs q) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= q.n) return;
+  if (q.ha) {
+    float h[HPL];
+    const float *hr = q.ha + static_cast<int64_t>(row) * q.da;
+#pragma unroll
+    for (int j = 0; j < HPL; ++j) {
+      const int k = lane + 64 * j;
+      h[j] = (k < q.da) ? hr[k] : 0.f;
+    }
+    float my_z = 0.f;
+    for (int a = 0; a < q.act_dim; ++a) {
+      const float *w = q.wa + static_cast<int64_t>(a) * q.da;
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < HPL; ++j) {
+        const int k = lane + 64 * j;
+        if (k < q.da) part = fmaf(h[j], w[k], part);
+      }
+      const float z = wave_sum(part);
+      if (lane == a) my_z = z;
+    }
+    float lp = 0.f;
+    if (lane < q.act_dim) {
+      const int a = lane;
+      const float z = q.ba ? my_z + q.ba[a] : my_z;
+      const float mu = q.omv * tanhf(z);
+      const float sd = expf(q.logstd[a]);
+      const int64_t idx = static_cast<int64_t>(row) * q.act_dim + a;
+      const float e = q.eps ? q.eps[idx] : philox_normal_at(q.seed, q.offset + idx);
+      const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
+      if (q.action) q.action[idx] = x;
+      if (q.mean) q.mean[idx] = mu;
+      const float d = x - mu;
+      const float var = sd * sd;
+      lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+    }
+    if (q.logp) {
+      float s = 0.f;
+      for (int a = 0; a < q.act_dim; ++a) s += __shfl(lp, a, 64);
+      if (lane == 0) q.logp[row] = s;
+    }
+  }
+  if (q.hc && q.value) {
+    const float *hr = q.hc + static_cast<int64_t>(row) * q.dc;
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < HPL; ++j) {
+      const int k = lane + 64 * j;
+      if (k < q.dc) part = fmaf(hr[k], q.wc[k], part);
+    }
+    const float v = wave_sum(part);
+    if (lane == 0) q.value[row] = q.bc ? v + q.bc[0] : v;
+  }
+}
+
+struct UpdateHeadArgs {
+  const float *ha, *hc;          // last hidden (rows, da) / (rows, dc), minibatch order
+  float *ga, *gc;                // OUT: dH_L (rows, da) / (rows, dc)
+  float *dza, *dzc;              // OUT: d(head pre-activation) (rows, A) / (rows, 1)
+  int da, dc, act_dim, act;
+  const float *wa, *ba, *logstd, *wc, *bc;
+  float omv;
+  const int32_t *rows;           // storage row of minibatch row j
+  int rows_max;
+  const int32_t *rows_n;         // device count (nullable)
+  const float *actions, *old_logp, *adv, *vtarget;  // storage arrays
+  float clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
+  float *logstd_part;            // (splits, A)
+  float *loss_part;              // (splits, 2): sum over rows of actor / critic loss terms
+  int splits;
+};
+
+// One block per split of the minibatch, one wave per row at a time.  Gradients follow torch's
+// autograd formulas: minimum() splits a tie's gradient in halves, clamp passes it on the closed
+// interval, huber_loss_backward clips at +-delta, tanh backward is grad*(1-y*y).
+template <int HPL>
+__global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
+  __shared__ float red[4][kMaxAct + 2];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int count = q.rows_n ? *q.rows_n : q.rows_max;
+  const int r0 = static_cast<int>((static_cast<int64_t>(blockIdx.x) * count) / q.splits);
+  const int r1 = static_cast<int>((static_cast<int64_t>(blockIdx.x + 1) * count) / q.splits);
+  const int A = q.act_dim;
+  float lsacc = 0.f;                 // lane a: d loss / d logstd_a over this wave's rows
+  float la_acc = 0.f, lc_acc = 0.f;  // lane 0: loss sums
+  for (int j = r0 + wid; j < r1; j += 4) {
+    const int64_t sr = q.rows[j];
+    // ---------------- actor ----------------
+    float h[HPL];
+    const float *hr = q.ha + static_cast<int64_t>(j) * q.da;
+#pragma unroll
+    for (int t = 0; t < HPL; ++t) {
+      const int k = lane + 64 * t;
+      h[t] = (k < q.da) ? hr[k] : 0.f;
+    }
+    float my_z = 0.f;
+    for (int a = 0; a < A; ++a) {
+      const float *w = q.wa + static_cast<int64_t>(a) * q.da;
+      float part = 0.f;
+#pragma unroll
+      for (int t = 0; t < HPL; ++t) {
+        const int k = lane + 64 * t;
+        if (k < q.da) part = fmaf(h[t], w[k], part);
+      }
+      const float z = wave_sum(part);
+      if (lane == a) my_z = z;
+    }
+    float lp = 0.f, y = 0.f, d = 0.f, var = 1.f;
+    if (lane < A) {
+      const float z = q.ba ? my_z + q.ba[lane] : my_z;
+      y = tanhf(z);
+      const float mu = q.omv * y;
+      const float sd = expf(q.logstd[lane]);
+      const float x = q.actions[sr * A + lane];
+      d = x - mu;
+      var = sd * sd;
+      lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+    }
+    float logp = 0.f;
+    for (int a = 0; a < A; ++a) logp += __shfl(lp, a, 64);
+    const float ratio = expf(logp - q.old_logp[sr]);
+    const float adv = q.adv[sr];
+    const float s1 = ratio * adv;
+    const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+    const float s2 = cl * adv;
+    const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+    const float g = -q.inv_b;
+    const float g1 = (s1 < s2) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+    const float g2 = (s2 < s1) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+    const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+    const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+    const float dlogp = dratio * ratio;
+    float dz = 0.f;
+    if (lane < A) {
+      const float dmu = dlogp * (d / var);
+      dz = (dmu * q.omv) * (1.f - y * y);
+      lsacc += dlogp * ((d * d) / var - 1.f) - q.ent_coef * q.inv_ba;
+      q.dza[static_cast<int64_t>(j) * A + lane] = dz;
+    }
+    if (lane == 0) la_acc += mn;
+    // dH_L(actor) = (dz . W_head) * act'(h)
+    float *gr = q.ga + static_cast<int64_t>(j) * q.da;
+#pragma unroll
+    for (int t = 0; t < HPL; ++t) {
+      const int k = lane + 64 * t;
+      if (k < q.da) {
+        float s = 0.f;
+        for (int a = 0; a < A; ++a) s = fmaf(__shfl(dz, a, 64), q.wa[static_cast<int64_t>(a) * q.da + k], s);
+        gr[k] = act_backward(s, h[t], q.act);
+      }
+    }
+    // ---------------- critic ----------------
+    const float *cr = q.hc + static_cast<int64_t>(j) * q.dc;
+#pragma unroll
+    for (int t = 0; t < HPL; ++t) {
+      const int k = lane + 64 * t;
+      h[t] = (k < q.dc) ? cr[k] : 0.f;
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int t = 0; t < HPL; ++t) {
+      const int k = lane + 64 * t;
+      if (k < q.dc) part = fmaf(h[t], q.wc[k], part);
+    }
+    float v = wave_sum(part);
+    if (q.bc) v = v + q.bc[0];
+    const float diff = v - q.vtarget[sr];
+    const float ad = fabsf(diff);
+    if (lane == 0) lc_acc += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+    const float dv = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+    if (lane == 0) q.dzc[j] = dv;
+    float *gc = q.gc + static_cast<int64_t>(j) * q.dc;
+#pragma unroll
+    for (int t = 0; t < HPL; ++t) {
+      const int k = lane + 64 * t;
+      if (k < q.dc) gc[k] = act_backward(dv * q.wc[k], h[t], q.act);
+    }
+  }
+  // fixed-order block reduction: waves 0..3
+  if (lane < A) red[wid][lane] = lsacc;
+  if (lane == 0) {
+    red[wid][kMaxAct] = la_acc;
+    red[wid][kMaxAct + 1] = lc_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < A) {
+    const float s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) +
+                    red[3][threadIdx.x];
+    q.logstd_part[static_cast<int64_t>(blockIdx.x) * A + threadIdx.x] = s;
+  }
+  if (threadIdx.x == 0) {
+    q.loss_part[2 * blockIdx.x] = ((red[0][kMaxAct] + red[1][kMaxAct]) + red[2][kMaxAct]) +
+                                  red[3][kMaxAct];
+    q.loss_part[2 * blockIdx.x + 1] =
+        ((red[0][kMaxAct + 1] + red[1][kMaxAct + 1]) + red[2][kMaxAct + 1]) + red[3][kMaxAct + 1];
+  }
+}
+
+// ============================================================================================
+// Split-K reduction of the slabs into the flat gradient + loss scalars
+// ============================================================================================
+constexpr int kMaxSegs = 48;
+struct ReduceSeg {
+  int64_t dst, len;
+  const float *src;
+  int64_t stride;
+  int nsplit;
+};
+struct ReduceArgs {
+  ReduceSeg seg[kMaxSegs];
+  int nseg;
+  int64_t total;
+  float *grad;
+  const float *loss_part;
+  int loss_splits;
+  float inv_b;           // actor loss = -(sum min)*inv_b - ent_coef*H ; critic = sum*inv_b
+  const float *logstd;   // H = mean_a(0.5 + 0.5 log 2pi + log(exp(logstd_a))) (Normal.entropy)
+  int act_dim;
+  float ent_coef;
+  float *loss_out;
+};
+
+__global__ void reduce_slabs_kernel(ReduceArgs q) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < q.total) {
+    int s = 0;
+    while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
+    const ReduceSeg &g = q.seg[s];
+    const int64_t off = i - g.dst;
+    float acc = 0.f;
+    for (int k = 0; k < g.nsplit; ++k) acc += g.src[k * g.stride + off];
+    q.grad[i] = acc;
+  }
+  if (i == 0 && q.loss_out) {
+    float la = 0.f, lc = 0.f;
+    for (int k = 0; k < q.loss_splits; ++k) {
+      la += q.loss_part[2 * k];
+      lc += q.loss_part[2 * k + 1];
+    }
+    float h = 0.f;
+    if (q.logstd) {
+      for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
+      h = h / static_cast<float>(q.act_dim);
+    }
+    q.loss_out[0] = -(la * q.inv_b) - h * q.ent_coef;
+    q.loss_out[1] = lc * q.inv_b;
+  }
+}
+
+// ============================================================================================
+// Context
+// ============================================================================================
+struct LayerDesc {
+  int in, out;
+  int64_t w_off, b_off;  // flat offsets (b_off < 0: no bias)
+};
+
+struct NetDesc {
+  int n_hidden;
+  LayerDesc layer[PPO_MAX_LAYERS + 1];  // hidden layers then the head
+  int64_t begin, count;
+  int64_t logstd_off;                   // actor only
+  float *h[PPO_MAX_LAYERS];             // workspace: hidden outputs (max_rows, width)
+  float *g;                             // workspace: dH_L
+  float *dz;                            // workspace: head pre-activation grads (max_rows, out)
+};
+
+}  // namespace ppo
+
+struct ppo_ctx {
+  ppo_net_cfg cfg;
+  int device;
+  ppo::NetDesc net[2];
+  int64_t total_params;
+  float *params;
+  float *slabs;          // (kSlabSplits, total_params)
+  float *head_part;      // logstd partials (kHeadSplits, A) + loss partials (kHeadSplits, 2)
+  void *arena;
+};
+
+namespace ppo {
+
+constexpr int kSlabSplits = 64;
+constexpr int kHeadSplits = 512;
+
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
+static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  const int tiles = ceil_div(max_m, BM) * ceil_div(max_n, BN);
+  dim3 grid(tiles, EPI == EPI_PARTIAL ? gb.splits : 1, nprob);
+  gemm_f32_kernel<TM, TN, WM, WN, 16, AMODE, BMODE, EPI><<<grid, 64 * WM * WN, 0, st>>>(gb);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// FWD (A_MK, B_NK) and DX (A_MK, B_KN): rows-major M; big tiles when the row count is large.
+template <int BMODE, int EPI>
+static int run_rowwise(const GemmBatch &gb, int nprob, int rows, int max_n, hipStream_t st) {
+  if (rows >= 8192) return launch_gemm<2, 2, 2, 2, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
+  return launch_gemm<1, 1, 1, 4, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
+}
+
+static int run_partial(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+  if (max_m <= 32) return launch_gemm<1, 1, 1, 4, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
+  if (max_n <= 32) return launch_gemm<1, 1, 4, 1, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
+  return launch_gemm<2, 2, 2, 2, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
+}
+
+static int hpl_for(int width) {
+  if (width <= 256) return 4;
+  if (width <= 512) return 8;
+  return 16;
+}
+
+// Forward through the hidden layers of the requested nets.  x: (rows, in) f32 with optional
+// row gather.  Nets whose layer-l shapes agree share one launch.
+static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const int32_t *x_rows,
+                          int rows, const int32_t *rows_n, hipStream_t st) {
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  const int max_l = std::max(use[0] ? ctx->net[0].n_hidden : 0, use[1] ? ctx->net[1].n_hidden : 0);
+  for (int l = 0; l < max_l; ++l) {
+    GemmBatch gb{};
+    gb.k = 0;
+    gb.rows_n = rows_n;
+    gb.act = ctx->cfg.activation;
+    int np = 0, max_n = 0;
+    int kdim = -1;
+    for (int z = 0; z < 2; ++z) {
+      const NetDesc &nd = ctx->net[z];
+      if (!use[z] || l >= nd.n_hidden) continue;
+      const LayerDesc &L = nd.layer[l];
+      if (kdim >= 0 && kdim != L.in) {  // shapes differ: flush what we have
+        int rc = run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+        if (rc) return rc;
+        np = 0;
+        max_n = 0;
+      }
+      kdim = L.in;
+      GemmProblem &P = gb.p[np++];
+      P.a = (l == 0) ? x : nd.h[l - 1];
+      P.a_rows = (l == 0) ? x_rows : nullptr;
+      P.lda = (l == 0) ? din : nd.layer[l - 1].out;
+      P.b = ctx->params + L.w_off;
+      P.ldb = L.in;
+      P.c = nd.h[l];
+      P.ldc = L.out;
+      P.bias = L.b_off >= 0 ? ctx->params + L.b_off : nullptr;
+      P.m = rows;
+      P.n = L.out;
+      gb.k = L.in;
+      max_n = std::max(max_n, L.out);
+    }
+    if (np) {
+      int rc = run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+static int check_ctx(const ppo_ctx *ctx) {
+  PPO_REQUIRE(ctx != nullptr, "null ppo_ctx");
+  PPO_REQUIRE(ctx->params != nullptr, "ppo_ctx: parameters not bound (ppo_bind_params)");
+  return 0;
+}
+
+}  // namespace ppo
+
+using namespace ppo;
+
+extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out) {
+  PPO_REQUIRE(cfg && out, "ppo_ctx_create: null argument");
+  PPO_REQUIRE(cfg->obs_dim > 0 && cfg->window > 0, "ppo_ctx_create: bad obs/window");
+  PPO_REQUIRE(cfg->act_dim > 0 && cfg->act_dim <= kMaxAct, "ppo_ctx_create: act_dim must be in [1, %d]",
+              kMaxAct);
+  PPO_REQUIRE(cfg->n_actor_hidden >= 1 && cfg->n_actor_hidden <= PPO_MAX_LAYERS &&
+                  cfg->n_critic_hidden >= 1 && cfg->n_critic_hidden <= PPO_MAX_LAYERS,
+              "ppo_ctx_create: hidden layer count must be in [1, %d]", PPO_MAX_LAYERS);
+  PPO_REQUIRE(cfg->activation >= PPO_ACT_RELU && cfg->activation <= PPO_ACT_ELU,
+              "ppo_ctx_create: unknown activation %d", cfg->activation);
+  PPO_REQUIRE(cfg->max_rows > 0, "ppo_ctx_create: max_rows must be positive");
+  PPO_HIP_TRY(hipSetDevice(device));
+  ppo_ctx *ctx = new (std::nothrow) ppo_ctx();
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_create: out of host memory");
+  ctx->cfg = *cfg;
+  ctx->device = device;
+  const int din = cfg->obs_dim * cfg->window;
+  int64_t off = 0;
+  size_t ws_floats = 0;
+  const int64_t R = cfg->max_rows;
+  for (int z = 0; z < 2; ++z) {
+    NetDesc &nd = ctx->net[z];
+    nd.begin = off;
+    const int nh = z == 0 ? cfg->n_actor_hidden : cfg->n_critic_hidden;
+    const int32_t *hid = z == 0 ? cfg->actor_hidden : cfg->critic_hidden;
+    const bool bias = z == 0 ? cfg->actor_use_bias != 0 : true;
+    nd.n_hidden = nh;
+    if (z == 0) {
+      nd.logstd_off = off;
+      off += cfg->act_dim;
+    } else {
+      nd.logstd_off = -1;
+    }
+    int width = din;
+    for (int l = 0; l <= nh; ++l) {
+      const int o = (l < nh) ? hid[l] : (z == 0 ? cfg->act_dim : 1);
+      if (l < nh && (o <= 0 || o > 1024)) {
+        delete ctx;
+        set_error("ppo_ctx_create: hidden width %d out of range [1, 1024]", o);
+        return PPO_EINVAL;
+      }
+      LayerDesc &L = nd.layer[l];
+      L.in = width;
+      L.out = o;
+      L.w_off = off;
+      off += static_cast<int64_t>(o) * width;
+      L.b_off = bias ? off : -1;
+      if (bias) off += o;
+      if (l < nh) ws_floats += static_cast<size_t>(R) * o;
+      width = o;
+    }
+    ws_floats += static_cast<size_t>(R) * width;  // g = dH_L
+    ws_floats += static_cast<size_t>(R) * nd.layer[nh].out;  // dz
+    nd.count = off - nd.begin;
+  }
+  ctx->total_params = off;
+  ws_floats += static_cast<size_t>(kSlabSplits) * off;
+  ws_floats += static_cast<size_t>(kHeadSplits) * (cfg->act_dim + 2);
+  void *arena = nullptr;
+  hipError_t e = hipMalloc(&arena, ws_floats * sizeof(float) + 256);
+  if (e != hipSuccess) {
+    delete ctx;
+    set_error("ppo_ctx_create: hipMalloc(%zu bytes) failed: %s", ws_floats * sizeof(float),
+              hipGetErrorString(e));
+    return PPO_EHIP;
+  }
+  ctx->arena = arena;
+  float *p = static_cast<float *>(arena);
+  for (int z = 0; z < 2; ++z) {
+    NetDesc &nd = ctx->net[z];
+    for (int l = 0; l < nd.n_hidden; ++l) {
+      nd.h[l] = p;
+      p += R * nd.layer[l].out;
+    }
+    nd.g = p;
+    p += R * nd.layer[nd.n_hidden - 1].out;
+    nd.dz = p;
+    p += R * nd.layer[nd.n_hidden].out;
+  }
+  ctx->slabs = p;
+  p += static_cast<int64_t>(kSlabSplits) * off;
+  ctx->head_part = p;
+  ctx->params = nullptr;
+  *out = ctx;
+  return 0;
+}
+
+extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
+  if (!ctx) return 0;
+  if (ctx->arena) {
+    hipSetDevice(ctx->device);
+    hipFree(ctx->arena);
+  }
+  delete ctx;
+  return 0;
+}
+
+extern "C" int64_t ppo_param_count(const ppo_ctx *ctx, int net) {
+  if (!ctx) return -1;
+  if (net == 0 || net == 1) return ctx->net[net].count;
+  return ctx->total_params;
+}
+
+extern "C" int ppo_bind_params(ppo_ctx *ctx, float *params_d) {
+  PPO_REQUIRE(ctx && params_d, "ppo_bind_params: null argument");
+  ctx->params = params_d;
+  return 0;
+}
+
+extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d,
+                               uint64_t seed, uint64_t offset, float *action_d, float *logp_d,
+                               float *value_d, float *mean_d, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(state_d && n > 0, "ppo_policy_step: bad state / n");
+  PPO_REQUIRE(n <= ctx->cfg.max_rows, "ppo_policy_step: n=%d exceeds max_rows=%d", n,
+              ctx->cfg.max_rows);
+  hipStream_t st = as_stream(stream);
+  const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
+  if (!use[0] && !use[1]) return 0;
+  if (int rc = forward_hidden(ctx, use, state_d, nullptr, n, nullptr, st)) return rc;
+  const NetDesc &A = ctx->net[0], &C = ctx->net[1];
+  PolicyHeadArgs q{};
+  q.n = n;
+  q.act_dim = ctx->cfg.act_dim;
+  q.omv = ctx->cfg.output_max_value;
+  if (use[0]) {
+    const LayerDesc &hl = A.layer[A.n_hidden];
+    q.ha = A.h[A.n_hidden - 1];
+    q.da = hl.in;
+    q.wa = ctx->params + hl.w_off;
+    q.ba = hl.b_off >= 0 ? ctx->params + hl.b_off : nullptr;
+    q.logstd = ctx->params + A.logstd_off;
+  }
+  if (use[1]) {
+    const LayerDesc &hl = C.layer[C.n_hidden];
+    q.hc = C.h[C.n_hidden - 1];
+    q.dc = hl.in;
+    q.wc = ctx->params + hl.w_off;
+    q.bc = ctx->params + hl.b_off;
+  }
+  q.eps = eps_d;
+  q.seed = seed;
+  q.offset = offset;
+  q.action = action_d;
+  q.logp = logp_d;
+  q.value = value_d;
+  q.mean = mean_d;
+  const int hpl = hpl_for(std::max(q.da, q.dc));
+  const int grid = ceil_div(n, 4);
+  if (hpl == 4) policy_head_kernel<4><<<grid, 256, 0, st>>>(q);
+  else if (hpl == 8) policy_head_kernel<8><<<grid, 256, 0, st>>>(q);
+  else policy_head_kernel<16><<<grid, 256, 0, st>>>(q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                                  const float *old_logp_d, const float *adv_d,
+                                  const float *vtarget_d, const int32_t *rows_d, int b,
+                                  const int32_t *count_d, float clip_lo, float clip_hi,
+                                  float entropy_coef, float inv_b, float inv_ba, float *grad_d,
+                                  float *loss_d, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(states_d && actions_d && old_logp_d && adv_d && vtarget_d && rows_d && grad_d,
+              "ppo_minibatch_grad: null buffer");
+  PPO_REQUIRE(b > 0 && b <= ctx->cfg.max_rows, "ppo_minibatch_grad: b=%d outside [1, max_rows=%d]",
+              b, ctx->cfg.max_rows);
+  hipStream_t st = as_stream(stream);
+  const bool both[2] = {true, true};
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  const int A = ctx->cfg.act_dim;
+  if (int rc = forward_hidden(ctx, both, states_d, rows_d, b, count_d, st)) return rc;
+
+  // ---- heads: loss, dz, dH_L -------------------------------------------------------------
+  NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
+  const LayerDesc &HA = NA.layer[NA.n_hidden], &HC = NC.layer[NC.n_hidden];
+  int head_splits = std::min(kHeadSplits, std::max(1, b / 32));
+  UpdateHeadArgs u{};
+  u.ha = NA.h[NA.n_hidden - 1];
+  u.hc = NC.h[NC.n_hidden - 1];
+  u.ga = NA.g;
+  u.gc = NC.g;
+  u.dza = NA.dz;
+  u.dzc = NC.dz;
+  u.da = HA.in;
+  u.dc = HC.in;
+  u.act_dim = A;
+  u.act = ctx->cfg.activation;
+  u.wa = ctx->params + HA.w_off;
+  u.ba = HA.b_off >= 0 ? ctx->params + HA.b_off : nullptr;
+  u.logstd = ctx->params + NA.logstd_off;
+  u.wc = ctx->params + HC.w_off;
+  u.bc = ctx->params + HC.b_off;
+  u.omv = ctx->cfg.output_max_value;
+  u.rows = rows_d;
+  u.rows_max = b;
+  u.rows_n = count_d;
+  u.actions = actions_d;
+  u.old_logp = old_logp_d;
+  u.adv = adv_d;
+  u.vtarget = vtarget_d;
+  u.clip_lo = clip_lo;
+  u.clip_hi = clip_hi;
+  u.ent_coef = entropy_coef;
+  u.inv_b = inv_b;
+  u.inv_ba = inv_ba;
+  u.logstd_part = ctx->head_part;
+  u.loss_part = ctx->head_part + static_cast<int64_t>(kHeadSplits) * A;
+  u.splits = head_splits;
+  const int hpl = hpl_for(std::max(u.da, u.dc));
+  if (hpl == 4) update_head_kernel<4><<<head_splits, 256, 0, st>>>(u);
+  else if (hpl == 8) update_head_kernel<8><<<head_splits, 256, 0, st>>>(u);
+  else update_head_kernel<16><<<head_splits, 256, 0, st>>>(u);
+  PPO_LAUNCHED();
+
+  // ---- weight gradients, split-K over rows, deepest layer first ---------------------------
+  const int splits = std::min(kSlabSplits, std::max(1, b / 64));
+  const int64_t P = ctx->total_params;
+  auto partial = [&](int layer_from_top) -> int {
+    // layer index per net: head = n_hidden, then n_hidden-1 ... 0
+    GemmBatch gb{};
+    gb.k = b;
+    gb.rows_n = count_d;
+    gb.splits = splits;
+    gb.slab_stride = P;
+    int np = 0, max_m = 0, max_n = 0;
+    for (int z = 0; z < 2; ++z) {
+      NetDesc &nd = ctx->net[z];
+      const int l = nd.n_hidden - layer_from_top;
+      if (l < 0) continue;
+      const LayerDesc &L = nd.layer[l];
+      GemmProblem &Q = gb.p[np++];
+      // dY of layer l: head -> dz, top hidden -> g, lower hidden -> h[l] (overwritten in place)
+      Q.a = (l == nd.n_hidden) ? nd.dz : (l == nd.n_hidden - 1 ? nd.g : nd.h[l]);
+      Q.lda = L.out;
+      Q.b = (l == 0) ? states_d : nd.h[l - 1];
+      Q.b_rows = (l == 0) ? rows_d : nullptr;
+      Q.ldb = (l == 0) ? din : L.in;
+      Q.c = ctx->slabs + L.w_off;
+      Q.ldc = L.in;
+      Q.colsum = L.b_off >= 0 ? ctx->slabs + L.b_off : nullptr;
+      Q.m = L.out;
+      Q.n = L.in;
+      max_m = std::max(max_m, L.out);
+      max_n = std::max(max_n, L.in);
+    }
+    if (!np) return 0;
+    if (np == 2 && (gb.p[0].m != gb.p[1].m || gb.p[0].n != gb.p[1].n) &&
+        ((gb.p[0].m <= 32) != (gb.p[1].m <= 32) || (gb.p[0].n <= 32) != (gb.p[1].n <= 32))) {
+      GemmBatch g1 = gb;
+      g1.p[0] = gb.p[1];
+      if (int rc = run_partial(gb, 1, gb.p[0].m, gb.p[0].n, st)) return rc;
+      return run_partial(g1, 1, g1.p[0].m, g1.p[0].n, st);
+    }
+    return run_partial(gb, np, max_m, max_n, st);
+  };
+  auto input_grad = [&](int layer_from_top) -> int {
+    // dH_{l-1} = (dY_l W_l) * act'(H_{l-1}), written over H_{l-1}; l = n_hidden - layer_from_top
+    GemmBatch gb{};
+    gb.rows_n = count_d;
+    gb.act = ctx->cfg.activation;
+    int np = 0, max_n = 0, kdim = -1;
+    for (int z = 0; z < 2; ++z) {
+      NetDesc &nd = ctx->net[z];
+      const int l = nd.n_hidden - layer_from_top;
+      if (l < 1 || l >= nd.n_hidden) continue;  // head handled in the head kernel
+      const LayerDesc &L = nd.layer[l];
+      if (kdim >= 0 && kdim != L.out) {
+        if (int rc = run_rowwise<B_KN, EPI_DX>(gb, np, b, max_n, st)) return rc;
+        np = 0;
+        max_n = 0;
+      }
+      kdim = L.out;
+      GemmProblem &Q = gb.p[np++];
+      Q.a = (l == nd.n_hidden - 1) ? nd.g : nd.h[l];
+      Q.lda = L.out;
+      Q.b = ctx->params + L.w_off;
+      Q.ldb = L.in;
+      Q.c = nd.h[l - 1];
+      Q.aux = nd.h[l - 1];
+      Q.ldc = L.in;
+      Q.m = b;
+      Q.n = L.in;
+      gb.k = L.out;
+      max_n = std::max(max_n, L.in);
+    }
+    if (!np) return 0;
+    return run_rowwise<B_KN, EPI_DX>(gb, np, b, max_n, st);
+  };
+  const int depth = std::max(NA.n_hidden, NC.n_hidden);
+  for (int s = 0; s <= depth; ++s) {
+    if (int rc = partial(s)) return rc;       // dW of layer n_hidden - s (needs its input)
+    if (int rc = input_grad(s)) return rc;    // then overwrite that input with its gradient
+  }
+
+  // ---- reduce slabs -> grad, loss scalars ---------------------------------------------------
+  ReduceArgs r{};
+  int ns = 0;
+  for (int z = 0; z < 2; ++z) {
+    NetDesc &nd = ctx->net[z];
+    if (z == 0) {
+      ReduceSeg &g = r.seg[ns++];
+      g.dst = nd.logstd_off;
+      g.len = A;
+      g.src = ctx->head_part;
+      g.stride = A;
+      g.nsplit = head_splits;
+    }
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      ReduceSeg &g = r.seg[ns++];
+      g.dst = L.w_off;
+      g.len = static_cast<int64_t>(L.out) * L.in;
+      g.src = ctx->slabs + L.w_off;
+      g.stride = P;
+      g.nsplit = splits;
+      if (L.b_off >= 0) {
+        ReduceSeg &gbs = r.seg[ns++];
+        gbs.dst = L.b_off;
+        gbs.len = L.out;
+        gbs.src = ctx->slabs + L.b_off;
+        gbs.stride = P;
+        gbs.nsplit = splits;
+      }
+    }
+  }
+  r.nseg = ns;
+  r.total = P;
+  r.grad = grad_d;
+  r.loss_part = u.loss_part;
+  r.loss_splits = head_splits;
+  r.inv_b = inv_b;
+  r.logstd = ctx->params + NA.logstd_off;
+  r.act_dim = A;
+  r.ent_coef = entropy_coef;
+  r.loss_out = loss_d;
+  reduce_slabs_kernel<<<ceil_div(P, 256), 256, 0, st>>>(r);
+  PPO_LAUNCHED();
+  return 0;
+}

@@ -1,0 +1,481 @@
+// HBM-bound kernels of the PPO hot path (gfx950): GAE scan (A7/A8), per-env standardisation
+// over T (A6/A9), observation window + per-sample standardisation (A1), minibatch row maps
+// (A10), fused Adam (A15), and the synthetic-env / Philox harness kernels.
+//
+// Layout: every (N, T) rollout quantity is time-major, element (n, t) at t*N + n, so a wave of
+// 64 envs reads one 256-B row segment per timestep (coalesced), and the per-env recurrences run
+// one env per lane with no cross-lane traffic.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+namespace ppo {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ============================================================================================
+// GAE + value target (torchrl 0.6.0 generalized_advantage_estimate, ppo.py:70-80)
+// ============================================================================================
+// Per env (lane) a backward recurrence over T carried in f64:
+//   g_nt  = gamma_f * (!term)                (f32, torch: python float * int tensor)
+//   delta = ((double)r + (double)(g_nt*v')) - (double)v        (f64: reward is f64)
+//   disc  = lg_f * (!done)                   (f32, lg_f = f32(lambda*gamma in double))
+//   prev  = delta + prev * (double)disc      (f64; two roundings, no FMA)
+//   adv = (float)prev ; vtarget = adv + v    (f32)
+// Loads are issued a chunk of CH timesteps ahead of the dependent chain so the scan is bound by
+// HBM latency/bandwidth rather than by one load per dependent step.
+template <typename RT, int CH>
+__global__ __launch_bounds__(64) void gae_kernel(const float *__restrict__ value,
+                                                 const float *__restrict__ next_value,
+                                                 const RT *__restrict__ reward,
+                                                 const uint8_t *__restrict__ done,
+                                                 const uint8_t *__restrict__ term, int force_last,
+                                                 int n, int t_len, float gamma_f, float lg_f,
+                                                 float *__restrict__ adv,
+                                                 float *__restrict__ vtarget) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n) return;
+  double prev = 0.0;
+  int t_hi = t_len;  // process chunks [t_hi-CH, t_hi) from the end
+  while (t_hi > 0) {
+    const int t_lo = t_hi - CH > 0 ? t_hi - CH : 0;
+    const int cnt = t_hi - t_lo;
+    float v[CH], vn[CH];
+    RT r[CH];
+    uint8_t dn[CH], tm[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (i < cnt) {
+        const int64_t idx = static_cast<int64_t>(t_lo + i) * n + env;
+        v[i] = value[idx];
+        vn[i] = next_value[idx];
+        r[i] = reward[idx];
+        tm[i] = term[idx];
+        dn[i] = done ? done[idx] : tm[i];
+      }
+    }
+#pragma unroll
+    for (int i = CH - 1; i >= 0; --i) {
+      if (i < cnt) {
+        const int t = t_lo + i;
+        const bool is_done = dn[i] != 0 || (force_last && t == t_len - 1);
+        const float g_nt = gamma_f * (tm[i] ? 0.f : 1.f);
+        const float gv = g_nt * vn[i];
+        const double delta = (static_cast<double>(r[i]) + static_cast<double>(gv)) -
+                             static_cast<double>(v[i]);
+        const float disc = lg_f * (is_done ? 0.f : 1.f);
+        prev = delta + prev * static_cast<double>(disc);
+        const float a = static_cast<float>(prev);
+        const int64_t idx = static_cast<int64_t>(t) * n + env;
+        adv[idx] = a;
+        vtarget[idx] = a + v[i];
+      }
+    }
+    t_hi = t_lo;
+  }
+}
+
+// ============================================================================================
+// Per-env standardisation over T (ppo.py:66-69 rewards f64, :81-88 advantage / value target f32)
+// x <- ((x - mean_T) / std_T) * scale, unbiased std.  torch computes mean in the tensor dtype and
+// std with a double Welford accumulator; we accumulate both in f64 and round where torch rounds.
+// ============================================================================================
+template <typename T>
+__global__ __launch_bounds__(64) void normalize_rows_kernel(T *__restrict__ x, int n, int t_len,
+                                                            double scale) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= n) return;
+  double s = 0.0;
+  for (int t = 0; t < t_len; ++t) s += static_cast<double>(x[static_cast<int64_t>(t) * n + env]);
+  const T mean = static_cast<T>(s / t_len);
+  double cs = 0.0;
+  for (int t = 0; t < t_len; ++t) {
+    const T c = x[static_cast<int64_t>(t) * n + env] - mean;
+    cs += static_cast<double>(c);
+  }
+  const double cmean = cs / t_len;
+  double ss = 0.0;
+  for (int t = 0; t < t_len; ++t) {
+    const double d = static_cast<double>(x[static_cast<int64_t>(t) * n + env] - mean) - cmean;
+    ss += d * d;
+  }
+  const T stdv = static_cast<T>(sqrt(ss / (t_len - 1)));
+  const T sc = static_cast<T>(scale);
+  for (int t = 0; t < t_len; ++t) {
+    const int64_t idx = static_cast<int64_t>(t) * n + env;
+    const T c = x[idx] - mean;
+    x[idx] = (c / stdv) * sc;
+  }
+}
+
+// ============================================================================================
+// Observation window (helper.py:51-64, running_gym_sequential_vectorized.py:120-125)
+// ============================================================================================
+template <typename OT>
+__global__ void obs_window_push_kernel(double *__restrict__ window, const OT *__restrict__ obs,
+                                       const uint8_t *__restrict__ reset, int all_reset, int n,
+                                       int o, int w) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // (env, feat)
+  if (i >= static_cast<int64_t>(n) * o) return;
+  const int env = static_cast<int>(i / o);
+  const double x = static_cast<double>(obs[i]);
+  double *row = window + i * w;
+  const bool full = all_reset || (reset && reset[env]);
+  if (full) {
+    for (int k = 0; k < w; ++k) row[k] = x;
+  } else {
+    for (int k = 0; k + 1 < w; ++k) row[k] = row[k + 1];
+    row[w - 1] = x;
+  }
+}
+
+struct SliceTable {
+  int32_t edge[16];
+  int32_t count;  // number of slices
+};
+
+// One thread per (env, window slot): standardise each feature slice in f64 (mean, unbiased std,
+// std==0 -> 1), cast to f32, write permuted (N, W, O).  running_gym_sequential_vectorized.py:61-92.
+__global__ void obs_normalize_kernel(const double *__restrict__ window, float *__restrict__ state,
+                                     int n, int o, int w, SliceTable tab, int normalize) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // (env, slot)
+  if (i >= static_cast<int64_t>(n) * w) return;
+  const int env = static_cast<int>(i / w);
+  const int slot = static_cast<int>(i % w);
+  const double *src = window + static_cast<int64_t>(env) * o * w + slot;  // feature f at f*w
+  float *dst = state + (static_cast<int64_t>(env) * w + slot) * o;
+  if (!normalize) {
+    for (int f = 0; f < o; ++f) dst[f] = static_cast<float>(src[static_cast<int64_t>(f) * w]);
+    return;
+  }
+  for (int s = 0; s < tab.count; ++s) {
+    const int lo = tab.edge[s], hi = tab.edge[s + 1];
+    const int cnt = hi - lo;
+    if (cnt <= 0) continue;
+    double sum = 0.0;
+    for (int f = lo; f < hi; ++f) sum += src[static_cast<int64_t>(f) * w];
+    const double mean = sum / cnt;
+    double csum = 0.0;
+    for (int f = lo; f < hi; ++f) csum += src[static_cast<int64_t>(f) * w] - mean;
+    const double cmean = csum / cnt;
+    double ss = 0.0;
+    for (int f = lo; f < hi; ++f) {
+      const double d = (src[static_cast<int64_t>(f) * w] - mean) - cmean;
+      ss += d * d;
+    }
+    double sd = sqrt(ss / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
+    if (sd == 0.0) sd = 1.0;
+    for (int f = lo; f < hi; ++f)
+      dst[f] = static_cast<float>((src[static_cast<int64_t>(f) * w] - mean) / sd);
+  }
+}
+
+// ============================================================================================
+// Synthetic VecEnv step (harness; oracle/ppo_ref.py RefSyntheticEnv)
+// ============================================================================================
+__global__ void synthetic_env_step_kernel(const float *__restrict__ base_obs,
+                                          const float *__restrict__ base_reward,
+                                          const uint8_t *__restrict__ base_term,
+                                          const float *__restrict__ action, int n, int o, int a,
+                                          double *__restrict__ obs_out,
+                                          double *__restrict__ reward_out,
+                                          uint8_t *__restrict__ term_out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(n) * o) return;
+  const int env = static_cast<int>(i / o);
+  const int f = static_cast<int>(i % o);
+  const double act = static_cast<double>(action[static_cast<int64_t>(env) * a + (f % a)]);
+  obs_out[i] = static_cast<double>(base_obs[i]) + 0.1 * act;
+  if (f == 0) {
+    double ctrl = 0.0;
+    for (int j = 0; j < a; ++j) {
+      const double aj = static_cast<double>(action[static_cast<int64_t>(env) * a + j]);
+      ctrl = ctrl + aj * aj;
+    }
+    reward_out[env] = static_cast<double>(base_reward[env]) - 0.01 * ctrl;
+    term_out[env] = base_term[env];
+  }
+}
+
+// ============================================================================================
+// Philox4x32-10 normals (perf-mode eps; the parity mode takes host torch.randn instead)
+// ============================================================================================
+__global__ void philox_normal_kernel(uint64_t seed, uint64_t offset, float *__restrict__ out,
+                                     int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = philox_normal_at(seed, offset + static_cast<uint64_t>(i));
+}
+
+// ============================================================================================
+// Minibatch rows (ppo.py:99-106): reference flat index f = n*T + t -> storage row t*N + n
+// ============================================================================================
+__global__ void perm_to_rows_kernel(const int64_t *__restrict__ perm, int64_t start, int b,
+                                    int n_envs, int t_len, int32_t *__restrict__ rows) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= b) return;
+  const int64_t f = perm[start + j];
+  const int env = static_cast<int>(f / t_len);
+  const int t = static_cast<int>(f % t_len);
+  rows[j] = t * n_envs + env;
+}
+
+// Exact data-parallel variant: keep envs of [lo, hi) in order (block-wide scan, one block).
+__global__ __launch_bounds__(1024) void perm_to_rows_shard_kernel(
+    const int64_t *__restrict__ perm, int64_t start, int b, int n_envs, int t_len, int lo, int hi,
+    int32_t *__restrict__ rows, int32_t *__restrict__ count) {
+  __shared__ int wave_tot[16];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < b; c0 += 1024) {
+    const int j = c0 + tid;
+    int keep = 0, row = 0;
+    if (j < b) {
+      const int64_t f = perm[start + j];
+      const int env = static_cast<int>(f / t_len);
+      const int t = static_cast<int>(f % t_len);
+      keep = (env >= lo && env < hi);
+      row = t * (hi - lo) + (env - lo);  // rank-local time-major storage
+    }
+    const uint64_t mask = __ballot(keep);
+    const int before = __popcll(mask & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wid] = __popcll(mask);
+    __syncthreads();
+    int off = base_s;
+    for (int k = 0; k < wid; ++k) off += wave_tot[k];
+    if (keep) rows[off + before] = row;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int k = 0; k < 16; ++k) tot += wave_tot[k];
+      base_s += tot;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *count = base_s;
+}
+
+// Perf-mode shuffle: 4-round Feistel bijection on [0, 4^h) with cycle walking into [0, NT).
+__device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t k) {
+  x ^= k;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ void feistel_rows_kernel(uint64_t seed, uint64_t epoch, int64_t start, int b,
+                                    int n_envs, int t_len, int half_bits,
+                                    int32_t *__restrict__ rows) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= b) return;
+  const uint32_t total = static_cast<uint32_t>(n_envs) * static_cast<uint32_t>(t_len);
+  const uint32_t hmask = (1u << half_bits) - 1u;
+  uint32_t k[4];
+  for (int r = 0; r < 4; ++r)
+    k[r] = mix32(static_cast<uint32_t>(seed) ^ (0x9E3779B9u * (r + 1)),
+                 static_cast<uint32_t>(seed >> 32) + static_cast<uint32_t>(epoch) * 0x85EBCA6Bu);
+  uint32_t x = static_cast<uint32_t>(start + j);
+  do {
+    uint32_t l = x >> half_bits, rr = x & hmask;
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t nl = rr;
+      rr = l ^ (mix32(rr, k[r]) & hmask);
+      l = nl;
+    }
+    x = (l << half_bits) | rr;
+  } while (x >= total);
+  const int env = static_cast<int>(x / t_len);
+  const int t = static_cast<int>(x % t_len);
+  rows[j] = t * n_envs + env;
+}
+
+// ============================================================================================
+// Fused Adam (torch.optim.Adam single-tensor CPU path, adam.py _single_tensor_adam)
+//   m = lerp(m, g, 1-b1)          -> vectorised lerp: fma(w, g-m, m) for w < 0.5
+//   v = v*b2 + ((1-b2)*g)*g       -> mul_ then addcmul_ (value*t1*t2, no FMA)
+//   denom = sqrt(v)/bc2_sqrt + eps
+//   p = p + (neg_step*m)/denom    -> addcdiv_ (value*t1/t2)
+// ============================================================================================
+__global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
+                            float *__restrict__ m, float *__restrict__ v, int64_t n,
+                            int64_t n_actor, float neg_step_a, float neg_step_c, float w1,
+                            float b2, float omb2, float bc2_sqrt, float eps) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  float mi = m[i];
+  mi = (w1 < 0.5f) ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.f, gi - mi, gi);
+  float vi = v[i] * b2;
+  vi = vi + (omb2 * gi) * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  const float ns = (i < n_actor) ? neg_step_a : neg_step_c;
+  p[i] = p[i] + (ns * mi) / denom;
+  m[i] = mi;
+  v[i] = vi;
+}
+
+}  // namespace ppo
+
+// ==============================================================================================
+// C-ABI entry points
+// ==============================================================================================
+using namespace ppo;
+
+extern "C" int ppo_abi_version(void) { return PPO_ABI_VERSION; }
+
+extern "C" const char *ppo_last_error(void) { return g_err; }
+
+extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const void *reward_d,
+                       int reward_is_f64, const uint8_t *done_d, const uint8_t *terminated_d,
+                       int force_last_done, int n, int t, double gamma, double lmbda,
+                       float *adv_d, float *vtarget_d, void *stream) {
+  PPO_REQUIRE(value_d && next_value_d && reward_d && terminated_d && adv_d && vtarget_d,
+              "ppo_gae: null buffer");
+  PPO_REQUIRE(n > 0 && t > 0, "ppo_gae: bad shape n=%d t=%d", n, t);
+  const float gamma_f = static_cast<float>(gamma);
+  const float lg_f = static_cast<float>(lmbda * gamma);
+  const int grid = ceil_div(n, 64);
+  if (reward_is_f64)
+    gae_kernel<double, 16><<<grid, 64, 0, as_stream(stream)>>>(
+        value_d, next_value_d, static_cast<const double *>(reward_d), done_d, terminated_d,
+        force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+  else
+    gae_kernel<float, 16><<<grid, 64, 0, as_stream(stream)>>>(
+        value_d, next_value_d, static_cast<const float *>(reward_d), done_d, terminated_d,
+        force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_normalize_rows(void *x_d, int is_f64, int n, int t, double scale,
+                                  void *stream) {
+  PPO_REQUIRE(x_d && n > 0 && t > 0, "ppo_normalize_rows: bad args");
+  const int grid = ceil_div(n, 64);
+  if (is_f64)
+    normalize_rows_kernel<double><<<grid, 64, 0, as_stream(stream)>>>(static_cast<double *>(x_d),
+                                                                      n, t, scale);
+  else
+    normalize_rows_kernel<float><<<grid, 64, 0, as_stream(stream)>>>(static_cast<float *>(x_d), n,
+                                                                     t, scale);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_obs_window_push(double *window_d, const void *obs_d, int obs_is_f64,
+                                   const uint8_t *reset_d, int all_reset, int n, int o, int w,
+                                   void *stream) {
+  PPO_REQUIRE(window_d && obs_d && n > 0 && o > 0 && w > 0, "ppo_obs_window_push: bad args");
+  const int64_t total = static_cast<int64_t>(n) * o;
+  const int grid = ceil_div(total, 256);
+  if (obs_is_f64)
+    obs_window_push_kernel<double><<<grid, 256, 0, as_stream(stream)>>>(
+        window_d, static_cast<const double *>(obs_d), reset_d, all_reset, n, o, w);
+  else
+    obs_window_push_kernel<float><<<grid, 256, 0, as_stream(stream)>>>(
+        window_d, static_cast<const float *>(obs_d), reset_d, all_reset, n, o, w);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_obs_normalize(const double *window_d, float *state_d, int n, int o, int w,
+                                 const int32_t *bounds, int n_bounds, int normalize,
+                                 void *stream) {
+  PPO_REQUIRE(window_d && state_d && n > 0 && o > 0 && w > 0, "ppo_obs_normalize: bad args");
+  PPO_REQUIRE(n_bounds >= 0 && n_bounds < 16, "ppo_obs_normalize: too many slices (%d)",
+              n_bounds);
+  SliceTable tab{};
+  tab.count = n_bounds;
+  for (int i = 0; i <= n_bounds && normalize; ++i) {
+    PPO_REQUIRE(bounds != nullptr, "ppo_obs_normalize: null bounds");
+    tab.edge[i] = bounds[i];
+    PPO_REQUIRE(bounds[i] >= 0 && bounds[i] <= o && (i == 0 || bounds[i] >= bounds[i - 1]),
+                "ppo_obs_normalize: bounds must be ascending within [0, O]");
+  }
+  const int64_t total = static_cast<int64_t>(n) * w;
+  obs_normalize_kernel<<<ceil_div(total, 128), 128, 0, as_stream(stream)>>>(window_d, state_d, n,
+                                                                            o, w, tab, normalize);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_synthetic_env_step(const float *base_obs_d, const float *base_reward_d,
+                                      const uint8_t *base_term_d, const float *action_d, int n,
+                                      int o, int a, double *obs_out_d, double *reward_out_d,
+                                      uint8_t *term_out_d, void *stream) {
+  PPO_REQUIRE(base_obs_d && base_reward_d && base_term_d && action_d && obs_out_d &&
+                  reward_out_d && term_out_d && n > 0 && o > 0 && a > 0,
+              "ppo_synthetic_env_step: bad args");
+  const int64_t total = static_cast<int64_t>(n) * o;
+  synthetic_env_step_kernel<<<ceil_div(total, 256), 256, 0, as_stream(stream)>>>(
+      base_obs_d, base_reward_d, base_term_d, action_d, n, o, a, obs_out_d, reward_out_d,
+      term_out_d);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, int64_t n,
+                                 void *stream) {
+  PPO_REQUIRE(out_d && n >= 0, "ppo_philox_normal: bad args");
+  if (n == 0) return 0;
+  philox_normal_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(seed, offset, out_d, n);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_perm_to_rows(const int64_t *perm_d, int64_t start, int b, int n_envs, int t,
+                                int shard_lo, int shard_hi, int32_t *rows_d, int32_t *count_d,
+                                void *stream) {
+  PPO_REQUIRE(perm_d && rows_d && b > 0 && n_envs > 0 && t > 0, "ppo_perm_to_rows: bad args");
+  PPO_REQUIRE(static_cast<int64_t>(n_envs) * t < (1ll << 31), "ppo_perm_to_rows: N*T overflows");
+  if (shard_lo < shard_hi) {
+    PPO_REQUIRE(count_d && shard_lo >= 0 && shard_hi <= n_envs,
+                "ppo_perm_to_rows: bad shard [%d, %d)", shard_lo, shard_hi);
+    perm_to_rows_shard_kernel<<<1, 1024, 0, as_stream(stream)>>>(perm_d, start, b, n_envs, t,
+                                                                 shard_lo, shard_hi, rows_d,
+                                                                 count_d);
+  } else {
+    perm_to_rows_kernel<<<ceil_div(b, 256), 256, 0, as_stream(stream)>>>(perm_d, start, b, n_envs,
+                                                                         t, rows_d);
+  }
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_feistel_rows(uint64_t seed, uint64_t epoch, int64_t start, int b, int n_envs,
+                                int t, int32_t *rows_d, void *stream) {
+  PPO_REQUIRE(rows_d && b > 0 && n_envs > 0 && t > 0, "ppo_feistel_rows: bad args");
+  const int64_t total = static_cast<int64_t>(n_envs) * t;
+  PPO_REQUIRE(total < (1ll << 30), "ppo_feistel_rows: N*T too large");
+  PPO_REQUIRE(start >= 0 && start + b <= total, "ppo_feistel_rows: slice out of range");
+  int bits = 1;
+  while ((1ll << bits) < total) ++bits;
+  const int half = (bits + 1) / 2;
+  feistel_rows_kernel<<<ceil_div(b, 256), 256, 0, as_stream(stream)>>>(seed, epoch, start, b,
+                                                                       n_envs, t, half, rows_d);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n,
+                        int64_t n_actor, float neg_step_actor, float neg_step_critic,
+                        float one_minus_beta1, float beta2, float one_minus_beta2, float bc2_sqrt,
+                        float eps, void *stream) {
+  PPO_REQUIRE(p_d && g_d && m_d && v_d && n > 0 && n_actor >= 0 && n_actor <= n,
+              "ppo_adam: bad args");
+  adam_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
+      p_d, g_d, m_d, v_d, n, n_actor, neg_step_actor, neg_step_critic, one_minus_beta1, beta2,
+      one_minus_beta2, bc2_sqrt, eps);
+  PPO_LAUNCHED();
+  return 0;
+}

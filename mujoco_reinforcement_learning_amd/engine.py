@@ -1,0 +1,251 @@
+"""Torch-tensor front end of the C-ABI: ``Engine`` owns one ``ppo_ctx`` per (process, GPU).
+
+Every call launches on ``torch.cuda.current_stream()`` and validates shapes/dtypes on the host
+before handing raw pointers to the library (include/ppo_engine.h); errors surface as
+``EngineError`` (a RuntimeError) carrying ``ppo_last_error()``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+HUMANOID_SLICE_EDGES = (0, 22, 45, 175, 253, 270)  # running_gym_sequential_vectorized.py:70-80
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _need(t: torch.Tensor, name: str, dtype=None, shape=None, device=None):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise RuntimeError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return t
+
+
+def slice_edges(obs_dim: int) -> list:
+    """The reference's Humanoid slices clipped to O, as ascending edges (python slice semantics)."""
+    edges = [min(e, obs_dim) for e in HUMANOID_SLICE_EDGES] + [obs_dim]
+    return edges
+
+
+class Engine:
+    """One ``ppo_ctx``: network shapes + activation workspace + split-K slabs on one GPU."""
+
+    def __init__(self, obs_dim: int, window: int, act_dim: int, actor_hidden: Sequence[int],
+                 critic_hidden: Sequence[int], activation: str = "relu",
+                 actor_use_bias: bool = True, output_max_value: float = 1.0,
+                 max_rows: int = 65536, device: Optional[torch.device] = None):
+        self.lib = _lib.load()
+        if activation not in _lib.ACT_CODES:
+            raise ValueError(f"unsupported activation {activation!r}; use one of "
+                             f"{sorted(_lib.ACT_CODES)}")
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        cfg = _lib.NetCfg()
+        cfg.obs_dim, cfg.window, cfg.act_dim = obs_dim, window, act_dim
+        cfg.activation = _lib.ACT_CODES[activation]
+        cfg.actor_use_bias = int(bool(actor_use_bias))
+        cfg.n_actor_hidden = len(actor_hidden)
+        cfg.n_critic_hidden = len(critic_hidden)
+        for i, h in enumerate(actor_hidden):
+            cfg.actor_hidden[i] = int(h)
+        for i, h in enumerate(critic_hidden):
+            cfg.critic_hidden[i] = int(h)
+        cfg.output_max_value = float(output_max_value)
+        cfg.max_rows = int(max_rows)
+        self.cfg = cfg
+        self.obs_dim, self.window, self.act_dim = obs_dim, window, act_dim
+        self.in_dim = obs_dim * window
+        self.max_rows = int(max_rows)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib.ppo_ctx_create(ctypes.byref(cfg), self.device.index or 0,
+                                          ctypes.byref(handle)))
+        self._ctx = handle
+        self.n_actor = int(self.lib.ppo_param_count(self._ctx, 0))
+        self.n_critic = int(self.lib.ppo_param_count(self._ctx, 1))
+        self.n_params = int(self.lib.ppo_param_count(self._ctx, -1))
+        self._params = None
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self.lib.ppo_ctx_destroy(ctx)
+            except Exception:  # interpreter shutdown
+                pass
+            self._ctx = None
+
+    # ---- parameters ----------------------------------------------------------------------
+    def bind(self, flat_params: torch.Tensor) -> None:
+        _need(flat_params, "flat_params", torch.float32, (self.n_params,), self.device)
+        check(self.lib.ppo_bind_params(self._ctx, ptr(flat_params)))
+        self._params = flat_params
+
+    # ---- A2-A4 ---------------------------------------------------------------------------
+    def policy_step(self, state: torch.Tensor, eps: Optional[torch.Tensor] = None, seed: int = 0,
+                    offset: int = 0, action=None, logp=None, value=None, mean=None) -> None:
+        n = state.shape[0]
+        _need(state, "state", torch.float32, device=self.device)
+        if state.numel() != n * self.in_dim:
+            raise RuntimeError(f"state has {state.numel() // max(n, 1)} features per row, "
+                               f"expected W*O={self.in_dim}")
+        if eps is not None:
+            _need(eps, "eps", torch.float32, (n, self.act_dim), self.device)
+        for name, t, shp in (("action", action, (n, self.act_dim)), ("logp", logp, (n,)),
+                             ("value", value, (n,)), ("mean", mean, (n, self.act_dim))):
+            if t is not None:
+                _need(t, name, torch.float32, device=self.device)
+                if t.numel() != n * (shp[1] if len(shp) == 2 else 1):
+                    raise RuntimeError(f"{name} has {t.numel()} elements, expected shape {shp}")
+        check(self.lib.ppo_policy_step(self._ctx, ptr(state), n, ptr(eps), seed, offset,
+                                       ptr(action), ptr(logp), ptr(value), ptr(mean),
+                                       _stream(self.device)))
+
+    # ---- A11-A13 -------------------------------------------------------------------------
+    def minibatch_grad(self, states, actions, old_logp, adv, vtarget, rows, b: int, grad, loss,
+                       clip_lo: float, clip_hi: float, entropy_coef: float, inv_b: float,
+                       inv_ba: float, count: Optional[torch.Tensor] = None) -> None:
+        _need(rows, "rows", torch.int32, device=self.device)
+        _need(grad, "grad", torch.float32, (self.n_params,), self.device)
+        _need(loss, "loss", torch.float32, device=self.device)
+        if loss.numel() != 2:
+            raise RuntimeError("loss must hold 2 floats")
+        check(self.lib.ppo_minibatch_grad(
+            self._ctx, ptr(states), ptr(actions), ptr(old_logp), ptr(adv), ptr(vtarget),
+            ptr(rows), int(b), ptr(count), clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
+            ptr(grad), ptr(loss), _stream(self.device)))
+
+
+# ==============================================================================================
+# Context-free kernels
+# ==============================================================================================
+def gae(value, next_value, reward, terminated, gamma: float, lmbda: float, adv, vtarget,
+        done=None, force_last_done: bool = True) -> None:
+    """A7/A8 on time-major (T, N) arrays (torchrl GAE semantics, f64 carry)."""
+    lib = _lib.load()
+    t, n = value.shape[0], value.shape[1]
+    dev = value.device
+    _need(value, "value", torch.float32, (t, n))
+    _need(next_value, "next_value", torch.float32, (t, n), dev)
+    if reward.dtype not in (torch.float32, torch.float64):
+        raise ValueError("reward must be f32 or f64")
+    _need(reward, "reward", None, (t, n), dev)
+    _need(terminated, "terminated", None, (t, n), dev)
+    if terminated.dtype not in (torch.bool, torch.uint8):
+        raise ValueError("terminated must be bool/uint8")
+    if done is not None:
+        _need(done, "done", None, (t, n), dev)
+    _need(adv, "adv", torch.float32, (t, n), dev)
+    _need(vtarget, "vtarget", torch.float32, (t, n), dev)
+    check(lib.ppo_gae(ptr(value), ptr(next_value), ptr(reward), int(reward.dtype == torch.float64),
+                      ptr(done), ptr(terminated), int(force_last_done), n, t, float(gamma),
+                      float(lmbda), ptr(adv), ptr(vtarget), _stream(dev)))
+
+
+def normalize_rows(x: torch.Tensor, scale: float = 1.0) -> None:
+    """A6/A9: per-env (column of a time-major (T, N) array) standardisation over T, in place."""
+    lib = _lib.load()
+    if x.dtype not in (torch.float32, torch.float64):
+        raise ValueError("x must be f32 or f64")
+    _need(x, "x")
+    t, n = x.shape[0], x.shape[1]
+    check(lib.ppo_normalize_rows(ptr(x), int(x.dtype == torch.float64), n, t, float(scale),
+                                 _stream(x.device)))
+
+
+def obs_window_push(window: torch.Tensor, obs: torch.Tensor, reset: Optional[torch.Tensor] = None,
+                    all_reset: bool = False) -> None:
+    lib = _lib.load()
+    n, o, w = window.shape
+    _need(window, "window", torch.float64)
+    if obs.dtype not in (torch.float32, torch.float64):
+        raise ValueError("obs must be f32 or f64")
+    _need(obs, "obs", None, (n, o), window.device)
+    if reset is not None:
+        _need(reset, "reset", None, (n,), window.device)
+    check(lib.ppo_obs_window_push(ptr(window), ptr(obs), int(obs.dtype == torch.float64),
+                                  ptr(reset), int(all_reset), n, o, w, _stream(window.device)))
+
+
+def obs_normalize(window: torch.Tensor, state: torch.Tensor, normalize: bool = True) -> None:
+    lib = _lib.load()
+    n, o, w = window.shape
+    _need(window, "window", torch.float64)
+    _need(state, "state", torch.float32, device=window.device)
+    if state.numel() != n * w * o:
+        raise RuntimeError(f"state must hold (N, W, O) = {(n, w, o)} floats")
+    edges = slice_edges(o)
+    arr = (ctypes.c_int32 * len(edges))(*edges)
+    check(lib.ppo_obs_normalize(ptr(window), ptr(state), n, o, w, arr, len(edges) - 1,
+                                int(normalize), _stream(window.device)))
+
+
+def perm_to_rows(perm: torch.Tensor, start: int, b: int, n_envs: int, horizon: int,
+                 rows: torch.Tensor, shard: Optional[tuple] = None,
+                 count: Optional[torch.Tensor] = None) -> None:
+    lib = _lib.load()
+    _need(perm, "perm", torch.int64)
+    _need(rows, "rows", torch.int32, device=perm.device)
+    lo, hi = shard if shard is not None else (0, 0)
+    check(lib.ppo_perm_to_rows(ptr(perm), int(start), int(b), n_envs, horizon, lo, hi, ptr(rows),
+                               ptr(count), _stream(perm.device)))
+
+
+def feistel_rows(seed: int, epoch: int, start: int, b: int, n_envs: int, horizon: int,
+                 rows: torch.Tensor) -> None:
+    lib = _lib.load()
+    _need(rows, "rows", torch.int32)
+    check(lib.ppo_feistel_rows(seed, epoch, int(start), int(b), n_envs, horizon, ptr(rows),
+                               _stream(rows.device)))
+
+
+def adam(p, g, m, v, n_actor: int, neg_step_actor: float, neg_step_critic: float,
+         one_minus_beta1: float, beta2: float, one_minus_beta2: float, bc2_sqrt: float,
+         eps: float) -> None:
+    lib = _lib.load()
+    n = p.numel()
+    for name, t in (("p", p), ("g", g), ("m", m), ("v", v)):
+        _need(t, name, torch.float32, (n,), p.device)
+    check(lib.ppo_adam(ptr(p), ptr(g), ptr(m), ptr(v), n, int(n_actor), neg_step_actor,
+                       neg_step_critic, one_minus_beta1, beta2, one_minus_beta2, bc2_sqrt, eps,
+                       _stream(p.device)))
+
+
+def synthetic_env_step(base_obs, base_reward, base_term, action, obs_out, reward_out,
+                       term_out) -> None:
+    lib = _lib.load()
+    n, o = base_obs.shape
+    a = action.shape[1]
+    dev = base_obs.device
+    _need(base_obs, "base_obs", torch.float32)
+    _need(base_reward, "base_reward", torch.float32, (n,), dev)
+    _need(base_term, "base_term", None, (n,), dev)
+    _need(action, "action", torch.float32, (n, a), dev)
+    _need(obs_out, "obs_out", torch.float64, (n, o), dev)
+    _need(reward_out, "reward_out", torch.float64, (n,), dev)
+    _need(term_out, "term_out", None, (n,), dev)
+    check(lib.ppo_synthetic_env_step(ptr(base_obs), ptr(base_reward), ptr(base_term), ptr(action),
+                                     n, o, a, ptr(obs_out), ptr(reward_out), ptr(term_out),
+                                     _stream(dev)))
+
+
+def philox_normal(seed: int, offset: int, out: torch.Tensor) -> None:
+    lib = _lib.load()
+    _need(out, "out", torch.float32)
+    check(lib.ppo_philox_normal(seed, offset, ptr(out), out.numel(), _stream(out.device)))

@@ -1,0 +1,145 @@
+"""VecEnv side of the drop-in: the ``EnvironmentHelper`` surface (helper.py:12-67,
+running_gym_sequential_vectorized.py:19-100) over device-resident state.
+
+``SyntheticVecEnvHelper`` is the benchmark / test environment.  MuJoCo physics is outside the hot
+path; the harness drives the loop with synthetic dynamics whose next observation
+depends on the action (so the T rollout steps stay sequential):
+
+    obs'      = base_obs[t+1] + 0.1 * a[:, o % A]            (f64)
+    reward    = base_reward[t] - 0.01 * sum_a a^2            (f64, a summed in order)
+    terminated = base_terminated[t]
+
+The observation window (N, O, W) f64 and its per-sample standardisation are the reference's
+(``timestep.observation`` + ``get_state``), computed by the engine's A1 kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from types import SimpleNamespace
+from typing import Optional
+
+import torch
+
+from . import engine as E
+from .features import Run
+
+
+@dataclass
+class Timestep:
+    """entities/timestep.py:5-11 with device tensors."""
+    observation: torch.Tensor
+    reward: torch.Tensor
+    terminated: torch.Tensor
+    truncated: torch.Tensor
+    info: dict = field(default_factory=dict)
+
+
+def make_synthetic_streams(num_envs: int, horizon: int, obs_dim: int, seed: int = 0,
+                           p_terminate: float = 0.0, device=None) -> dict:
+    """Seeded base streams: obs ~ N(0,1) (T+1, N, O) f32, reward ~ U(-1,1) (T, N) f32,
+    terminated ~ Bernoulli(p) (T, N) bool.  ``device='cuda'`` draws on the GPU generator (bench
+    inputs; not the CPU stream the parity tests use)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    g = torch.Generator(device=dev).manual_seed(seed)
+    base_obs = torch.randn(horizon + 1, num_envs, obs_dim, generator=g, device=dev)
+    base_reward = torch.rand(horizon, num_envs, generator=g, device=dev) * 2 - 1
+    base_term = torch.rand(horizon, num_envs, generator=g, device=dev) < p_terminate
+    return {"base_obs": base_obs, "base_reward": base_reward, "base_terminated": base_term}
+
+
+class SyntheticVecEnvHelper:
+    """EnvironmentHelper over the synthetic device VecEnv."""
+
+    writes_into_buffer = True  # step(reward_out=, terminated_out=) / get_state(out=)
+
+    def __init__(self, streams: Optional[dict] = None, run: Optional[Run] = None,
+                 device: Optional[torch.device] = None, seed: int = 0, p_terminate: float = 0.0):
+        self.rewards = []
+        self.memory = []
+        self.images = []
+        self.run = run or Run.instance()
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self._streams = streams
+        self._seed = seed
+        self._p_terminate = p_terminate
+        self.initialize()
+        self.environment.timestep = self.timestep
+        self.test_environment.timestep = self.test_timestep
+
+    def initialize(self):
+        ec, nc = self.run.environment_config, self.run.network_config
+        n, t, o, w = ec.num_envs, ec.maximum_timesteps, nc.input_shape, ec.window_length
+        self.num_envs, self.horizon, self.obs_dim, self.window = n, t, o, w
+        streams = self._streams or make_synthetic_streams(n, t, o, self._seed, self._p_terminate)
+        dev = self.device
+        self.base_obs = streams["base_obs"].to(dev, torch.float32).contiguous()
+        self.base_reward = streams["base_reward"].to(dev, torch.float32).contiguous()
+        self.base_terminated = streams["base_terminated"].to(dev, torch.bool).contiguous()
+        if self.base_obs.shape[0] < t + 1 or self.base_reward.shape[0] < t:
+            raise ValueError("synthetic streams shorter than the horizon")
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.timestep = Timestep(torch.zeros(n, o, w, **f64), torch.zeros(n, **f64),
+                                 torch.zeros(n, dtype=torch.bool, device=dev),
+                                 torch.zeros(n, dtype=torch.bool, device=dev), {})
+        self.test_timestep = Timestep(torch.zeros(1, o, w, **f64), torch.zeros(1, **f64),
+                                      torch.zeros(1, dtype=torch.bool, device=dev),
+                                      torch.zeros(1, dtype=torch.bool, device=dev), {})
+        self.environment = SimpleNamespace(num_envs=n)
+        self.test_environment = SimpleNamespace(num_envs=1)
+        self._obs_next = torch.empty(n, o, **f64)
+        self.t = 0
+
+    # ---- EnvironmentHelper API -------------------------------------------------------------
+    def reset(self, release_memory: bool = True):
+        self.rewards = []
+        if release_memory:
+            self.memory = []
+        self.images = []
+
+    def reset_environment(self, test_phase: bool):
+        """helper.py:59-64 + running_gym_sequential_vectorized.py:161-167."""
+        if test_phase:
+            E.obs_window_push(self.test_timestep.observation, self.base_obs[0, :1].contiguous(),
+                              all_reset=True)
+            self.test_timestep.terminated.zero_()
+            self.test_timestep.truncated.zero_()
+            return
+        self.t = 0
+        E.obs_window_push(self.timestep.observation, self.base_obs[0], all_reset=True)
+        self.timestep.terminated.zero_()
+        self.timestep.truncated.zero_()
+
+    def step(self, action: torch.Tensor, reward_out: Optional[torch.Tensor] = None,
+             terminated_out: Optional[torch.Tensor] = None):
+        """Training-phase step of all N envs (running_gym_sequential_vectorized.py:107-126).
+        ``reward_out`` / ``terminated_out`` let the engine land the outputs straight in its
+        rollout buffer."""
+        t = self.t
+        if t >= self.horizon:
+            raise RuntimeError("synthetic VecEnv: horizon exhausted; call reset_environment()")
+        reward = reward_out if reward_out is not None else self.timestep.reward
+        term = terminated_out if terminated_out is not None else self.timestep.terminated
+        E.synthetic_env_step(self.base_obs[t + 1], self.base_reward[t], self.base_terminated[t],
+                             action.contiguous(), self._obs_next, reward, term)
+        E.obs_window_push(self.timestep.observation, self._obs_next, reset=term)
+        self.timestep.reward = reward
+        self.timestep.terminated = term
+        self.t = t + 1
+
+    def get_state(self, test_phase: bool = False, out: Optional[torch.Tensor] = None):
+        """(N, W, O) ``Run.dtype`` state (running_gym_sequential_vectorized.py:150-159)."""
+        ts = self.test_timestep if test_phase else self.timestep
+        n, o, w = ts.observation.shape
+        if out is None:
+            out = torch.empty(n, w, o, dtype=torch.float32, device=self.device)
+        E.obs_normalize(ts.observation, out, normalize=self.run.normalize_observations)
+        return out.view(n, w, o)
+
+    def shift_observations(self, test_phase: bool, environment_index: int):
+        ts = self.test_timestep if test_phase else self.timestep
+        if test_phase:
+            ts.observation[..., :-1] = ts.observation[..., 1:].clone()
+        else:
+            ts.observation[environment_index, :, :-1] = ts.observation[environment_index, :,
+                                                                       1:].clone()
