@@ -1,0 +1,215 @@
+#!/usr/bin/env python
+"""bench.py -- env-steps/sec of the PPO iteration on N MI355X GPUs (BASELINE.json metric).
+
+One "step" = one full PPO iteration of the hot path on each rank: T=128 sequential rollout steps
+over N=4096 synthetic envs (device dynamics + obs standardisation + actor/critic forward +
+sampling + log-prob), GAE + value targets, then E=10 epochs x 8 minibatches of 65,536 rows
+(actor/critic forward + loss + backward + fused Adam; for N_gpus > 1 one RCCL all-reduce of the
+flat gradient per optimizer step).  Inputs are resident in HBM before timing starts.
+value = N_gpus * 4096 * 128 * steps / max-over-ranks wall time (weak scaling: envs per GPU fixed).
+
+Also reported on the same JSON line:
+  roofline      dominant kernel class from HIP events recorded live in the timed region
+                (algorithmic FLOPs or bytes per launch / mean launch time vs the MI355X peak)
+  gae_roofline  the GAE scan (north-star >= 40 % HBM target), events around its launch
+  cpu_baseline  the oracle (oracle/ppo_ref.py, torch-CPU restatement of ppo.py) on a bounded
+                sample of the same workload, on rank 0 at N_gpus = 1 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+METRIC = "env-steps/sec (whole node) HalfCheetah-v4 4096 envs at 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
+PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--num-envs", type=int, default=4096)
+    p.add_argument("--horizon", type=int, default=128)
+    p.add_argument("--obs-dim", type=int, default=17)
+    p.add_argument("--act-dim", type=int, default=6)
+    p.add_argument("--hidden", type=str, default="256,256")
+    p.add_argument("--batch", type=int, default=65536)
+    p.add_argument("--epochs", type=int, default=10)
+    p.add_argument("--rng", choices=("philox", "torch"), default="philox")
+    p.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
+    p.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    p.add_argument("--cpu-rollout-steps", type=int, default=32)
+    p.add_argument("--cpu-epochs", type=int, default=1)
+    p.add_argument("--no-timing", action="store_true", help="skip per-kernel event timing")
+    return p.parse_args()
+
+
+def cpu_baseline(args, hidden):
+    """Oracle on the host cores: rollout_steps of the T-step rollout, the full GAE, cpu_epochs of
+    the E-epoch update; extrapolated linearly to one full iteration."""
+    from oracle import ppo_ref as R
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    n, t = args.num_envs, args.horizon
+    cfg = R.RefConfig(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
+                      actor_hidden=hidden, critic_hidden=hidden, batch_size=args.batch,
+                      epochs=args.cpu_epochs)
+    g = torch.Generator().manual_seed(0)
+    env = R.RefSyntheticEnv(torch.randn(t + 1, n, args.obs_dim, generator=g),
+                            torch.rand(t, n, generator=g) * 2 - 1,
+                            torch.zeros(t, n, dtype=torch.bool), 1, args.act_dim)
+    torch.manual_seed(0)
+    agent = R.RefAgent(cfg)
+    k = min(args.cpu_rollout_steps, t)
+    cfg.horizon = k
+    t0 = time.perf_counter()
+    mem = R.rollout(env, agent)  # k steps
+    t_roll = (time.perf_counter() - t0) * (t / k)
+    cfg.horizon = t
+    # full-size buffer for GAE / update: tile the k sampled steps to T
+    reps = (t + k - 1) // k
+    full = {key: v.repeat(1, reps, *([1] * (v.dim() - 2)))[:, :t].contiguous()
+            for key, v in mem.items()}
+    t0 = time.perf_counter()
+    R.calculate_advantages(full, cfg)
+    t_gae = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    R.train(agent, full, 0)
+    t_epoch = (time.perf_counter() - t0) / args.cpu_epochs
+    t_iter = t_roll + t_gae + t_epoch * args.epochs
+    return {"value": n * t / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle/ppo_ref.py (torch {torch.__version__} CPU, {threads} threads): "
+                       f"{k} of {t} rollout steps + full GAE + {args.cpu_epochs} of {args.epochs} "
+                       f"epochs at N={n}, B={args.batch}, 2x{hidden[0]} MLP; extrapolated "
+                       f"(rollout {t_roll:.2f}s, gae {t_gae:.3f}s, epoch {t_epoch:.2f}s/iter-scaled)"),
+            "seconds_per_iteration": t_iter}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd import engine as E
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    n, t = args.num_envs, args.horizon
+    run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
+                   hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
+                   seed=rank)
+    torch.manual_seed(0)  # identical initial parameters on every rank
+    agent = PPOEngineAgent(run, device=dev)
+    streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
+    helper = SyntheticVecEnvHelper(streams, run, device=dev)
+    algo = PPOEngine(helper, agent, log=lambda m: None)
+
+    # GAE launch timing (events on the launch stream around the single GAE kernel)
+    gae_ev = []
+    orig_gae = E.gae
+
+    def timed_gae(*a, **kw):
+        if timing_on[0]:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            orig_gae(*a, **kw)
+            e.record()
+            gae_ev.append((s, e))
+        else:
+            orig_gae(*a, **kw)
+    timing_on = [False]
+    E.gae = timed_gae
+
+    for _ in range(args.warmup):
+        algo._iterate()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    if not args.no_timing:
+        agent.engine.timing(True, capacity=200000)
+        timing_on[0] = True
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        algo._iterate()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt)
+    timing_on[0] = False
+    classes = agent.engine.timing_read() if not args.no_timing else {}
+    agent.engine.timing(False)
+
+    value = world * n * t * args.steps / elapsed
+    line = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",
+            "config": {"workload": (f"HalfCheetah-v4 shapes: {n} envs/GPU x {t} steps, obs "
+                                    f"{args.obs_dim}, act {args.act_dim}, actor+critic "
+                                    f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
+                                    f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
+                       "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
+                       "epochs": args.epochs, "rng": args.rng,
+                       "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
+    if classes:
+        dom = max(classes.items(), key=lambda kv: kv[1]["ms"])
+        name, c = dom
+        avg_ms = c["ms"] / max(c["launches"], 1)
+        mfma = name.startswith("gemm")
+        if mfma:
+            achieved = c["flops"] / c["launches"] / (avg_ms * 1e-3) / 1e12
+            peak, unit = PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        else:
+            achieved = c["bytes"] / c["launches"] / (avg_ms * 1e-3) / 1e9
+            peak, unit = PEAK_HBM_GBS, "GB/s"
+        line["roofline"] = {"bound": "mfma" if mfma else "hbm", "kernel": name,
+                            "achieved": achieved, "peak": peak, "unit": unit,
+                            "frac": achieved / peak, "traffic": None,
+                            "avg_launch_us": avg_ms * 1e3, "launches": c["launches"]}
+        line["kernel_classes_ms_per_step"] = {k: v["ms"] / args.steps for k, v in classes.items()}
+    if gae_ev:
+        gms = sum(s.elapsed_time(e) for s, e in gae_ev) / len(gae_ev)
+        # algorithmic bytes/element: read V 4 + V' 4 + reward 8 (f64) + terminated 1 (done is
+        # derived in-kernel), write adv 4 + vtarget 4 = 25 B
+        gbytes = 25.0 * n * t
+        ach = gbytes / (gms * 1e-3) / 1e9
+        line["gae_roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                                "avg_launch_us": gms * 1e3, "bytes_per_launch": gbytes}
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, hidden)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

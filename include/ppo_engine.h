@@ -149,6 +149,17 @@ int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n, in
              float neg_step_actor, float neg_step_critic, float one_minus_beta1, float beta2,
              float one_minus_beta2, float bc2_sqrt, float eps, void *stream);
 
+/* ---- measurement: per-kernel-class timing (no reference counterpart; replaces @timeit,
+ * error_handling_utils.py:5-17, with device-side timing) -----------------------------------------
+ * enable=1 (re)starts recording a HIP event pair around every launch the ctx issues, on the
+ * launch's stream (up to `capacity` launches); enable=0 stops.  ppo_ctx_timing_read synchronises
+ * on the recorded events and returns per class: summed kernel ms, launches, algorithmic FLOPs and
+ * algorithmic bytes.  kclass < 0 returns the number of classes. */
+int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity);
+int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
+                        double *flops, double *bytes);
+const char *ppo_kernel_class_name(int kclass);
+
 /* ---- harness: synthetic VecEnv dynamics on device + Philox normals ---------------------------
  * The bench/test environment (physics is out of scope): obs' = base_obs + 0.1*a[:, o % A],
  * r = base_r - 0.01*sum_a a^2 (f64), terminated = base_term.  obs_out (N, O) f64, reward (N,) f64,

@@ -61,6 +61,10 @@ _SIGNATURES = {
     "ppo_synthetic_env_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_philox_normal": (c_int, [c_uint64, c_uint64, c_void_p, c_int64, c_void_p]),
+    "ppo_ctx_timing": (c_int, [c_void_p, c_int, c_int]),
+    "ppo_ctx_timing_read": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64),
+                                    POINTER(c_double), POINTER(c_double)]),
+    "ppo_kernel_class_name": (ctypes.c_char_p, [c_int]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

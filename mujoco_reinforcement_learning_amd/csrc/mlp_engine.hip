@@ -514,6 +514,51 @@ struct NetDesc {
   float *dz;                            // workspace: head pre-activation grads (max_rows, out)
 };
 
+// ============================================================================================
+// Per-kernel-class timing: HIP events recorded around each launch ON the launch stream while
+// enabled (bench.py's live roofline), read back after the timed region.
+// ============================================================================================
+enum {
+  KC_GEMM_FWD = 0,
+  KC_GEMM_DGRAD,
+  KC_GEMM_WGRAD,
+  KC_UPDATE_HEAD,
+  KC_POLICY_HEAD,
+  KC_REDUCE,
+  KC_COUNT
+};
+static const char *const kClassNames[KC_COUNT] = {"gemm_fwd",    "gemm_dgrad",  "gemm_wgrad",
+                                                  "update_head", "policy_head", "reduce_slabs"};
+
+struct Timing {
+  bool on = false;
+  int capacity = 0;
+  int used = 0;
+  hipEvent_t *ev = nullptr;  // 2 per record
+  int *cls = nullptr;
+  double *flops = nullptr, *bytes = nullptr;
+  double ms[KC_COUNT] = {}, fl[KC_COUNT] = {}, by[KC_COUNT] = {};
+  int64_t n[KC_COUNT] = {};
+};
+
+static thread_local Timing *g_tim = nullptr;  // set by the entry point for the call's duration
+
+static inline void tim_begin(hipStream_t st) {
+  Timing *t = g_tim;
+  if (t && t->used < t->capacity) (void)hipEventRecord(t->ev[2 * t->used], st);
+}
+
+static inline void tim_end(int cls, double flops, double bytes, hipStream_t st) {
+  Timing *t = g_tim;
+  if (t && t->used < t->capacity) {
+    (void)hipEventRecord(t->ev[2 * t->used + 1], st);
+    t->cls[t->used] = cls;
+    t->flops[t->used] = flops;
+    t->bytes[t->used] = bytes;
+    ++t->used;
+  }
+}
+
 }  // namespace ppo
 
 struct ppo_ctx {
@@ -525,9 +570,25 @@ struct ppo_ctx {
   float *slabs;          // (kSlabSplits, total_params)
   float *head_part;      // logstd partials (kHeadSplits, A) + loss partials (kHeadSplits, 2)
   void *arena;
+  ppo::Timing tim;
 };
 
 namespace ppo {
+
+struct TimingScope {  // routes this thread's launches to ctx->tim while timing is enabled
+  explicit TimingScope(ppo_ctx *ctx) { g_tim = ctx->tim.on ? &ctx->tim : nullptr; }
+  ~TimingScope() { g_tim = nullptr; }
+};
+
+static double gemm_flops(const GemmBatch &gb, int nprob, int epi) {
+  double f = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const GemmProblem &p = gb.p[i];
+    const double k = (epi == EPI_PARTIAL) ? gb.k : gb.k;
+    f += 2.0 * p.m * p.n * k;
+  }
+  return f;
+}
 
 constexpr int kSlabSplits = 64;
 constexpr int kHeadSplits = 512;
@@ -537,8 +598,17 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   const int tiles = ceil_div(max_m, BM) * ceil_div(max_n, BN);
   dim3 grid(tiles, EPI == EPI_PARTIAL ? gb.splits : 1, nprob);
+  tim_begin(st);
   gemm_f32_kernel<TM, TN, WM, WN, 16, AMODE, BMODE, EPI><<<grid, 64 * WM * WN, 0, st>>>(gb);
   PPO_LAUNCHED();
+  const int cls = EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD);
+  double bytes = 0;
+  for (int i = 0; i < nprob; ++i) {  // algorithmic: A + B read once, C written once (f32)
+    const GemmProblem &p = gb.p[i];
+    bytes += 4.0 * (static_cast<double>(p.m) * gb.k + static_cast<double>(gb.k) * p.n +
+                    static_cast<double>(p.m) * p.n * (EPI == EPI_DX ? 2 : 1));
+  }
+  tim_end(cls, gemm_flops(gb, nprob, EPI), bytes, st);
   return 0;
 }
 
@@ -668,7 +738,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       if (l < nh) ws_floats += static_cast<size_t>(R) * o;
       width = o;
     }
-    ws_floats += static_cast<size_t>(R) * width;  // g = dH_L
+    ws_floats += static_cast<size_t>(R) * nd.layer[nh].in;   // g = dH_L (last hidden width)
     ws_floats += static_cast<size_t>(R) * nd.layer[nh].out;  // dz
     nd.count = off - nd.begin;
   }
@@ -699,6 +769,13 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
   ctx->slabs = p;
   p += static_cast<int64_t>(kSlabSplits) * off;
   ctx->head_part = p;
+  p += static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2);
+  if (static_cast<size_t>(p - static_cast<float *>(arena)) != ws_floats) {
+    hipFree(arena);
+    delete ctx;
+    set_error("ppo_ctx_create: internal workspace carve-out mismatch");
+    return PPO_EHIP;
+  }
   ctx->params = nullptr;
   *out = ctx;
   return 0;
@@ -706,10 +783,13 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
 
 extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
   if (!ctx) return 0;
-  if (ctx->arena) {
-    hipSetDevice(ctx->device);
-    hipFree(ctx->arena);
-  }
+  (void)hipSetDevice(ctx->device);
+  for (int i = 0; i < 2 * ctx->tim.capacity; ++i) (void)hipEventDestroy(ctx->tim.ev[i]);
+  delete[] ctx->tim.ev;
+  delete[] ctx->tim.cls;
+  delete[] ctx->tim.flops;
+  delete[] ctx->tim.bytes;
+  if (ctx->arena) (void)hipFree(ctx->arena);
   delete ctx;
   return 0;
 }
@@ -734,6 +814,7 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   PPO_REQUIRE(n <= ctx->cfg.max_rows, "ppo_policy_step: n=%d exceeds max_rows=%d", n,
               ctx->cfg.max_rows);
   hipStream_t st = as_stream(stream);
+  TimingScope timing_scope(ctx);
   const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
   if (!use[0] && !use[1]) return 0;
   if (int rc = forward_hidden(ctx, use, state_d, nullptr, n, nullptr, st)) return rc;
@@ -766,10 +847,16 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   q.mean = mean_d;
   const int hpl = hpl_for(std::max(q.da, q.dc));
   const int grid = ceil_div(n, 4);
+  tim_begin(st);
   if (hpl == 4) policy_head_kernel<4><<<grid, 256, 0, st>>>(q);
   else if (hpl == 8) policy_head_kernel<8><<<grid, 256, 0, st>>>(q);
   else policy_head_kernel<16><<<grid, 256, 0, st>>>(q);
   PPO_LAUNCHED();
+  const int na = q.act_dim;
+  tim_end(KC_POLICY_HEAD, 2.0 * n * (static_cast<double>(q.da) * na + q.dc),
+          4.0 * n * (q.da + q.dc + (eps_d ? na : 0) + (action_d ? na : 0) + (mean_d ? na : 0) +
+                     (logp_d ? 1 : 0) + (value_d ? 1 : 0)),
+          st);
   return 0;
 }
 
@@ -785,6 +872,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   PPO_REQUIRE(b > 0 && b <= ctx->cfg.max_rows, "ppo_minibatch_grad: b=%d outside [1, max_rows=%d]",
               b, ctx->cfg.max_rows);
   hipStream_t st = as_stream(stream);
+  TimingScope timing_scope(ctx);
   const bool both[2] = {true, true};
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
@@ -827,10 +915,15 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   u.loss_part = ctx->head_part + static_cast<int64_t>(kHeadSplits) * A;
   u.splits = head_splits;
   const int hpl = hpl_for(std::max(u.da, u.dc));
+  tim_begin(st);
   if (hpl == 4) update_head_kernel<4><<<head_splits, 256, 0, st>>>(u);
   else if (hpl == 8) update_head_kernel<8><<<head_splits, 256, 0, st>>>(u);
   else update_head_kernel<16><<<head_splits, 256, 0, st>>>(u);
   PPO_LAUNCHED();
+  // algorithmic bytes per row: read H_L (actor, critic), action, 4 scalars + row index;
+  // write dH_L (actor, critic) and dz (A + 1)
+  tim_end(KC_UPDATE_HEAD, 2.0 * b * (3.0 * A * u.da + 3.0 * u.dc),
+          4.0 * b * (2.0 * u.da + 2.0 * u.dc + 2.0 * A + 6.0), st);
 
   // ---- weight gradients, split-K over rows, deepest layer first ---------------------------
   const int splits = std::min(kSlabSplits, std::max(1, b / 64));
@@ -953,7 +1046,61 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   r.act_dim = A;
   r.ent_coef = entropy_coef;
   r.loss_out = loss_d;
+  tim_begin(st);
   reduce_slabs_kernel<<<ceil_div(P, 256), 256, 0, st>>>(r);
   PPO_LAUNCHED();
+  tim_end(KC_REDUCE, static_cast<double>(splits) * P, 4.0 * (static_cast<double>(splits) + 1) * P,
+          st);
   return 0;
+}
+
+extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing: null ctx");
+  Timing &t = ctx->tim;
+  if (enable && capacity > t.capacity) {
+    for (int i = 0; i < 2 * t.capacity; ++i) (void)hipEventDestroy(t.ev[i]);
+    delete[] t.ev;
+    delete[] t.cls;
+    delete[] t.flops;
+    delete[] t.bytes;
+    t.ev = new hipEvent_t[2 * capacity];
+    t.cls = new int[capacity];
+    t.flops = new double[capacity];
+    t.bytes = new double[capacity];
+    for (int i = 0; i < 2 * capacity; ++i) PPO_HIP_TRY(hipEventCreate(&t.ev[i]));
+    t.capacity = capacity;
+  }
+  if (enable) {
+    t.used = 0;
+    for (int c = 0; c < KC_COUNT; ++c) t.ms[c] = t.fl[c] = t.by[c] = 0, t.n[c] = 0;
+  }
+  t.on = enable != 0 && t.capacity > 0;
+  return 0;
+}
+
+extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
+                                   double *flops, double *bytes) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_read: null ctx");
+  if (kclass < 0) return KC_COUNT;
+  PPO_REQUIRE(kclass < KC_COUNT, "ppo_ctx_timing_read: class %d out of range", kclass);
+  Timing &t = ctx->tim;
+  for (int i = 0; i < t.used; ++i) {  // fold pending records (host sync on their events)
+    PPO_HIP_TRY(hipEventSynchronize(t.ev[2 * i + 1]));
+    float ms = 0.f;
+    PPO_HIP_TRY(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
+    t.ms[t.cls[i]] += ms;
+    t.fl[t.cls[i]] += t.flops[i];
+    t.by[t.cls[i]] += t.bytes[i];
+    t.n[t.cls[i]] += 1;
+  }
+  t.used = 0;
+  if (total_ms) *total_ms = t.ms[kclass];
+  if (launches) *launches = t.n[kclass];
+  if (flops) *flops = t.fl[kclass];
+  if (bytes) *bytes = t.by[kclass];
+  return 0;
+}
+
+extern "C" const char *ppo_kernel_class_name(int kclass) {
+  return (kclass >= 0 && kclass < KC_COUNT) ? kClassNames[kclass] : "";
 }

@@ -24,11 +24,12 @@ void set_error(const char *fmt, ...) {
 // ============================================================================================
 // GAE + value target (torchrl 0.6.0 generalized_advantage_estimate, ppo.py:70-80)
 // ============================================================================================
-// Per env (lane) a backward recurrence over T carried in f64:
+// Per env (lane) a backward recurrence over T carried in the REWARD's dtype (torch promotion:
+// f64 numpy rewards make delta and prev_advantage f64; f32 rewards keep everything f32):
 //   g_nt  = gamma_f * (!term)                (f32, torch: python float * int tensor)
-//   delta = ((double)r + (double)(g_nt*v')) - (double)v        (f64: reward is f64)
+//   delta = ((RT)r + (RT)(g_nt*v')) - (RT)v
 //   disc  = lg_f * (!done)                   (f32, lg_f = f32(lambda*gamma in double))
-//   prev  = delta + prev * (double)disc      (f64; two roundings, no FMA)
+//   prev  = delta + prev * (RT)disc          (two roundings, no FMA)
 //   adv = (float)prev ; vtarget = adv + v    (f32)
 // Loads are issued a chunk of CH timesteps ahead of the dependent chain so the scan is bound by
 // HBM latency/bandwidth rather than by one load per dependent step.
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float *__restrict__ value
                                                  float *__restrict__ vtarget) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= n) return;
-  double prev = 0.0;
+  RT prev = 0;
   int t_hi = t_len;  // process chunks [t_hi-CH, t_hi) from the end
   while (t_hi > 0) {
     const int t_lo = t_hi - CH > 0 ? t_hi - CH : 0;
@@ -69,10 +70,9 @@ __global__ __launch_bounds__(64) void gae_kernel(const float *__restrict__ value
         const bool is_done = dn[i] != 0 || (force_last && t == t_len - 1);
         const float g_nt = gamma_f * (tm[i] ? 0.f : 1.f);
         const float gv = g_nt * vn[i];
-        const double delta = (static_cast<double>(r[i]) + static_cast<double>(gv)) -
-                             static_cast<double>(v[i]);
+        const RT delta = (r[i] + static_cast<RT>(gv)) - static_cast<RT>(v[i]);
         const float disc = lg_f * (is_done ? 0.f : 1.f);
-        prev = delta + prev * static_cast<double>(disc);
+        prev = delta + prev * static_cast<RT>(disc);
         const float a = static_cast<float>(prev);
         const int64_t idx = static_cast<int64_t>(t) * n + env;
         adv[idx] = a;
@@ -303,7 +303,7 @@ __global__ void feistel_rows_kernel(uint64_t seed, uint64_t epoch, int64_t start
 // ============================================================================================
 // Fused Adam (torch.optim.Adam single-tensor CPU path, adam.py _single_tensor_adam)
 //   m = lerp(m, g, 1-b1)          -> vectorised lerp: fma(w, g-m, m) for w < 0.5
-//   v = v*b2 + ((1-b2)*g)*g       -> mul_ then addcmul_ (value*t1*t2, no FMA)
+//   v = fma((1-b2)*g, g, v*b2)    -> mul_ then addcmul_ (contracted to one FMA on CPU)
 //   denom = sqrt(v)/bc2_sqrt + eps
 //   p = p + (neg_step*m)/denom    -> addcdiv_ (value*t1/t2)
 // ============================================================================================
@@ -316,8 +316,8 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
   const float gi = g[i];
   float mi = m[i];
   mi = (w1 < 0.5f) ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.f, gi - mi, gi);
-  float vi = v[i] * b2;
-  vi = vi + (omb2 * gi) * gi;
+  // torch's vectorised addcmul (self + value*t1*t2) is built with FP contraction: one FMA
+  const float vi = fmaf(omb2 * gi, gi, v[i] * b2);
   const float denom = sqrtf(vi) / bc2_sqrt + eps;
   const float ns = (i < n_actor) ? neg_step_a : neg_step_c;
   p[i] = p[i] + (ns * mi) / denom;

@@ -117,6 +117,25 @@ class Engine:
                                        ptr(action), ptr(logp), ptr(value), ptr(mean),
                                        _stream(self.device)))
 
+    # ---- measurement ---------------------------------------------------------------------
+    def timing(self, enable: bool, capacity: int = 65536) -> None:
+        """Record a HIP event pair around every kernel this context launches (live roofline)."""
+        check(self.lib.ppo_ctx_timing(self._ctx, int(enable), int(capacity)))
+
+    def timing_read(self) -> dict:
+        """{class: {"ms": total kernel ms, "launches": n, "flops": algorithmic, "bytes": ...}}"""
+        out = {}
+        n_cls = self.lib.ppo_ctx_timing_read(self._ctx, -1, None, None, None, None)
+        for c in range(n_cls):
+            ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            cnt = ctypes.c_int64()
+            check(self.lib.ppo_ctx_timing_read(self._ctx, c, ctypes.byref(ms), ctypes.byref(cnt),
+                                               ctypes.byref(fl), ctypes.byref(by)))
+            name = self.lib.ppo_kernel_class_name(c).decode()
+            out[name] = {"ms": ms.value, "launches": cnt.value, "flops": fl.value,
+                         "bytes": by.value}
+        return out
+
     # ---- A11-A13 -------------------------------------------------------------------------
     def minibatch_grad(self, states, actions, old_logp, adv, vtarget, rows, b: int, grad, loss,
                        clip_lo: float, clip_hi: float, entropy_coef: float, inv_b: float,
