@@ -23,7 +23,8 @@
  * Flat parameter layout: actor then critic, each in torch `Module.parameters()` order, i.e.
  *   actor : actor_logstd[A], then per layer l: W_l[out][in] (row-major, torch Linear), b_l[out]
  *   critic: per layer l: W_l[out][in], b_l[out]
- * Gradients, Adam moments and split-K partial slabs use the same layout.
+ * each tensor starting at a 16-float aligned offset (ppo_param_offsets) so weight rows load as
+ * 16-B vectors.  Gradients, Adam moments and split-K partial slabs use the same layout.
  */
 #ifndef PPO_ENGINE_H
 #define PPO_ENGINE_H
@@ -68,6 +69,10 @@ int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out);
 int ppo_ctx_destroy(ppo_ctx *ctx);
 /* net = 0 actor, 1 critic, -1 both: number of fp32 parameters in the flat layout. */
 int64_t ppo_param_count(const ppo_ctx *ctx, int net);
+/* Offsets (floats) of every parameter tensor in the flat layout, in torch parameters() order
+ * (actor then critic); every tensor starts 16-float (64-B) aligned, padding in between is zero
+ * in gradients.  Writes min(count, max_tensors) offsets; returns the tensor count. */
+int ppo_param_offsets(const ppo_ctx *ctx, int64_t *offsets, int max_tensors);
 /* Bind the flat fp32 parameter buffer (device, ppo_param_count(ctx,-1) floats). */
 int ppo_bind_params(ppo_ctx *ctx, float *params_d);
 

@@ -40,6 +40,7 @@ _SIGNATURES = {
     "ppo_ctx_destroy": (c_int, [c_void_p]),
     "ppo_param_count": (c_int64, [c_void_p, c_int]),
     "ppo_bind_params": (c_int, [c_void_p, c_void_p]),
+    "ppo_param_offsets": (c_int, [c_void_p, POINTER(c_int64), c_int]),
     "ppo_obs_window_push": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                                     c_int, c_void_p]),
     "ppo_obs_normalize": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, POINTER(c_int32), c_int,

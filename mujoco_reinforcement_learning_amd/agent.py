@@ -64,11 +64,11 @@ class FlatAdam:
                self.param_groups[0]["eps"])
 
     def _views(self):
-        off = 0
-        for p in self.params:
+        base = self._p.data_ptr()
+        for p in self.params:  # each parameter is a view of the flat buffer (padded layout)
+            off = (p.data_ptr() - base) // p.element_size()
             n = p.numel()
             yield p, self._m[off:off + n].view(p.shape), self._v[off:off + n].view(p.shape)
-            off += n
 
     def state_dict(self):
         state = {}
@@ -145,16 +145,14 @@ class PPOEngineAgent:
         self.networks["actor"] = EngineActor(in_dim, hidden, nc.output_shape, act_cls,
                                              nc.use_bias, nc.output_max_value)
         self.networks["critic"] = EngineCritic(in_dim, critic_hidden, act_cls)
-        self.flat_params = move_to_flat(self.networks, self.device)
         for m in (self.networks["actor"], self.networks["critic"]):
             m._agent = self
         rows = max_rows or max(ec.num_envs, int(run.training_config.batch_size))
         self.engine = E.Engine(nc.input_shape, ec.window_length, nc.output_shape, hidden,
                                critic_hidden, _ACT_NAMES[act_cls], nc.use_bias,
                                nc.output_max_value, rows, self.device)
-        if self.engine.n_params != self.flat_params.numel():
-            raise RuntimeError(f"flat layout mismatch: engine {self.engine.n_params} vs modules "
-                               f"{self.flat_params.numel()}")
+        self.flat_params = move_to_flat(self.networks, self.device, self.engine.param_offsets(),
+                                        self.engine.n_params)
         self.engine.bind(self.flat_params)
         self.flat_grad = torch.zeros_like(self.flat_params)
         self.flat_m = torch.zeros_like(self.flat_params)
@@ -169,6 +167,19 @@ class PPOEngineAgent:
                                self.engine.n_params, lr),
         }
         self.schedulers = {k: ExponentialLRFacade(o, 0.999) for k, o in self.optimizers.items()}
+
+    def packed_params(self) -> torch.Tensor:
+        """All parameters concatenated in parameters() order (no alignment padding)."""
+        return torch.cat([p.detach().reshape(-1) for p in self.networks.parameters()])
+
+    def packed(self, flat: torch.Tensor) -> torch.Tensor:
+        """Any flat-layout buffer (grad, m, v) gathered into parameters() order."""
+        base = self.flat_params.data_ptr()
+        out = []
+        for p in self.networks.parameters():
+            off = (p.data_ptr() - base) // 4
+            out.append(flat[off:off + p.numel()])
+        return torch.cat(out)
 
     # ---- fused optimizer step for both networks (ppo.py:122 + :135 in one launch) -------------
     def step_both(self) -> None:

@@ -54,18 +54,88 @@ struct GemmBatch {
   int64_t slab_stride;     // EPI_PARTIAL: floats between split slabs
 };
 
-template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI>
+// One operand's share of a k-tile: NV vectors of V floats per thread, staged in registers.
+// KC: the stored rows run along k ([rows][k], transposed on the LDS store); otherwise they run
+// along the tile dimension ([k][rows]).  `rows` gathers the stored row index.  Out-of-range
+// elements load as zero.  V = 4 requires 16-B aligned rows (ld % 4 == 0, aligned base).
+template <int R, int BK, int NT, int V, bool KC>
+struct OperandTile {
+  static constexpr int NV = R * BK / (NT * V);
+  static_assert((R * BK) % (NT * V) == 0, "tile/thread mismatch");
+  float v[NV][V];
+
+  __device__ __forceinline__ static void coords(int e, int &rr, int &kk) {
+    if (KC) {
+      kk = (e % (BK / V)) * V;
+      rr = e / (BK / V);
+    } else {
+      rr = (e % (R / V)) * V;
+      kk = e / (R / V);
+    }
+  }
+  __device__ __forceinline__ static void span(const float *src, int first, int lim,
+                                              float (&out)[V]) {
+    if (V == 4 && first + 3 < lim) {
+      const float4 x = *reinterpret_cast<const float4 *>(src);
+      out[0] = x.x;
+      out[1 % V] = x.y;
+      out[2 % V] = x.z;
+      out[3 % V] = x.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) out[j] = (first + j < lim) ? src[j] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void load(const float *base, const int32_t *rows, int64_t ld, int r0,
+                                       int rlim, int k0, int kend, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int rr, kk;
+      coords(tid + i * NT, rr, kk);
+      const int gr = r0 + rr, gk = k0 + kk;
+      const bool ok = KC ? (gr < rlim) : (gk < kend);
+      if (ok) {
+        const int64_t row = rows ? rows[KC ? gr : gk] : (KC ? gr : gk);
+        if (KC) span(base + row * ld + gk, gk, kend, v[i]);
+        else span(base + row * ld + gr, gr, rlim, v[i]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[i][j] = 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float *s, int stride, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int rr, kk;
+      coords(tid + i * NT, rr, kk);
+      if (KC) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) s[(kk + j) * stride + rr] = v[i][j];
+      } else if (V == 4) {
+        *reinterpret_cast<float4 *>(&s[kk * stride + rr]) =
+            make_float4(v[i][0], v[i][1 % V], v[i][2 % V], v[i][3 % V]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) s[kk * stride + rr + j] = v[i][j];
+      }
+    }
+  }
+};
+
+// VA / VB = vector width (1 or 4 floats) of the A / B operand's global loads.
+template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI, int VA, int VB>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 32 * TM * WM;
   constexpr int BN = 32 * TN * WN;
-  constexpr int SA = BM + 2;
-  constexpr int SB = BN + 2;
-  constexpr int A_PER = BM * BK / NT;
-  constexpr int B_PER = BN * BK / NT;
-  static_assert((BM * BK) % NT == 0 && (BN * BK) % NT == 0, "tile/thread mismatch");
+  // LDS images are [k][m] / [k][n].  A k-contiguous operand is transposed on its store: a row
+  // stride == 1 (mod 32) puts the 32 lanes of a store group on 32 distinct banks.  An m/n-
+  // contiguous operand is stored as it arrives, 16-B aligned rows for ds_write_b128.
+  constexpr int SA = (AMODE == A_MK) ? BM + 1 : BM + 4;
+  constexpr int SB = (BMODE == B_NK) ? BN + 1 : BN + 4;
   static_assert(BK % 2 == 0, "BK must be even for 32x32x2");
-  __shared__ float lds[2 * BK * (SA + SB)];
+  __shared__ __attribute__((aligned(16))) float lds[2 * BK * (SA + SB)];
 
   const GemmProblem P = (blockIdx.z == 0) ? gb.p[0] : gb.p[1];
   int M = P.m, N = P.n, K = gb.k;
@@ -89,62 +159,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
 
-  float ra[A_PER], rb[B_PER];
+  OperandTile<BM, BK, NT, VA, AMODE == A_MK> ta;
+  OperandTile<BN, BK, NT, VB, BMODE == B_NK> tb;
   auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + i * NT;
-      int mm, kk;
-      if (AMODE == A_MK) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
-      const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < kend) {
-        if (AMODE == A_MK) {
-          const int64_t row = P.a_rows ? P.a_rows[gm] : gm;
-          v = P.a[row * P.lda + gk];
-        } else {
-          const int64_t row = P.a_rows ? P.a_rows[gk] : gk;
-          v = P.a[row * P.lda + gm];
-        }
-      }
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + i * NT;
-      int nn, kk;
-      if (BMODE == B_NK) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
-      const int gn = n0 + nn, gk = k0 + kk;
-      float v = 0.f;
-      if (gn < N && gk < kend) {
-        if (BMODE == B_NK) {
-          const int64_t row = P.b_rows ? P.b_rows[gn] : gn;
-          v = P.b[row * P.ldb + gk];
-        } else {
-          const int64_t row = P.b_rows ? P.b_rows[gk] : gk;
-          v = P.b[row * P.ldb + gn];
-        }
-      }
-      rb[i] = v;
-    }
+    ta.load(P.a, P.a_rows, P.lda, m0, M, k0, kend, tid);
+    tb.load(P.b, P.b_rows, P.ldb, n0, N, k0, kend, tid);
   };
   auto lstore = [&](int buf) {
     float *As = lds + buf * BK * (SA + SB);
-    float *Bs = As + BK * SA;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + i * NT;
-      int mm, kk;
-      if (AMODE == A_MK) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
-      As[kk * SA + mm] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + i * NT;
-      int nn, kk;
-      if (BMODE == B_NK) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
-      Bs[kk * SB + nn] = rb[i];
-    }
+    ta.store(As, SA, tid);
+    tb.store(As + BK * SA, SB, tid);
   };
 
   f32x16 acc[TM][TN];
@@ -318,9 +342,201 @@ struct UpdateHeadArgs {
   int splits;
 };
 
-// One block per split of the minibatch, one wave per row at a time.  Gradients follow torch's
-// autograd formulas: minimum() splits a tie's gradient in halves, clamp passes it on the closed
-// interval, huber_loss_backward clips at +-delta, tanh backward is grad*(1-y*y).
+// Fast head: 4 lanes per row, 16 rows per wave pass, D = 16*NJ columns (actor and critic last
+// hidden widths equal).  Lane (row r = lane>>2, quarter qd = lane&3) holds float4 chunks
+// 16t + 4qd of its row; a head dot product is NJ float4 FMAs against LDS-staged head weights
+// (same address for the 16 rows -> LDS broadcast) plus a 2-step shuffle over the row's 4 lanes.
+// Per-action work (tanh, log-prob, dz) is spread over the 4 lanes: lane qd owns actions
+// a = 4k + qd.  Same torch formulas as update_head_kernel below.
+template <int NJ>
+__global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
+  constexpr int D = 16 * NJ;
+  constexpr int KA = kMaxAct / 4;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float red[4][kMaxAct + 2];
+  const int A = q.act_dim;
+  float *wsh = smem;                   // (A + 1) x D: actor head rows, then the critic row
+  float *lps = smem + (A + 1) * D;     // [4 waves][16 rows][kMaxAct] log-probs
+  float *dzs = lps + 4 * 16 * kMaxAct;  // [4 waves][16 rows][kMaxAct] d(pre-tanh)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane >> 2, qd = lane & 3;
+  for (int i = tid; i < A * D; i += 256) wsh[i] = q.wa[i];
+  for (int i = tid; i < D; i += 256) wsh[A * D + i] = q.wc[i];
+  __syncthreads();
+  const int count = q.rows_n ? *q.rows_n : q.rows_max;
+  const int r0 = static_cast<int>((static_cast<int64_t>(blockIdx.x) * count) / q.splits);
+  const int r1 = static_cast<int>((static_cast<int64_t>(blockIdx.x + 1) * count) / q.splits);
+  float *lp_row = lps + (wid * 16 + r) * kMaxAct;
+  float *dz_row = dzs + (wid * 16 + r) * kMaxAct;
+  float ls_acc[KA];
+#pragma unroll
+  for (int k = 0; k < KA; ++k) ls_acc[k] = 0.f;
+  float la_acc = 0.f, lc_acc = 0.f;
+  for (int base = r0 + 16 * wid; base < r1; base += 64) {  // wave-uniform trip count
+    const int j = base + r;
+    const bool valid = j < r1;
+    const int64_t sr = valid ? q.rows[j] : 0;
+    float4 h[NJ];
+    const float4 *hrow = reinterpret_cast<const float4 *>(q.ha + static_cast<int64_t>(j) * D);
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) h[t] = valid ? hrow[4 * t + qd] : make_float4(0, 0, 0, 0);
+    // ---- actor head: z_a for the lane's own actions a = 4k + qd
+    float zk[KA];
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      zk[k] = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int a = 4 * k + qq;
+        if (a < A) {
+          const float4 *w = reinterpret_cast<const float4 *>(wsh + a * D);
+          float p = 0.f;
+#pragma unroll
+          for (int t = 0; t < NJ; ++t) {
+            const float4 wv = w[4 * t + qd];
+            p = fmaf(h[t].x, wv.x, p);
+            p = fmaf(h[t].y, wv.y, p);
+            p = fmaf(h[t].z, wv.z, p);
+            p = fmaf(h[t].w, wv.w, p);
+          }
+          p += __shfl_xor(p, 1, 64);
+          p += __shfl_xor(p, 2, 64);
+          if (qq == qd) zk[k] = p;
+        }
+      }
+    }
+    float yk[KA], dk[KA], vk[KA];
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int a = 4 * k + qd;
+      yk[k] = 0.f, dk[k] = 0.f, vk[k] = 1.f;
+      if (a < A) {
+        const float z = q.ba ? zk[k] + q.ba[a] : zk[k];
+        const float y = tanhf(z);
+        const float mu = q.omv * y;
+        const float sd = expf(q.logstd[a]);
+        const float x = valid ? q.actions[sr * A + a] : mu;
+        const float d = x - mu;
+        const float var = sd * sd;
+        lp_row[a] = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+        yk[k] = y, dk[k] = d, vk[k] = var;
+      }
+    }
+    __threadfence_block();
+    float logp = 0.f;
+    for (int a = 0; a < A; ++a) logp += lp_row[a];
+    const float old_lp = valid ? q.old_logp[sr] : logp;
+    const float adv = valid ? q.adv[sr] : 0.f;
+    const float ratio = expf(logp - old_lp);
+    const float s1 = ratio * adv;
+    const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+    const float s2 = cl * adv;
+    const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+    const float g = -q.inv_b;
+    const float g1 = (s1 < s2) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+    const float g2 = (s2 < s1) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+    const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+    const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+    const float dlogp = valid ? dratio * ratio : 0.f;
+    if (valid && qd == 0) la_acc += mn;
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int a = 4 * k + qd;
+      if (a < A) {
+        const float dmu = dlogp * (dk[k] / vk[k]);
+        const float dz = (dmu * q.omv) * (1.f - yk[k] * yk[k]);
+        dz_row[a] = dz;
+        if (valid) {
+          ls_acc[k] += dlogp * ((dk[k] * dk[k]) / vk[k] - 1.f) - q.ent_coef * q.inv_ba;
+          q.dza[static_cast<int64_t>(j) * A + a] = dz;
+        }
+      }
+    }
+    __threadfence_block();
+    // ---- dH_L(actor) = (dz . W_head) * act'(h)
+    float4 *grow = reinterpret_cast<float4 *>(q.ga + static_cast<int64_t>(j) * D);
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+      float4 s = make_float4(0, 0, 0, 0);
+      for (int a = 0; a < A; ++a) {
+        const float dz = dz_row[a];
+        const float4 wv = reinterpret_cast<const float4 *>(wsh + a * D)[4 * t + qd];
+        s.x = fmaf(dz, wv.x, s.x);
+        s.y = fmaf(dz, wv.y, s.y);
+        s.z = fmaf(dz, wv.z, s.z);
+        s.w = fmaf(dz, wv.w, s.w);
+      }
+      if (valid)
+        grow[4 * t + qd] = make_float4(act_backward(s.x, h[t].x, q.act), act_backward(s.y, h[t].y, q.act),
+                                       act_backward(s.z, h[t].z, q.act), act_backward(s.w, h[t].w, q.act));
+    }
+    // ---- critic
+    const float4 *crow = reinterpret_cast<const float4 *>(q.hc + static_cast<int64_t>(j) * D);
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) h[t] = valid ? crow[4 * t + qd] : make_float4(0, 0, 0, 0);
+    const float4 *wc = reinterpret_cast<const float4 *>(wsh + A * D);
+    float p = 0.f;
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+      const float4 wv = wc[4 * t + qd];
+      p = fmaf(h[t].x, wv.x, p);
+      p = fmaf(h[t].y, wv.y, p);
+      p = fmaf(h[t].z, wv.z, p);
+      p = fmaf(h[t].w, wv.w, p);
+    }
+    p += __shfl_xor(p, 1, 64);
+    p += __shfl_xor(p, 2, 64);
+    const float v = q.bc ? p + q.bc[0] : p;
+    const float vt = valid ? q.vtarget[sr] : v;
+    const float diff = v - vt;
+    const float ad = fabsf(diff);
+    if (valid && qd == 0) lc_acc += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+    const float dv = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+    if (valid && qd == 0) q.dzc[j] = dv;
+    float4 *gcrow = reinterpret_cast<float4 *>(q.gc + static_cast<int64_t>(j) * D);
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+      const float4 wv = wc[4 * t + qd];
+      if (valid)
+        gcrow[4 * t + qd] =
+            make_float4(act_backward(dv * wv.x, h[t].x, q.act), act_backward(dv * wv.y, h[t].y, q.act),
+                        act_backward(dv * wv.z, h[t].z, q.act), act_backward(dv * wv.w, h[t].w, q.act));
+    }
+  }
+  // ---- fixed-order reductions: over the 16 rows of the wave (lane bits 2..5), then waves 0..3
+#pragma unroll
+  for (int k = 0; k < KA; ++k)
+#pragma unroll
+    for (int off = 4; off < 64; off <<= 1) ls_acc[k] += __shfl_xor(ls_acc[k], off, 64);
+#pragma unroll
+  for (int off = 4; off < 64; off <<= 1) {
+    la_acc += __shfl_xor(la_acc, off, 64);
+    lc_acc += __shfl_xor(lc_acc, off, 64);
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int k = 0; k < KA; ++k)
+      if (4 * k + qd < A) red[wid][4 * k + qd] = ls_acc[k];
+    if (qd == 0) {
+      red[wid][kMaxAct] = la_acc;
+      red[wid][kMaxAct + 1] = lc_acc;
+    }
+  }
+  __syncthreads();
+  if (tid < A)
+    q.logstd_part[static_cast<int64_t>(blockIdx.x) * A + tid] =
+        ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (tid == 0) {
+    q.loss_part[2 * blockIdx.x] = ((red[0][kMaxAct] + red[1][kMaxAct]) + red[2][kMaxAct]) +
+                                  red[3][kMaxAct];
+    q.loss_part[2 * blockIdx.x + 1] =
+        ((red[0][kMaxAct + 1] + red[1][kMaxAct + 1]) + red[2][kMaxAct + 1]) + red[3][kMaxAct + 1];
+  }
+}
+
+// Generic head (any widths): one wave per row.  Gradients follow torch's autograd formulas:
+// minimum() splits a tie's gradient in halves, clamp passes it on the closed interval,
+// huber_loss_backward clips at +-delta, tanh backward is grad*(1-y*y).
 template <int HPL>
 __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
   __shared__ float red[4][kMaxAct + 2];
@@ -446,6 +662,21 @@ __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
 }
 
 // ============================================================================================
+// Minibatch state gather: xg[j][0:din] = states[rows[j]][:], zero padded to ldx (16-B rows), so
+// both layer-1 GEMMs (forward and weight-gradient) stream one contiguous, vector-loadable buffer
+// instead of re-gathering 68-B rows element by element.
+// ============================================================================================
+__global__ void gather_states_kernel(const float *__restrict__ states, const int32_t *__restrict__ rows,
+                                     const int32_t *__restrict__ rows_n, int b, int din, int ldx,
+                                     float *__restrict__ xg) {
+  const int count = rows_n ? *rows_n : b;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(count) * ldx) return;
+  const int j = static_cast<int>(i / ldx), c = static_cast<int>(i % ldx);
+  xg[i] = (c < din) ? states[static_cast<int64_t>(rows[j]) * din + c] : 0.f;
+}
+
+// ============================================================================================
 // Split-K reduction of the slabs into the flat gradient + loss scalars
 // ============================================================================================
 constexpr int kMaxSegs = 48;
@@ -469,30 +700,74 @@ struct ReduceArgs {
   float *loss_out;
 };
 
-__global__ void reduce_slabs_kernel(ReduceArgs q) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+// Block = 64 float4 groups x 4 split-chunks (one wave per chunk): each thread sums a quarter of
+// the splits for 4 consecutive parameters (tensors start 16-float aligned, so a group never
+// straddles two tensors), then the chunks combine in a fixed order through LDS.  Block 0 also
+// reduces the per-split loss partials with a fixed-shape tree.  Deterministic run to run.
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceArgs q) {
+  __shared__ float4 part[4][64];
+  __shared__ float lred[2][256];
+  const int tid = threadIdx.x, grp = tid & 63, chunk = tid >> 6;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * grp;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < q.total) {
     int s = 0;
     while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
     const ReduceSeg &g = q.seg[s];
     const int64_t off = i - g.dst;
-    float acc = 0.f;
-    for (int k = 0; k < g.nsplit; ++k) acc += g.src[k * g.stride + off];
-    q.grad[i] = acc;
+    const int k0 = (g.nsplit * chunk) / 4, k1 = (g.nsplit * (chunk + 1)) / 4;
+    if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
+        reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
+      const float *src = g.src + off;
+#pragma unroll 4
+      for (int k = k0; k < k1; ++k) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+    } else if (off >= 0) {  // tail of a tensor / unaligned source; padding stays zero
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 4; ++e)
+        if (off + e < g.len)
+          for (int k = k0; k < k1; ++k) a4[e] += g.src[k * g.stride + off + e];
+      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
+    }
   }
-  if (i == 0 && q.loss_out) {
+  part[chunk][grp] = acc;
+  __syncthreads();
+  if (chunk == 0 && i < q.total) {
+    const float4 a = part[0][grp], b = part[1][grp], c = part[2][grp], d = part[3][grp];
+    *reinterpret_cast<float4 *>(q.grad + i) =
+        make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
+                    ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
+  }
+  if (blockIdx.x == 0 && q.loss_out) {
     float la = 0.f, lc = 0.f;
-    for (int k = 0; k < q.loss_splits; ++k) {
+    for (int k = tid; k < q.loss_splits; k += 256) {
       la += q.loss_part[2 * k];
       lc += q.loss_part[2 * k + 1];
     }
-    float h = 0.f;
-    if (q.logstd) {
-      for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
-      h = h / static_cast<float>(q.act_dim);
+    lred[0][tid] = la;
+    lred[1][tid] = lc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w) {
+        lred[0][tid] += lred[0][tid + w];
+        lred[1][tid] += lred[1][tid + w];
+      }
+      __syncthreads();
     }
-    q.loss_out[0] = -(la * q.inv_b) - h * q.ent_coef;
-    q.loss_out[1] = lc * q.inv_b;
+    if (tid == 0) {
+      float h = 0.f;
+      if (q.logstd) {
+        for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
+        h = h / static_cast<float>(q.act_dim);
+      }
+      q.loss_out[0] = -(lred[0][0] * q.inv_b) - h * q.ent_coef;
+      q.loss_out[1] = lred[1][0] * q.inv_b;
+    }
   }
 }
 
@@ -525,10 +800,12 @@ enum {
   KC_UPDATE_HEAD,
   KC_POLICY_HEAD,
   KC_REDUCE,
+  KC_GATHER,
   KC_COUNT
 };
 static const char *const kClassNames[KC_COUNT] = {"gemm_fwd",    "gemm_dgrad",  "gemm_wgrad",
-                                                  "update_head", "policy_head", "reduce_slabs"};
+                                                  "update_head", "policy_head", "reduce_slabs",
+                                                  "gather_states"};
 
 struct Timing {
   bool on = false;
@@ -569,6 +846,8 @@ struct ppo_ctx {
   float *params;
   float *slabs;          // (kSlabSplits, total_params)
   float *head_part;      // logstd partials (kHeadSplits, A) + loss partials (kHeadSplits, 2)
+  float *xg;             // gathered minibatch states (max_rows, ldx)
+  int ldx;               // round_up(W*O, 4)
   void *arena;
   ppo::Timing tim;
 };
@@ -591,7 +870,24 @@ static double gemm_flops(const GemmBatch &gb, int nprob, int epi) {
 }
 
 constexpr int kSlabSplits = 64;
+constexpr int64_t kParamAlign = 16;  // floats: every flat tensor starts 64-B aligned
+constexpr int64_t kWsAlign = 64;     // floats: workspace buffers start 256-B aligned
+
+static inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 constexpr int kHeadSplits = 512;
+
+constexpr int kGemmBK = 32;
+
+// float4 loads need every row of the operand 16-B aligned: ld % 4 == 0 and a 16-B aligned base.
+static bool vec4_ok(const GemmBatch &gb, int nprob, bool operand_a) {
+  for (int i = 0; i < nprob; ++i) {
+    const GemmProblem &p = gb.p[i];
+    const int64_t ld = operand_a ? p.lda : p.ldb;
+    const void *base = operand_a ? static_cast<const void *>(p.a) : static_cast<const void *>(p.b);
+    if (ld % 4 || reinterpret_cast<uintptr_t>(base) % 16) return false;
+  }
+  return true;
+}
 
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
@@ -599,7 +895,16 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
   const int tiles = ceil_div(max_m, BM) * ceil_div(max_n, BN);
   dim3 grid(tiles, EPI == EPI_PARTIAL ? gb.splits : 1, nprob);
   tim_begin(st);
-  gemm_f32_kernel<TM, TN, WM, WN, 16, AMODE, BMODE, EPI><<<grid, 64 * WM * WN, 0, st>>>(gb);
+  const bool va = vec4_ok(gb, nprob, true), vb = vec4_ok(gb, nprob, false);
+  constexpr int NTH = 64 * WM * WN;
+  if (va && vb)
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 4><<<grid, NTH, 0, st>>>(gb);
+  else if (va)
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 1><<<grid, NTH, 0, st>>>(gb);
+  else if (vb)
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 4><<<grid, NTH, 0, st>>>(gb);
+  else
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 1><<<grid, NTH, 0, st>>>(gb);
   PPO_LAUNCHED();
   const int cls = EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD);
   double bytes = 0;
@@ -634,8 +939,7 @@ static int hpl_for(int width) {
 // Forward through the hidden layers of the requested nets.  x: (rows, in) f32 with optional
 // row gather.  Nets whose layer-l shapes agree share one launch.
 static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const int32_t *x_rows,
-                          int rows, const int32_t *rows_n, hipStream_t st) {
-  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+                          int rows, const int32_t *rows_n, hipStream_t st, int ldx) {
   const int max_l = std::max(use[0] ? ctx->net[0].n_hidden : 0, use[1] ? ctx->net[1].n_hidden : 0);
   for (int l = 0; l < max_l; ++l) {
     GemmBatch gb{};
@@ -658,7 +962,7 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
       GemmProblem &P = gb.p[np++];
       P.a = (l == 0) ? x : nd.h[l - 1];
       P.a_rows = (l == 0) ? x_rows : nullptr;
-      P.lda = (l == 0) ? din : nd.layer[l - 1].out;
+      P.lda = (l == 0) ? ldx : nd.layer[l - 1].out;
       P.b = ctx->params + L.w_off;
       P.ldb = L.in;
       P.c = nd.h[l];
@@ -705,7 +1009,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
   ctx->device = device;
   const int din = cfg->obs_dim * cfg->window;
   int64_t off = 0;
-  size_t ws_floats = 0;
+  int64_t ws_floats = 0;
   const int64_t R = cfg->max_rows;
   for (int z = 0; z < 2; ++z) {
     NetDesc &nd = ctx->net[z];
@@ -716,7 +1020,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
     nd.n_hidden = nh;
     if (z == 0) {
       nd.logstd_off = off;
-      off += cfg->act_dim;
+      off = align_up(off + cfg->act_dim, kParamAlign);
     } else {
       nd.logstd_off = -1;
     }
@@ -732,19 +1036,21 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       L.in = width;
       L.out = o;
       L.w_off = off;
-      off += static_cast<int64_t>(o) * width;
+      off = align_up(off + static_cast<int64_t>(o) * width, kParamAlign);
       L.b_off = bias ? off : -1;
-      if (bias) off += o;
-      if (l < nh) ws_floats += static_cast<size_t>(R) * o;
+      if (bias) off = align_up(off + o, kParamAlign);
+      if (l < nh) ws_floats += align_up(R * o, kWsAlign);
       width = o;
     }
-    ws_floats += static_cast<size_t>(R) * nd.layer[nh].in;   // g = dH_L (last hidden width)
-    ws_floats += static_cast<size_t>(R) * nd.layer[nh].out;  // dz
+    ws_floats += align_up(R * nd.layer[nh].in, kWsAlign);   // g = dH_L (last hidden width)
+    ws_floats += align_up(R * nd.layer[nh].out, kWsAlign);  // dz
     nd.count = off - nd.begin;
   }
   ctx->total_params = off;
-  ws_floats += static_cast<size_t>(kSlabSplits) * off;
-  ws_floats += static_cast<size_t>(kHeadSplits) * (cfg->act_dim + 2);
+  ws_floats += align_up(static_cast<int64_t>(kSlabSplits) * off, kWsAlign);
+  ws_floats += align_up(static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2), kWsAlign);
+  const int ldx = static_cast<int>(align_up(din, 4));
+  ws_floats += align_up(R * ldx, kWsAlign);
   void *arena = nullptr;
   hipError_t e = hipMalloc(&arena, ws_floats * sizeof(float) + 256);
   if (e != hipSuccess) {
@@ -759,19 +1065,22 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
     NetDesc &nd = ctx->net[z];
     for (int l = 0; l < nd.n_hidden; ++l) {
       nd.h[l] = p;
-      p += R * nd.layer[l].out;
+      p += align_up(R * nd.layer[l].out, kWsAlign);
     }
     nd.g = p;
-    p += R * nd.layer[nd.n_hidden - 1].out;
+    p += align_up(R * nd.layer[nd.n_hidden].in, kWsAlign);
     nd.dz = p;
-    p += R * nd.layer[nd.n_hidden].out;
+    p += align_up(R * nd.layer[nd.n_hidden].out, kWsAlign);
   }
   ctx->slabs = p;
-  p += static_cast<int64_t>(kSlabSplits) * off;
+  p += align_up(static_cast<int64_t>(kSlabSplits) * off, kWsAlign);
   ctx->head_part = p;
-  p += static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2);
-  if (static_cast<size_t>(p - static_cast<float *>(arena)) != ws_floats) {
-    hipFree(arena);
+  p += align_up(static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2), kWsAlign);
+  ctx->xg = p;
+  ctx->ldx = ldx;
+  p += align_up(R * ldx, kWsAlign);
+  if (static_cast<int64_t>(p - static_cast<float *>(arena)) != ws_floats) {
+    (void)hipFree(arena);
     delete ctx;
     set_error("ppo_ctx_create: internal workspace carve-out mismatch");
     return PPO_EHIP;
@@ -800,6 +1109,24 @@ extern "C" int64_t ppo_param_count(const ppo_ctx *ctx, int net) {
   return ctx->total_params;
 }
 
+extern "C" int ppo_param_offsets(const ppo_ctx *ctx, int64_t *offsets, int max_tensors) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_param_offsets: null ctx");
+  int n = 0;
+  auto put = [&](int64_t off) {
+    if (offsets && n < max_tensors) offsets[n] = off;
+    ++n;
+  };
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    if (z == 0) put(nd.logstd_off);
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      put(nd.layer[l].w_off);
+      if (nd.layer[l].b_off >= 0) put(nd.layer[l].b_off);
+    }
+  }
+  return n;
+}
+
 extern "C" int ppo_bind_params(ppo_ctx *ctx, float *params_d) {
   PPO_REQUIRE(ctx && params_d, "ppo_bind_params: null argument");
   ctx->params = params_d;
@@ -817,7 +1144,9 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   TimingScope timing_scope(ctx);
   const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
   if (!use[0] && !use[1]) return 0;
-  if (int rc = forward_hidden(ctx, use, state_d, nullptr, n, nullptr, st)) return rc;
+  if (int rc = forward_hidden(ctx, use, state_d, nullptr, n, nullptr, st,
+                              ctx->cfg.obs_dim * ctx->cfg.window))
+    return rc;
   const NetDesc &A = ctx->net[0], &C = ctx->net[1];
   PolicyHeadArgs q{};
   q.n = n;
@@ -876,7 +1205,12 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   const bool both[2] = {true, true};
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
-  if (int rc = forward_hidden(ctx, both, states_d, rows_d, b, count_d, st)) return rc;
+  tim_begin(st);
+  gather_states_kernel<<<ceil_div(static_cast<int64_t>(b) * ctx->ldx, 256), 256, 0, st>>>(
+      states_d, rows_d, count_d, b, din, ctx->ldx, ctx->xg);
+  PPO_LAUNCHED();
+  tim_end(KC_GATHER, 0.0, 4.0 * b * (2.0 * din + 1), st);
+  if (int rc = forward_hidden(ctx, both, ctx->xg, nullptr, b, count_d, st, ctx->ldx)) return rc;
 
   // ---- heads: loss, dz, dH_L -------------------------------------------------------------
   NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
@@ -916,9 +1250,33 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   u.splits = head_splits;
   const int hpl = hpl_for(std::max(u.da, u.dc));
   tim_begin(st);
-  if (hpl == 4) update_head_kernel<4><<<head_splits, 256, 0, st>>>(u);
-  else if (hpl == 8) update_head_kernel<8><<<head_splits, 256, 0, st>>>(u);
-  else update_head_kernel<16><<<head_splits, 256, 0, st>>>(u);
+  const int nj = (u.da == u.dc && u.da % 16 == 0) ? u.da / 16 : 0;
+  const bool aligned = reinterpret_cast<uintptr_t>(u.ha) % 16 == 0 &&
+                       reinterpret_cast<uintptr_t>(u.hc) % 16 == 0;
+  if (aligned && (nj == 2 || nj == 4 || nj == 8 || nj == 16 || nj == 32)) {
+    const size_t shm = sizeof(float) * ((A + 1) * static_cast<size_t>(u.da) + 2 * 4 * 16 * kMaxAct);
+    auto launch = [&](auto kernel) -> int {
+      if (shm > 64 * 1024)
+        PPO_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        static_cast<int>(shm)));
+      kernel<<<head_splits, 256, shm, st>>>(u);
+      return 0;
+    };
+    int rc = 0;
+    if (nj == 2) rc = launch(update_head_q4_kernel<2>);
+    else if (nj == 4) rc = launch(update_head_q4_kernel<4>);
+    else if (nj == 8) rc = launch(update_head_q4_kernel<8>);
+    else if (nj == 16) rc = launch(update_head_q4_kernel<16>);
+    else rc = launch(update_head_q4_kernel<32>);
+    if (rc) return rc;
+  } else if (hpl == 4) {
+    update_head_kernel<4><<<head_splits, 256, 0, st>>>(u);
+  } else if (hpl == 8) {
+    update_head_kernel<8><<<head_splits, 256, 0, st>>>(u);
+  } else {
+    update_head_kernel<16><<<head_splits, 256, 0, st>>>(u);
+  }
   PPO_LAUNCHED();
   // algorithmic bytes per row: read H_L (actor, critic), action, 4 scalars + row index;
   // write dH_L (actor, critic) and dz (A + 1)
@@ -945,9 +1303,9 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
       // dY of layer l: head -> dz, top hidden -> g, lower hidden -> h[l] (overwritten in place)
       Q.a = (l == nd.n_hidden) ? nd.dz : (l == nd.n_hidden - 1 ? nd.g : nd.h[l]);
       Q.lda = L.out;
-      Q.b = (l == 0) ? states_d : nd.h[l - 1];
-      Q.b_rows = (l == 0) ? rows_d : nullptr;
-      Q.ldb = (l == 0) ? din : L.in;
+      Q.b = (l == 0) ? ctx->xg : nd.h[l - 1];
+      Q.b_rows = nullptr;
+      Q.ldb = (l == 0) ? ctx->ldx : L.in;
       Q.c = ctx->slabs + L.w_off;
       Q.ldc = L.in;
       Q.colsum = L.b_off >= 0 ? ctx->slabs + L.b_off : nullptr;
@@ -1047,7 +1405,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   r.ent_coef = entropy_coef;
   r.loss_out = loss_d;
   tim_begin(st);
-  reduce_slabs_kernel<<<ceil_div(P, 256), 256, 0, st>>>(r);
+  reduce_slabs_kernel<<<ceil_div(P, 256), 256, 0, st>>>(r);  // P % 16 == 0
   PPO_LAUNCHED();
   tim_end(KC_REDUCE, static_cast<double>(splits) * P, 4.0 * (static_cast<double>(splits) + 1) * P,
           st);

@@ -83,6 +83,69 @@ __global__ __launch_bounds__(64) void gae_kernel(const float *__restrict__ value
   }
 }
 
+// LDS-staged variant: a 256-thread block owns EB envs.  Phase 1: every thread issues its share
+// of the [T][EB] tile loads (V, V', r, terminated) at once -> LDS (latency paid once, all CUs
+// loading).  Phase 2: EB lanes run the same recurrence as gae_kernel out of LDS.  Phase 3: all
+// threads store adv / vtarget coalesced.  Bit-identical to gae_kernel.  T*EB must fit LDS.
+template <typename RT, int EB>
+__global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ value,
+                                                      const float *__restrict__ next_value,
+                                                      const RT *__restrict__ reward,
+                                                      const uint8_t *__restrict__ done,
+                                                      const uint8_t *__restrict__ term,
+                                                      int force_last, int n, int t_len,
+                                                      float gamma_f, float lg_f,
+                                                      float *__restrict__ adv,
+                                                      float *__restrict__ vtarget) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gae_smem[];
+  const int total = t_len * EB;
+  RT *s_r = reinterpret_cast<RT *>(gae_smem);
+  float *s_v = reinterpret_cast<float *>(s_r + total);
+  float *s_vn = s_v + total;
+  uint8_t *s_fl = reinterpret_cast<uint8_t *>(s_vn + total);  // bit0 term, bit1 done
+  const int env0 = blockIdx.x * EB;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < total; e += 256) {
+    const int t = e / EB, c = e - (e / EB) * EB;
+    const int env = env0 + c;
+    if (env < n) {
+      const int64_t idx = static_cast<int64_t>(t) * n + env;
+      s_v[e] = value[idx];
+      s_vn[e] = next_value[idx];
+      s_r[e] = reward[idx];
+      const uint8_t tm = term[idx];
+      const uint8_t dn = done ? done[idx] : tm;
+      s_fl[e] = static_cast<uint8_t>((tm ? 1 : 0) | ((dn || (force_last && t == t_len - 1)) ? 2 : 0));
+    }
+  }
+  __syncthreads();
+  if (tid < EB && env0 + tid < n) {
+    RT prev = 0;
+    for (int t = t_len - 1; t >= 0; --t) {
+      const int e = t * EB + tid;
+      const uint8_t fl = s_fl[e];
+      const float g_nt = gamma_f * ((fl & 1) ? 0.f : 1.f);
+      const float gv = g_nt * s_vn[e];
+      const RT delta = (s_r[e] + static_cast<RT>(gv)) - static_cast<RT>(s_v[e]);
+      const float disc = lg_f * ((fl & 2) ? 0.f : 1.f);
+      prev = delta + prev * static_cast<RT>(disc);
+      const float a = static_cast<float>(prev);
+      s_vn[e] = a;                 // V' slot is dead once read: reuse it for adv
+      s_v[e] = a + s_v[e];         // and V's slot for the value target
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < total; e += 256) {
+    const int t = e / EB, c = e - (e / EB) * EB;
+    const int env = env0 + c;
+    if (env < n) {
+      const int64_t idx = static_cast<int64_t>(t) * n + env;
+      adv[idx] = s_vn[e];
+      vtarget[idx] = s_v[e];
+    }
+  }
+}
+
 // ============================================================================================
 // Per-env standardisation over T (ppo.py:66-69 rewards f64, :81-88 advantage / value target f32)
 // x <- ((x - mean_T) / std_T) * scale, unbiased std.  torch computes mean in the tensor dtype and
@@ -345,6 +408,41 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
   PPO_REQUIRE(n > 0 && t > 0, "ppo_gae: bad shape n=%d t=%d", n, t);
   const float gamma_f = static_cast<float>(gamma);
   const float lg_f = static_cast<float>(lmbda * gamma);
+  // LDS-staged scan: 16 envs per block (>= 256 blocks at N = 4096), halved until the [T][EB]
+  // tile fits 64 KiB; very long horizons fall back to the register-chunked kernel.
+  const size_t per_elem = (reward_is_f64 ? 8 : 4) + 4 + 4 + 1;
+  int eb = 16;
+  while (eb > 1 && static_cast<size_t>(t) * eb * per_elem > 65536) eb >>= 1;
+  const size_t shm = static_cast<size_t>(t) * eb * per_elem + 16;
+  if (shm <= 65536) {
+    const int blocks = ceil_div(n, eb);
+    hipStream_t st = as_stream(stream);
+#define PPO_GAE_LDS(RT, EB)                                                                    \
+  gae_lds_kernel<RT, EB><<<blocks, 256, shm, st>>>(value_d, next_value_d,                     \
+                                                  static_cast<const RT *>(reward_d), done_d,   \
+                                                  terminated_d, force_last_done, n, t, gamma_f, \
+                                                  lg_f, adv_d, vtarget_d)
+    if (reward_is_f64) {
+      switch (eb) {
+        case 16: PPO_GAE_LDS(double, 16); break;
+        case 8: PPO_GAE_LDS(double, 8); break;
+        case 4: PPO_GAE_LDS(double, 4); break;
+        case 2: PPO_GAE_LDS(double, 2); break;
+        default: PPO_GAE_LDS(double, 1); break;
+      }
+    } else {
+      switch (eb) {
+        case 16: PPO_GAE_LDS(float, 16); break;
+        case 8: PPO_GAE_LDS(float, 8); break;
+        case 4: PPO_GAE_LDS(float, 4); break;
+        case 2: PPO_GAE_LDS(float, 2); break;
+        default: PPO_GAE_LDS(float, 1); break;
+      }
+    }
+#undef PPO_GAE_LDS
+    PPO_LAUNCHED();
+    return 0;
+  }
   const int grid = ceil_div(n, 64);
   if (reward_is_f64)
     gae_kernel<double, 16><<<grid, 64, 0, as_stream(stream)>>>(

@@ -92,6 +92,13 @@ class Engine:
             self._ctx = None
 
     # ---- parameters ----------------------------------------------------------------------
+    def param_offsets(self) -> list:
+        """Flat offset of every parameter tensor (torch parameters() order, actor then critic)."""
+        n = self.lib.ppo_param_offsets(self._ctx, None, 0)
+        arr = (ctypes.c_int64 * n)()
+        self.lib.ppo_param_offsets(self._ctx, arr, n)
+        return list(arr)
+
     def bind(self, flat_params: torch.Tensor) -> None:
         _need(flat_params, "flat_params", torch.float32, (self.n_params,), self.device)
         check(self.lib.ppo_bind_params(self._ctx, ptr(flat_params)))

@@ -72,9 +72,11 @@ class EngineCritic(nn.Module):
         return self._agent.get_state_value(x)
 
 
-def move_to_flat(networks: nn.ModuleDict, device: torch.device) -> torch.Tensor:
-    """Copy every parameter (ModuleDict order, ``parameters()`` order inside) into one flat
-    device tensor and re-point each ``nn.Parameter`` at its slice.  Returns the flat tensor."""
+def move_to_flat(networks: nn.ModuleDict, device: torch.device, offsets: Sequence[int],
+                 total: int) -> torch.Tensor:
+    """Copy every parameter (``parameters()`` order: actor then critic) into one zero-padded
+    flat device tensor at the engine's offsets (ppo_param_offsets: 16-float aligned) and
+    re-point each ``nn.Parameter`` at its slice.  Returns the flat tensor."""
     slots = []
     for mod in networks.modules():
         for name, p in list(mod.named_parameters(recurse=False)):
@@ -83,13 +85,12 @@ def move_to_flat(networks: nn.ModuleDict, device: torch.device) -> torch.Tensor:
     # C layout follows; rebuild the order from parameters() identity.
     order = {id(p): i for i, p in enumerate(networks.parameters())}
     slots.sort(key=lambda s: order[id(s[2])])
-    total = sum(p.numel() for _, _, p in slots)
-    flat = torch.empty(total, dtype=torch.float32, device=device)
-    off = 0
-    for mod, name, p in slots:
+    if len(offsets) != len(slots):
+        raise RuntimeError(f"engine layout has {len(offsets)} tensors, modules {len(slots)}")
+    flat = torch.zeros(total, dtype=torch.float32, device=device)
+    for (mod, name, p), off in zip(slots, offsets):
         n = p.numel()
         view = flat[off:off + n].view(p.shape)
         view.copy_(p.detach().to(torch.float32))
         setattr(mod, name, nn.Parameter(view, requires_grad=False))
-        off += n
     return flat

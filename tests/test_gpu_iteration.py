@@ -42,7 +42,7 @@ def _setup(gpu, n=16, t=32, b=128, epochs=2, hidden=(64, 64), p_term=0.05, rng="
 @pytest.mark.parametrize("kw", [{}, {"normalize_advantage": True, "normalize_rewards": True}])
 def test_iteration_matches_oracle(gpu, kw):
     algo, agent, ref, env, cfg = _setup(gpu, **kw)
-    assert torch.equal(agent.flat_params.cpu(), R.flat_params(ref))
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref))
     torch.manual_seed(1234)
     mem = algo.rollout()
     algo.calculate_advantages(mem)
@@ -79,7 +79,7 @@ def test_iteration_matches_oracle(gpu, kw):
     algo.train(mem)
     torch.manual_seed(99)
     R.train(ref, ref_mem, 0)
-    p_eng, p_ref = agent.flat_params.cpu(), R.flat_params(ref)
+    p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
     diff = (p_eng - p_ref).abs()
     n_steps = cfg.epochs * (cfg.num_envs * cfg.horizon // cfg.batch_size)
     lr = cfg.learning_rate
@@ -102,7 +102,7 @@ def test_single_minibatch_update_tight(gpu):
     algo.train(mem)
     torch.manual_seed(8)
     R.train(ref, ref_mem, 0)
-    p_eng, p_ref = agent.flat_params.cpu(), R.flat_params(ref)
+    p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
     close = (p_eng - p_ref).abs() <= 1e-5 * p_ref.abs() + 1e-7
     assert float(close.float().mean()) >= 0.99
     assert float((p_eng - p_ref).abs().max()) <= 2.5e-4
@@ -116,7 +116,7 @@ def test_philox_mode_runs_and_is_reproducible(gpu):
         algo.iterate(verbose=False)
         assert all(map(lambda x: x == x, algo.last_losses))
         assert not torch.equal(before, agent.flat_params)
-        outs.append(agent.flat_params.cpu().clone())
+        outs.append(agent.packed_params().cpu().clone())
     assert torch.equal(outs[0], outs[1]), "philox mode must be bit-reproducible"
 
 
@@ -135,12 +135,12 @@ def test_checkpoint_roundtrip(gpu, tmp_path):
     algo.iterate(verbose=False)
     agent.run.dynamic_config.current_episode = 3
     agent.save()
-    saved = agent.flat_params.clone()
-    m_saved = agent.flat_m.clone()
+    saved = agent.packed_params().clone()
+    m_saved = agent.packed(agent.flat_m).clone()
     agent.flat_params.add_(1.0)
     agent.flat_m.zero_()
     agent.load()
-    assert torch.equal(agent.flat_params, saved)
-    assert torch.equal(agent.flat_m, m_saved)
+    assert torch.equal(agent.packed_params(), saved)
+    assert torch.equal(agent.packed(agent.flat_m), m_saved)
     sd = torch.load(tmp_path / "networks" / "3" / "networks.pth", weights_only=True)
     assert "actor.actor.first_layers.0.weight" in sd and "critic.network.last_layer.bias" in sd

@@ -229,7 +229,7 @@ def _agents(gpu, seed, **kw):
 def test_policy_step_matches_oracle(gpu, hidden, act, n, window):
     run, eng, ref, cfg = _agents(gpu, 3, num_envs=n, hidden=hidden, activation=act, window=window,
                                  batch_size=n)
-    assert torch.equal(eng.flat_params.cpu(), R.flat_params(ref)), "init differs from oracle"
+    assert torch.equal(eng.packed_params().cpu(), R.flat_params(ref)), "init differs from oracle"
     g = torch.Generator().manual_seed(9)
     state = torch.randn(n, window, 17, generator=g)
     eps = torch.randn(n, 6, generator=g)
@@ -290,7 +290,7 @@ def test_minibatch_grad_matches_autograd(gpu, hidden, act, rows_total, b):
     ref.networks.zero_grad()
     (la + lc).backward()
     gref = torch.cat([p.grad.flatten() for p in ref.networks.parameters()])
-    gd = grad.cpu()
+    gd = eng.packed(grad).cpu()
     off = 0
     for name, p in ref.networks.named_parameters():
         k = p.numel()
