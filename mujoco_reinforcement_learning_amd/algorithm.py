@@ -24,6 +24,7 @@ import torch
 
 from . import engine as E
 from .buffer import RolloutBuffer
+from .distributed import DataParallel
 from .features import Run
 
 
@@ -38,10 +39,10 @@ class PPOEngine:
         self.agent = agent
         self.run: Run = environment_helper.run
         self.log = log or _default_log
-        self.pg = process_group
-        self.world = 1
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            self.world = torch.distributed.get_world_size(process_group)
+        self.dp = DataParallel(process_group, mode=getattr(self.run.engine_config, "dp_mode",
+                                                           "local"))
+        self.world = self.dp.world
+        self.dp.broadcast_params(agent.flat_params)  # every replica starts from rank 0's params
         ec, nc = self.run.environment_config, self.run.network_config
         self.buffer = RolloutBuffer(ec.num_envs, ec.maximum_timesteps, nc.input_shape,
                                     ec.window_length, nc.output_shape, agent.device)
@@ -50,6 +51,7 @@ class PPOEngine:
         self.last_mean_reward = float("nan")
         self.timings = {}
         self._rows = None
+        self._count = None
         self._loss_buf = None
 
     # ---- helpers -----------------------------------------------------------------------------
@@ -60,9 +62,16 @@ class PPOEngine:
         return int(self.run.engine_config.seed)
 
     def _eps(self, n: int, a: int):
-        """(eps tensor or None, philox offset) for one (n, A) sampling draw."""
+        """(eps tensor or None, philox offset) for one (n, A) sampling draw.  In exact data
+        parallel mode every rank draws the GLOBAL (N, A) normals and keeps its shard's rows, so
+        the sharded run consumes the reference RNG stream exactly like one process."""
         if self._rng() == "torch":
-            return torch.randn(n, a).to(self.agent.device, non_blocking=True), 0
+            if self.dp.active and self.dp.mode == "exact":
+                lo, hi = self.dp.my_shard(n)
+                eps = torch.randn(self.dp.global_envs(n), a)[lo:hi]
+            else:
+                eps = torch.randn(n, a)
+            return eps.to(self.agent.device, non_blocking=True), 0
         return None, None
 
     # ---- ppo.py:13-60 ----------------------------------------------------------------------
@@ -81,7 +90,7 @@ class PPOEngine:
             else:
                 buf.states[slot].copy_(helper.get_state(test_phase=False).reshape(n, -1))
 
-        seed = self._seed() * 1_000_003 + 17
+        seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
         base_off = self.iteration * (t_len * n * a)
         observe(0)
         eps, _ = self._eps(n, a)
@@ -131,7 +140,10 @@ class PPOEngine:
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
         bs = run.training_config.batch_size
         epochs = int(run.training_config.epochs_per_iteration)
-        batches_per_epoch = int(t_len * n / bs)
+        exact = self.dp.active and self.dp.mode == "exact"
+        # exact DP: ppo.py:97-106 over the GLOBAL buffer (single-process N*T and B)
+        n_glob = self.dp.global_envs(n) if exact else n
+        batches_per_epoch = int(t_len * n_glob / bs)
         if batches_per_epoch <= 0 or float(bs) != int(bs):
             # ppo.py:142: an epoch without a full minibatch divides by len([]) == 0
             raise ZeroDivisionError("division by zero")
@@ -145,25 +157,35 @@ class PPOEngine:
         ppo = run.ppo_config
         clip_lo = 1.0 - ppo.clip_epsilon
         clip_hi = 1.0 + ppo.clip_epsilon
-        b_global = b * self.world
+        if exact:
+            if self._count is None:
+                self._count = torch.zeros(1, dtype=torch.int32, device=dev)
+            if self._rng() != "torch":
+                raise ValueError("exact data-parallel mode replays the reference RNG: rng='torch'")
+        b_global = self.dp.loss_scale(b)
         inv_b = 1.0 / b_global
         inv_ba = 1.0 / (b_global * a)
         states = buf.states
         for epoch in range(epochs):
             if self._rng() == "torch":
-                perm = torch.randperm(n * t_len).to(dev, non_blocking=True)
+                perm = torch.randperm((n_glob if exact else n) * t_len).to(dev, non_blocking=True)
             for i in range(batches_per_epoch):
-                if self._rng() == "torch":
+                count = None
+                if exact:
                     torch.randn(b, a)  # ppo.py:110: agent.act draws a sample it never uses
+                    E.perm_to_rows(perm, i * b, b, n_glob, t_len, self._rows,
+                                   shard=self.dp.my_shard(n), count=self._count)
+                    count = self._count
+                elif self._rng() == "torch":
+                    torch.randn(b, a)  # ppo.py:110
                     E.perm_to_rows(perm, i * b, b, n, t_len, self._rows)
                 else:
-                    E.feistel_rows(self._seed(), self.iteration * epochs + epoch, i * b, b, n,
-                                   t_len, self._rows)
+                    E.feistel_rows(self._seed() + 7919 * self.dp.rank,
+                                   self.iteration * epochs + epoch, i * b, b, n, t_len, self._rows)
                 eng.minibatch_grad(states, buf.actions, buf.logp, buf.advantage, buf.value_target,
                                    self._rows, b, agent.flat_grad, self._loss_buf[epoch, i],
-                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba)
-                if self.world > 1:
-                    torch.distributed.all_reduce(agent.flat_grad, group=self.pg)
+                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba, count=count)
+                self.dp.allreduce_grad(agent.flat_grad)
                 agent.step_both()
         if run.dynamic_config.current_episode < 2500:
             for scheduler in agent.schedulers.values():

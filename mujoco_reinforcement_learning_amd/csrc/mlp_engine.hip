@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 
 #include "common.h"
 
@@ -32,10 +33,8 @@ enum { EPI_FWD = 0, EPI_DX = 1, EPI_PARTIAL = 2 };
 
 struct GemmProblem {
   const float *a;
-  const int32_t *a_rows;  // gather on the stored matrix's row index
   int64_t lda;
   const float *b;
-  const int32_t *b_rows;
   int64_t ldb;
   float *c;
   int64_t ldc;
@@ -56,8 +55,9 @@ struct GemmBatch {
 
 // One operand's share of a k-tile: NV vectors of V floats per thread, staged in registers.
 // KC: the stored rows run along k ([rows][k], transposed on the LDS store); otherwise they run
-// along the tile dimension ([k][rows]).  `rows` gathers the stored row index.  Out-of-range
-// elements load as zero.  V = 4 requires 16-B aligned rows (ld % 4 == 0, aligned base).
+// along the tile dimension ([k][rows]).  load(): bounds-checked, out-of-range elements load as
+// zero; load_full(): the tile is known interior, no checks.  V = 4 requires 16-B aligned rows
+// (ld % 4 == 0, aligned base).
 template <int R, int BK, int NT, int V, bool KC>
 struct OperandTile {
   static constexpr int NV = R * BK / (NT * V);
@@ -86,8 +86,27 @@ struct OperandTile {
       for (int j = 0; j < V; ++j) out[j] = (first + j < lim) ? src[j] : 0.f;
     }
   }
-  __device__ __forceinline__ void load(const float *base, const int32_t *rows, int64_t ld, int r0,
-                                       int rlim, int k0, int kend, int tid) {
+  __device__ __forceinline__ void load_full(const float *base, int64_t ld, int r0, int k0,
+                                            int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int rr, kk;
+      coords(tid + i * NT, rr, kk);
+      const float *src = KC ? base + static_cast<int64_t>(r0 + rr) * ld + (k0 + kk)
+                            : base + static_cast<int64_t>(k0 + kk) * ld + (r0 + rr);
+      if (V == 4) {
+        const float4 x = *reinterpret_cast<const float4 *>(src);
+        v[i][0] = x.x;
+        v[i][1 % V] = x.y;
+        v[i][2 % V] = x.z;
+        v[i][3 % V] = x.w;
+      } else {
+        v[i][0] = src[0];
+      }
+    }
+  }
+  __device__ __forceinline__ void load(const float *base, int64_t ld, int r0, int rlim, int k0,
+                                       int kend, int tid) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       int rr, kk;
@@ -95,7 +114,7 @@ struct OperandTile {
       const int gr = r0 + rr, gk = k0 + kk;
       const bool ok = KC ? (gr < rlim) : (gk < kend);
       if (ok) {
-        const int64_t row = rows ? rows[KC ? gr : gk] : (KC ? gr : gk);
+        const int64_t row = KC ? gr : gk;
         if (KC) span(base + row * ld + gk, gk, kend, v[i]);
         else span(base + row * ld + gr, gr, rlim, v[i]);
       } else {
@@ -124,7 +143,10 @@ struct OperandTile {
 };
 
 // VA / VB = vector width (1 or 4 floats) of the A / B operand's global loads.
-template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI, int VA, int VB>
+// NBUF = 2: double-buffered LDS, one barrier per k-tile; NBUF = 1: one buffer (half the LDS, more
+// blocks per CU), two barriers per k-tile.
+template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI, int VA, int VB,
+          int NBUF>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 32 * TM * WM;
@@ -135,7 +157,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   constexpr int SA = (AMODE == A_MK) ? BM + 1 : BM + 4;
   constexpr int SB = (BMODE == B_NK) ? BN + 1 : BN + 4;
   static_assert(BK % 2 == 0, "BK must be even for 32x32x2");
-  __shared__ __attribute__((aligned(16))) float lds[2 * BK * (SA + SB)];
+  __shared__ __attribute__((aligned(16))) float lds[NBUF * BK * (SA + SB)];
 
   const GemmProblem P = (blockIdx.z == 0) ? gb.p[0] : gb.p[1];
   int M = P.m, N = P.n, K = gb.k;
@@ -162,8 +184,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   OperandTile<BM, BK, NT, VA, AMODE == A_MK> ta;
   OperandTile<BN, BK, NT, VB, BMODE == B_NK> tb;
   auto gload = [&](int k0) {
-    ta.load(P.a, P.a_rows, P.lda, m0, M, k0, kend, tid);
-    tb.load(P.b, P.b_rows, P.ldb, n0, N, k0, kend, tid);
+    // interior tiles (all of these shapes but edge tiles) take the branch-free path
+    const bool kfull = k0 + BK <= kend;
+    if (kfull && m0 + BM <= M) ta.load_full(P.a, P.lda, m0, k0, tid);
+    else ta.load(P.a, P.lda, m0, M, k0, kend, tid);
+    if (kfull && n0 + BN <= N) tb.load_full(P.b, P.ldb, n0, k0, tid);
+    else tb.load(P.b, P.ldb, n0, N, k0, kend, tid);
   };
   auto lstore = [&](int buf) {
     float *As = lds + buf * BK * (SA + SB);
@@ -191,21 +217,33 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
   int cur = 0;
   for (int kt = 0; kt < ntiles; ++kt) {
     if (kt + 1 < ntiles) gload(kbeg + (kt + 1) * BK);
-    const float *As = lds + cur * BK * (SA + SB);
+    const float *As = lds + (NBUF == 2 ? cur : 0) * BK * (SA + SB);
     const float *Bs = As + BK * SA;
+    // fragments for k-pair kp+1 are read from LDS while the MFMAs of kp run
+    float av[TM], bv[TN];
+    auto frag = [&](int kp, float(&a)[TM], float(&b)[TN]) {
+      const int kk = 2 * kp + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[kk * SA + (wm * TM + i) * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[kk * SB + (wn * TN + j) * 32 + (lane & 31)];
+    };
+    frag(0, av, bv);
 #pragma unroll
     for (int kp = 0; kp < BK / 2; ++kp) {
-      const int kk = 2 * kp + (lane >> 5);
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = As[kk * SA + (wm * TM + i) * 32 + (lane & 31)];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = Bs[kk * SB + (wn * TN + j) * 32 + (lane & 31)];
+      float an[TM], bn[TN];
+      if (kp + 1 < BK / 2) frag(kp + 1, an, bn);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      if (kp + 1 < BK / 2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[i] = an[i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[j] = bn[j];
+      }
     }
     if (do_colsum) {
       float s = 0.f;
@@ -213,36 +251,43 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
       for (int kk = 0; kk < BK; ++kk) s += As[kk * SA + tid];
       colacc += s;
     }
-    if (kt + 1 < ntiles) lstore(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
+    if (NBUF == 2) {
+      if (kt + 1 < ntiles) lstore(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    } else if (kt + 1 < ntiles) {
+      __syncthreads();  // every wave is done reading the single buffer
+      lstore(0);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: 32x32 C map (row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31) ----------
   float *cbase = P.c + (EPI == EPI_PARTIAL ? static_cast<int64_t>(split) * gb.slab_stride : 0);
+  auto emit = [&](auto checked) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + (wn * TN + j) * 32 + (lane & 31);
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + (wn * TN + j) * 32 + (lane & 31);
+        float bias = 0.f;
+        if (EPI == EPI_FWD && P.bias && (!checked || col < N)) bias = P.bias[col];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < M && col < N) {
-          const int64_t off = static_cast<int64_t>(row) * P.ldc + col;
-          float v = acc[i][j][r];
-          if (EPI == EPI_FWD) {
-            if (P.bias) v = v + P.bias[col];
-            cbase[off] = act_forward(v, gb.act);
-          } else if (EPI == EPI_DX) {
-            cbase[off] = act_backward(v, P.aux[off], gb.act);
-          } else {
-            cbase[off] = v;
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (!checked || (row < M && col < N)) {
+            const int64_t off = static_cast<int64_t>(row) * P.ldc + col;
+            const float v = acc[i][j][r];
+            if (EPI == EPI_FWD) cbase[off] = act_forward(P.bias ? v + bias : v, gb.act);
+            else if (EPI == EPI_DX) cbase[off] = act_backward(v, P.aux[off], gb.act);
+            else cbase[off] = v;
           }
         }
       }
     }
-  }
+  };
+  if (m0 + BM <= M && n0 + BN <= N) emit(std::false_type{});
+  else emit(std::true_type{});
   if (do_colsum && m0 + tid < M)
     P.colsum[static_cast<int64_t>(split) * gb.slab_stride + m0 + tid] = colacc;
 }
@@ -889,7 +934,7 @@ static bool vec4_ok(const GemmBatch &gb, int nprob, bool operand_a) {
   return true;
 }
 
-template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int NBUF = 2>
 static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   const int tiles = ceil_div(max_m, BM) * ceil_div(max_n, BN);
@@ -898,13 +943,17 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
   const bool va = vec4_ok(gb, nprob, true), vb = vec4_ok(gb, nprob, false);
   constexpr int NTH = 64 * WM * WN;
   if (va && vb)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 4><<<grid, NTH, 0, st>>>(gb);
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 4, NBUF>
+        <<<grid, NTH, 0, st>>>(gb);
   else if (va)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 1><<<grid, NTH, 0, st>>>(gb);
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 1, NBUF>
+        <<<grid, NTH, 0, st>>>(gb);
   else if (vb)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 4><<<grid, NTH, 0, st>>>(gb);
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 4, NBUF>
+        <<<grid, NTH, 0, st>>>(gb);
   else
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 1><<<grid, NTH, 0, st>>>(gb);
+    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 1, NBUF>
+        <<<grid, NTH, 0, st>>>(gb);
   PPO_LAUNCHED();
   const int cls = EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD);
   double bytes = 0;
@@ -917,17 +966,37 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
   return 0;
 }
 
+// Experiment knobs for the large-M tiles (read once): PPO_GEMM_NBUF=1|2 LDS buffers,
+// PPO_GEMM_WIDE=1 for 128x256 tiles (4 waves, 64x128 per wave).
+static int env_knob(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+static const int g_nbuf = env_knob("PPO_GEMM_NBUF", 2);
+static const int g_wide = env_knob("PPO_GEMM_WIDE", 0);
+
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
+static int launch_big(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+  if (g_nbuf == 1)
+    return launch_gemm<TM, TN, WM, WN, AMODE, BMODE, EPI, 1>(gb, nprob, max_m, max_n, st);
+  return launch_gemm<TM, TN, WM, WN, AMODE, BMODE, EPI, 2>(gb, nprob, max_m, max_n, st);
+}
+
 // FWD (A_MK, B_NK) and DX (A_MK, B_KN): rows-major M; big tiles when the row count is large.
 template <int BMODE, int EPI>
 static int run_rowwise(const GemmBatch &gb, int nprob, int rows, int max_n, hipStream_t st) {
-  if (rows >= 8192) return launch_gemm<2, 2, 2, 2, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
+  if (rows >= 8192) {
+    if (g_wide && max_n > 128)
+      return launch_big<2, 4, 2, 2, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
+    return launch_big<2, 2, 2, 2, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
+  }
   return launch_gemm<1, 1, 1, 4, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
 }
 
 static int run_partial(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
   if (max_m <= 32) return launch_gemm<1, 1, 1, 4, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
   if (max_n <= 32) return launch_gemm<1, 1, 4, 1, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
-  return launch_gemm<2, 2, 2, 2, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
+  return launch_big<2, 2, 2, 2, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
 }
 
 static int hpl_for(int width) {
@@ -961,7 +1030,6 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
       kdim = L.in;
       GemmProblem &P = gb.p[np++];
       P.a = (l == 0) ? x : nd.h[l - 1];
-      P.a_rows = (l == 0) ? x_rows : nullptr;
       P.lda = (l == 0) ? ldx : nd.layer[l - 1].out;
       P.b = ctx->params + L.w_off;
       P.ldb = L.in;
@@ -1304,7 +1372,6 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
       Q.a = (l == nd.n_hidden) ? nd.dz : (l == nd.n_hidden - 1 ? nd.g : nd.h[l]);
       Q.lda = L.out;
       Q.b = (l == 0) ? ctx->xg : nd.h[l - 1];
-      Q.b_rows = nullptr;
       Q.ldb = (l == 0) ? ctx->ldx : L.in;
       Q.c = ctx->slabs + L.w_off;
       Q.ldc = L.in;

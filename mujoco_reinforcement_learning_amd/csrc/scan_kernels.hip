@@ -121,7 +121,33 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
   __syncthreads();
   if (tid < EB && env0 + tid < n) {
     RT prev = 0;
-    for (int t = t_len - 1; t >= 0; --t) {
+    // delta and disc do not depend on the carry: compute 8 steps of them from LDS first, then
+    // run the dependent chain over those 8 (same operation order per step as gae_kernel)
+    constexpr int U = 8;
+    int t = t_len - 1;
+    for (; t >= U - 1; t -= U) {
+      RT delta[U];
+      float disc[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = (t - u) * EB + tid;
+        const uint8_t fl = s_fl[e];
+        const float g_nt = gamma_f * ((fl & 1) ? 0.f : 1.f);
+        const float gv = g_nt * s_vn[e];
+        vv[u] = s_v[e];
+        delta[u] = (s_r[e] + static_cast<RT>(gv)) - static_cast<RT>(vv[u]);
+        disc[u] = lg_f * ((fl & 2) ? 0.f : 1.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        prev = delta[u] + prev * static_cast<RT>(disc[u]);
+        const float a = static_cast<float>(prev);
+        const int e = (t - u) * EB + tid;
+        s_vn[e] = a;          // V' slot is dead once read: reuse it for adv
+        s_v[e] = a + vv[u];   // and V's slot for the value target
+      }
+    }
+    for (; t >= 0; --t) {
       const int e = t * EB + tid;
       const uint8_t fl = s_fl[e];
       const float g_nt = gamma_f * ((fl & 1) ? 0.f : 1.f);
@@ -130,8 +156,8 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
       const float disc = lg_f * ((fl & 2) ? 0.f : 1.f);
       prev = delta + prev * static_cast<RT>(disc);
       const float a = static_cast<float>(prev);
-      s_vn[e] = a;                 // V' slot is dead once read: reuse it for adv
-      s_v[e] = a + s_v[e];         // and V's slot for the value target
+      s_vn[e] = a;
+      s_v[e] = a + s_v[e];
     }
   }
   __syncthreads();

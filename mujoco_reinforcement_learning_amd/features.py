@@ -124,10 +124,13 @@ class EngineConfig:
     critic_hidden_shapes: hidden widths of the MLP critic; None = the actor's
          ``linear_hidden_shapes`` (the reference critic.py hard-codes [128, 128]).
     seed: key of the philox streams.
+    dp_mode: "local" (weak scaling: per-rank shuffles, loss / (B*world)) or "exact" (global
+         reference permutation sharded across ranks, loss / B) -- distributed.py.
     """
     rng: str = "torch"
     critic_hidden_shapes: Optional[List[int]] = None
     seed: int = 0
+    dp_mode: str = "local"
 
 
 @dataclass
