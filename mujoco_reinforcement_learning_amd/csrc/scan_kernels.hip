@@ -7,6 +7,8 @@
 // one env per lane with no cross-lane traffic.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float *__restrict__ value
 // of the [T][EB] tile loads (V, V', r, terminated) at once -> LDS (latency paid once, all CUs
 // loading).  Phase 2: EB lanes run the same recurrence as gae_kernel out of LDS.  Phase 3: all
 // threads store adv / vtarget coalesced.  Bit-identical to gae_kernel.  T*EB must fit LDS.
-template <typename RT, int EB>
+template <typename RT, int EB, int IT>  // IT = ceil(T*EB / 256) load slots per thread
 __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ value,
                                                       const float *__restrict__ next_value,
                                                       const RT *__restrict__ reward,
@@ -105,59 +107,64 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
   uint8_t *s_fl = reinterpret_cast<uint8_t *>(s_vn + total);  // bit0 term, bit1 done
   const int env0 = blockIdx.x * EB;
   const int tid = threadIdx.x;
-  for (int e = tid; e < total; e += 256) {
+  // issue every load of this thread before the first LDS store: one HBM latency per block
+  // delta and the discount do not depend on the carry: every thread computes them for its slots
+  // (same operations as gae_kernel), so the serial chain below is one mul + one add per step.
+  float lv[IT];
+  RT ld[IT];
+  uint8_t lfl[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int e = tid + 256 * k;
     const int t = e / EB, c = e - (e / EB) * EB;
     const int env = env0 + c;
-    if (env < n) {
+    if (e < total && env < n) {
       const int64_t idx = static_cast<int64_t>(t) * n + env;
-      s_v[e] = value[idx];
-      s_vn[e] = next_value[idx];
-      s_r[e] = reward[idx];
+      const float v = value[idx];
+      const float vn = next_value[idx];
+      const RT r = reward[idx];
       const uint8_t tm = term[idx];
       const uint8_t dn = done ? done[idx] : tm;
-      s_fl[e] = static_cast<uint8_t>((tm ? 1 : 0) | ((dn || (force_last && t == t_len - 1)) ? 2 : 0));
+      const float g_nt = gamma_f * (tm ? 0.f : 1.f);
+      const float gv = g_nt * vn;
+      lv[k] = v;
+      ld[k] = (r + static_cast<RT>(gv)) - static_cast<RT>(v);
+      lfl[k] = static_cast<uint8_t>((dn || (force_last && t == t_len - 1)) ? 1 : 0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int e = tid + 256 * k;
+    if (e < total && env0 + (e - (e / EB) * EB) < n) {
+      s_v[e] = lv[k];
+      s_r[e] = ld[k];  // delta
+      s_fl[e] = lfl[k];
     }
   }
   __syncthreads();
   if (tid < EB && env0 + tid < n) {
     RT prev = 0;
-    // delta and disc do not depend on the carry: compute 8 steps of them from LDS first, then
-    // run the dependent chain over those 8 (same operation order per step as gae_kernel)
-    constexpr int U = 8;
+    constexpr int U = 8;  // LDS reads of 8 steps issued ahead of their dependent chain
     int t = t_len - 1;
     for (; t >= U - 1; t -= U) {
       RT delta[U];
-      float disc[U], vv[U];
+      float disc[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = (t - u) * EB + tid;
-        const uint8_t fl = s_fl[e];
-        const float g_nt = gamma_f * ((fl & 1) ? 0.f : 1.f);
-        const float gv = g_nt * s_vn[e];
-        vv[u] = s_v[e];
-        delta[u] = (s_r[e] + static_cast<RT>(gv)) - static_cast<RT>(vv[u]);
-        disc[u] = lg_f * ((fl & 2) ? 0.f : 1.f);
+        delta[u] = s_r[e];
+        disc[u] = lg_f * (s_fl[e] ? 0.f : 1.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         prev = delta[u] + prev * static_cast<RT>(disc[u]);
-        const float a = static_cast<float>(prev);
-        const int e = (t - u) * EB + tid;
-        s_vn[e] = a;          // V' slot is dead once read: reuse it for adv
-        s_v[e] = a + vv[u];   // and V's slot for the value target
+        s_vn[(t - u) * EB + tid] = static_cast<float>(prev);
       }
     }
     for (; t >= 0; --t) {
       const int e = t * EB + tid;
-      const uint8_t fl = s_fl[e];
-      const float g_nt = gamma_f * ((fl & 1) ? 0.f : 1.f);
-      const float gv = g_nt * s_vn[e];
-      const RT delta = (s_r[e] + static_cast<RT>(gv)) - static_cast<RT>(s_v[e]);
-      const float disc = lg_f * ((fl & 2) ? 0.f : 1.f);
-      prev = delta + prev * static_cast<RT>(disc);
-      const float a = static_cast<float>(prev);
-      s_vn[e] = a;
-      s_v[e] = a + s_v[e];
+      prev = s_r[e] + prev * static_cast<RT>(lg_f * (s_fl[e] ? 0.f : 1.f));
+      s_vn[e] = static_cast<float>(prev);
     }
   }
   __syncthreads();
@@ -166,8 +173,9 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
     const int env = env0 + c;
     if (env < n) {
       const int64_t idx = static_cast<int64_t>(t) * n + env;
-      adv[idx] = s_vn[e];
-      vtarget[idx] = s_v[e];
+      const float a = s_vn[e];
+      adv[idx] = a;
+      vtarget[idx] = a + s_v[e];  // value_target = advantage + state_value (f32)
     }
   }
 }
@@ -434,38 +442,62 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
   PPO_REQUIRE(n > 0 && t > 0, "ppo_gae: bad shape n=%d t=%d", n, t);
   const float gamma_f = static_cast<float>(gamma);
   const float lg_f = static_cast<float>(lmbda * gamma);
-  // LDS-staged scan: 16 envs per block (>= 256 blocks at N = 4096), halved until the [T][EB]
-  // tile fits 64 KiB; very long horizons fall back to the register-chunked kernel.
+  // LDS-staged scan.  EB envs per block: 16 (>= 256 blocks at N = 4096), 32 once N gives >= 2048
+  // blocks anyway (full 128-B lines per time row); halved until the [T][EB] tile fits 128 KiB and
+  // the per-thread load slots fit 16.  Very long horizons fall back to the register-chunked kernel.
   const size_t per_elem = (reward_is_f64 ? 8 : 4) + 4 + 4 + 1;
-  int eb = 16;
-  while (eb > 1 && static_cast<size_t>(t) * eb * per_elem > 65536) eb >>= 1;
+  static const int eb_knob = [] {  // PPO_GAE_EB overrides envs per block (experiments)
+    const char *v = getenv("PPO_GAE_EB");
+    return v ? atoi(v) : 0;
+  }();
+  int eb = eb_knob > 0 ? eb_knob : ((n >= 65536) ? 32 : 16);
+  while (eb > 1 && (static_cast<size_t>(t) * eb * per_elem > 131072 || t * eb > 16 * 256))
+    eb >>= 1;
   const size_t shm = static_cast<size_t>(t) * eb * per_elem + 16;
-  if (shm <= 65536) {
+  static const int kind = [] {  // PPO_GAE_KERNEL=reg forces the register-chunked scan
+    const char *v = getenv("PPO_GAE_KERNEL");
+    return (v && v[0] == 'r') ? 1 : 0;
+  }();
+  // measured (tools/gae_sweep.py, T=128): LDS-staged wins up to N = 65,536, the register-
+  // chunked scan from N = 262,144 (its ~16k waves stream near 4.2 TB/s)
+  if (kind == 0 && n < 131072 && shm <= 131072 && t * eb <= 16 * 256) {
     const int blocks = ceil_div(n, eb);
+    const int it = ceil_div(static_cast<int64_t>(t) * eb, 256);
     hipStream_t st = as_stream(stream);
-#define PPO_GAE_LDS(RT, EB)                                                                    \
-  gae_lds_kernel<RT, EB><<<blocks, 256, shm, st>>>(value_d, next_value_d,                     \
-                                                  static_cast<const RT *>(reward_d), done_d,   \
-                                                  terminated_d, force_last_done, n, t, gamma_f, \
-                                                  lg_f, adv_d, vtarget_d)
-    if (reward_is_f64) {
+    int rc = 0;
+    auto pick_it = [&](auto rt_tag, auto eb_tag) {
+      using RT = decltype(rt_tag);
+      constexpr int EB = decltype(eb_tag)::value;
+      const RT *r = static_cast<const RT *>(reward_d);
+      auto go = [&](auto kernel) {
+        if (shm > 65536 &&
+            hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(shm)) != hipSuccess) {
+          rc = PPO_EHIP;
+          set_error("ppo_gae: cannot raise dynamic LDS to %zu bytes", shm);
+          return;
+        }
+        kernel<<<blocks, 256, shm, st>>>(value_d, next_value_d, r, done_d, terminated_d,
+                                         force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+      };
+      if (it <= 4) go(gae_lds_kernel<RT, EB, 4>);
+      else if (it <= 8) go(gae_lds_kernel<RT, EB, 8>);
+      else go(gae_lds_kernel<RT, EB, 16>);
+    };
+    auto pick_eb = [&](auto rt_tag) {
       switch (eb) {
-        case 16: PPO_GAE_LDS(double, 16); break;
-        case 8: PPO_GAE_LDS(double, 8); break;
-        case 4: PPO_GAE_LDS(double, 4); break;
-        case 2: PPO_GAE_LDS(double, 2); break;
-        default: PPO_GAE_LDS(double, 1); break;
+        case 32: pick_it(rt_tag, std::integral_constant<int, 32>{}); break;
+        case 16: pick_it(rt_tag, std::integral_constant<int, 16>{}); break;
+        case 8: pick_it(rt_tag, std::integral_constant<int, 8>{}); break;
+        case 4: pick_it(rt_tag, std::integral_constant<int, 4>{}); break;
+        case 2: pick_it(rt_tag, std::integral_constant<int, 2>{}); break;
+        default: pick_it(rt_tag, std::integral_constant<int, 1>{}); break;
       }
-    } else {
-      switch (eb) {
-        case 16: PPO_GAE_LDS(float, 16); break;
-        case 8: PPO_GAE_LDS(float, 8); break;
-        case 4: PPO_GAE_LDS(float, 4); break;
-        case 2: PPO_GAE_LDS(float, 2); break;
-        default: PPO_GAE_LDS(float, 1); break;
-      }
-    }
-#undef PPO_GAE_LDS
+    };
+    if (reward_is_f64) pick_eb(double{});
+    else pick_eb(float{});
+    if (rc) return rc;
     PPO_LAUNCHED();
     return 0;
   }
