@@ -9,9 +9,12 @@ flat gradient per optimizer step).  Inputs are resident in HBM before timing sta
 value = N_gpus * 4096 * 128 * steps / max-over-ranks wall time (weak scaling: envs per GPU fixed).
 
 Also reported on the same JSON line:
-  roofline      dominant kernel class from HIP events recorded live in the timed region
-                (algorithmic FLOPs or bytes per launch / mean launch time vs the MI355X peak)
-  gae_roofline  the GAE scan (north-star >= 40 % HBM target), events around its launch
+  roofline      the dominant kernel instantiation (most device time in the timed region), from
+                HIP events on its dispatch packets (hipExtLaunchKernelGGL) recorded live:
+                algorithmic FLOPs or bytes per launch / mean launch time vs the MI355X peak;
+                `kernel` is its rocprofv3 name; `traffic` = PMC HBM bytes per launch from
+                profiles/traffic.json when present (same command under rocprofv3 --pmc)
+  gae_roofline  the same for the GAE scan (north-star >= 40 % HBM target)
   cpu_baseline  the oracle (oracle/ppo_ref.py, torch-CPU restatement of ppo.py) on a bounded
                 sample of the same workload, on rank 0 at N_gpus = 1 only
 """
@@ -49,7 +52,34 @@ def parse():
     p.add_argument("--cpu-rollout-steps", type=int, default=32)
     p.add_argument("--cpu-epochs", type=int, default=1)
     p.add_argument("--no-timing", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     return p.parse_args()
+
+
+def load_traffic(path):
+    """{kernel name: HBM bytes per launch} from a PMC pass over this same command
+    (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or {}."""
+    if not path or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f).get("bytes_per_launch", {})
+
+
+def roofline(name, c, traffic, force_hbm=False):
+    """Roofline of one kernel instantiation from its live event records: algorithmic FLOPs
+    (MFMA-bound GEMMs) or bytes (everything else) per launch / mean launch duration."""
+    launches = max(c["launches"], 1)
+    avg_s = c["ms"] * 1e-3 / launches
+    mfma = c["class"].startswith("gemm") and not force_hbm
+    if mfma:
+        achieved, peak, unit = c["flops"] / launches / avg_s / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = c["bytes"] / launches / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    return {"bound": "mfma" if mfma else "hbm", "kernel": name, "achieved": achieved,
+            "peak": peak, "unit": unit, "frac": achieved / peak,
+            "traffic": traffic.get(name), "avg_launch_us": avg_s * 1e6, "launches": c["launches"],
+            "algorithmic_per_launch": (c["flops"] if mfma else c["bytes"]) / launches}
 
 
 def cpu_baseline(args, hidden):
@@ -124,22 +154,6 @@ def main():
     helper = SyntheticVecEnvHelper(streams, run, device=dev)
     algo = PPOEngine(helper, agent, log=lambda m: None)
 
-    # GAE launch timing (events on the launch stream around the single GAE kernel)
-    gae_ev = []
-    orig_gae = E.gae
-
-    def timed_gae(*a, **kw):
-        if timing_on[0]:
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            orig_gae(*a, **kw)
-            e.record()
-            gae_ev.append((s, e))
-        else:
-            orig_gae(*a, **kw)
-    timing_on = [False]
-    E.gae = timed_gae
-
     for _ in range(args.warmup):
         algo._iterate()
     torch.cuda.synchronize()
@@ -147,7 +161,6 @@ def main():
         torch.distributed.barrier()
     if not args.no_timing:
         agent.engine.timing(True, capacity=200000)
-        timing_on[0] = True
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -162,8 +175,8 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt)
-    timing_on[0] = False
     classes = agent.engine.timing_read() if not args.no_timing else {}
+    kernels = agent.engine.timing_kernels() if not args.no_timing else {}
     agent.engine.timing(False)
 
     value = world * n * t * args.steps / elapsed
@@ -178,31 +191,18 @@ def main():
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
                        "epochs": args.epochs, "rng": args.rng,
                        "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
-    if classes:
-        dom = max(classes.items(), key=lambda kv: kv[1]["ms"])
-        name, c = dom
-        avg_ms = c["ms"] / max(c["launches"], 1)
-        mfma = name.startswith("gemm")
-        if mfma:
-            achieved = c["flops"] / c["launches"] / (avg_ms * 1e-3) / 1e12
-            peak, unit = PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
-        else:
-            achieved = c["bytes"] / c["launches"] / (avg_ms * 1e-3) / 1e9
-            peak, unit = PEAK_HBM_GBS, "GB/s"
-        line["roofline"] = {"bound": "mfma" if mfma else "hbm", "kernel": name,
-                            "achieved": achieved, "peak": peak, "unit": unit,
-                            "frac": achieved / peak, "traffic": None,
-                            "avg_launch_us": avg_ms * 1e3, "launches": c["launches"]}
-        line["kernel_classes_ms_per_step"] = {k: v["ms"] / args.steps for k, v in classes.items()}
-    if gae_ev:
-        gms = sum(s.elapsed_time(e) for s, e in gae_ev) / len(gae_ev)
-        # algorithmic bytes/element: read V 4 + V' 4 + reward 8 (f64) + terminated 1 (done is
-        # derived in-kernel), write adv 4 + vtarget 4 = 25 B
-        gbytes = 25.0 * n * t
-        ach = gbytes / (gms * 1e-3) / 1e9
-        line["gae_roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
-                                "avg_launch_us": gms * 1e3, "bytes_per_launch": gbytes}
+    if kernels:
+        traffic = load_traffic(args.traffic)
+        name, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])
+        line["roofline"] = roofline(name, c, traffic)
+        gae = {k: v for k, v in kernels.items() if v["class"] == "gae"}
+        if gae:
+            gname, gc = max(gae.items(), key=lambda kv: kv[1]["ms"])
+            line["gae_roofline"] = roofline(gname, gc, traffic, force_hbm=True)
+        line["kernel_classes_ms_per_step"] = {k: v["ms"] / args.steps for k, v in classes.items()
+                                              if v["launches"]}
+        line["kernels_ms_per_step"] = {k: round(v["ms"] / args.steps, 4) for k, v in
+                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
     if rank == 0 and world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, hidden)
     if rank == 0:

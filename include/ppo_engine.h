@@ -164,6 +164,12 @@ int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity);
 int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
                         double *flops, double *bytes);
 const char *ppo_kernel_class_name(int kclass);
+/* The same records per kernel instantiation.  `name` is spelled as rocprofv3 demangles the
+ * kernel (e.g. "gemm_f32_kernel<2, 2, 2, 2, 32, 0, 1, 1, 4, 4, 2>", without "void ppo::" and
+ * the argument list), so a timed kernel maps to one row of a rocprof --stats file; the string
+ * lives as long as the library.  index < 0 returns the number of kernels seen. */
+int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name, int *kclass,
+                          double *total_ms, int64_t *launches, double *flops, double *bytes);
 
 /* ---- harness: synthetic VecEnv dynamics on device + Philox normals ---------------------------
  * The bench/test environment (physics is out of scope): obs' = base_obs + 0.1*a[:, o % A],

@@ -1,6 +1,10 @@
-"""Build libppo_engine.so for gfx950 with hipcc (in-tree, so the .so travels with the repo)."""
+"""Build libppo_engine.so for gfx950 with hipcc (in-tree, so the .so travels with the repo).
+
+Each source compiles to an object in parallel (one hipcc per file), then one link step.
+"""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
@@ -8,22 +12,34 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip"]
-FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 
 
 def build_library(verbose: bool = True) -> str:
     out = os.path.join(HERE, "libppo_engine.so")
     srcs = [os.path.join(HERE, s) for s in SOURCES]
-    deps = srcs + [os.path.join(HERE, "csrc", "common.h"),
-                   os.path.join(ROOT, "include", "ppo_engine.h")]
+    deps = srcs + glob.glob(os.path.join(HERE, "csrc", "*.h")) + \
+        [os.path.join(ROOT, "include", "ppo_engine.h")]
     if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", *srcs]
+    objs, procs = [], []
+    for src in srcs:
+        obj = os.path.join(HERE, "build", os.path.basename(src) + ".o")
+        os.makedirs(os.path.dirname(obj), exist_ok=True)
+        cmd = [hipcc, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((cmd, subprocess.Popen(cmd, cwd=HERE)))
+        objs.append(obj)
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True, cwd=HERE)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.run(link, check=True, cwd=HERE)
     os.replace(out + ".tmp", out)
     return out
 

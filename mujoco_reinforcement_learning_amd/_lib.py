@@ -66,6 +66,9 @@ _SIGNATURES = {
     "ppo_ctx_timing_read": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64),
                                     POINTER(c_double), POINTER(c_double)]),
     "ppo_kernel_class_name": (ctypes.c_char_p, [c_int]),
+    "ppo_ctx_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
+                                      POINTER(c_double), POINTER(c_int64), POINTER(c_double),
+                                      POINTER(c_double)]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

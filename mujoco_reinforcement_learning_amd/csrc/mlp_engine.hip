@@ -16,12 +16,19 @@
 // A11-A13).  Reductions are in a fixed order (split slabs summed 0..S-1), so results are
 // bit-reproducible run to run.
 #include <algorithm>
+#include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <new>
+#include <string>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
+#include "timing.h"
 
 namespace ppo {
 
@@ -385,6 +392,11 @@ struct UpdateHeadArgs {
   float *logstd_part;            // (splits, A)
   float *loss_part;              // (splits, 2): sum over rows of actor / critic loss terms
   int splits;
+  // fused head weight gradient (update_head_q4_kernel<NJ, true>): per split, at hw_part +
+  // split * hw_stride: actor W (A, da) | actor b (A) at off_ba | critic W (dc) at off_wc |
+  // critic b at off_bc
+  float *hw_part;
+  int hw_stride, off_ba, off_wc, off_bc;
 };
 
 // Fast head: 4 lanes per row, 16 rows per wave pass, D = 16*NJ columns (actor and critic last
@@ -393,12 +405,20 @@ struct UpdateHeadArgs {
 // (same address for the 16 rows -> LDS broadcast) plus a 2-step shuffle over the row's 4 lanes.
 // Per-action work (tanh, log-prob, dz) is spread over the 4 lanes: lane qd owns actions
 // a = 4k + qd.  Same torch formulas as update_head_kernel below.
-template <int NJ>
+// FW (A <= kFusedHeadAct): also accumulate the head layer's weight gradient, dW = dz^T H_L and
+// db = sum dz per net, over the block's rows while H_L is hot in L1/L2 -- lane owns float4
+// column chunk c = lane + 64u of both nets -- so the split-K head GEMM (a second full read of
+// H_L) is not launched.  Waves combine in a fixed order; one partial per block.
+constexpr int kFusedHeadAct = 8;
+template <int NJ, bool FW>
 __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
   constexpr int D = 16 * NJ;
   constexpr int KA = kMaxAct / 4;
+  constexpr int CH = (4 * NJ + 63) / 64;  // float4 column chunks per lane (fused wgrad)
+  constexpr int AF = FW ? kFusedHeadAct : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float red[4][kMaxAct + 2];
+  __shared__ float dvs[4][16];
   const int A = q.act_dim;
   float *wsh = smem;                   // (A + 1) x D: actor head rows, then the critic row
   float *lps = smem + (A + 1) * D;     // [4 waves][16 rows][kMaxAct] log-probs
@@ -417,6 +437,14 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
 #pragma unroll
   for (int k = 0; k < KA; ++k) ls_acc[k] = 0.f;
   float la_acc = 0.f, lc_acc = 0.f;
+  float4 wa_acc[CH][AF], wc_acc[CH];
+  float b_acc = 0.f;  // lane a < A: actor bias a; lane A: critic bias
+#pragma unroll
+  for (int u = 0; u < CH; ++u) {
+    wc_acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int a = 0; a < AF; ++a) wa_acc[u][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   for (int base = r0 + 16 * wid; base < r1; base += 64) {  // wave-uniform trip count
     const int j = base + r;
     const bool valid = j < r1;
@@ -547,6 +575,82 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
             make_float4(act_backward(dv * wv.x, h[t].x, q.act), act_backward(dv * wv.y, h[t].y, q.act),
                         act_backward(dv * wv.z, h[t].z, q.act), act_backward(dv * wv.w, h[t].w, q.act));
     }
+    if constexpr (FW) {
+      // head dW += dz^T H over this pass's 16 rows (dz rows of invalid j are exactly 0 and are
+      // skipped anyway); H re-read by columns from L1/L2
+      if (qd == 0) dvs[wid][r] = valid ? dv : 0.f;
+      __threadfence_block();
+      const int nrow = min(16, r1 - base);
+      for (int rr = 0; rr < nrow; ++rr) {
+        const int64_t jj = base + rr;
+        const float *dzr = dzs + (wid * 16 + rr) * kMaxAct;
+        const float dvr = dvs[wid][rr];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int c = lane + 64 * u;
+          if (c < 4 * NJ) {
+            const float4 ha4 = reinterpret_cast<const float4 *>(q.ha + jj * D)[c];
+            const float4 hc4 = reinterpret_cast<const float4 *>(q.hc + jj * D)[c];
+#pragma unroll
+            for (int a = 0; a < AF; ++a) {
+              if (a < A) {
+                const float dz = dzr[a];
+                wa_acc[u][a].x = fmaf(dz, ha4.x, wa_acc[u][a].x);
+                wa_acc[u][a].y = fmaf(dz, ha4.y, wa_acc[u][a].y);
+                wa_acc[u][a].z = fmaf(dz, ha4.z, wa_acc[u][a].z);
+                wa_acc[u][a].w = fmaf(dz, ha4.w, wa_acc[u][a].w);
+              }
+            }
+            wc_acc[u].x = fmaf(dvr, hc4.x, wc_acc[u].x);
+            wc_acc[u].y = fmaf(dvr, hc4.y, wc_acc[u].y);
+            wc_acc[u].z = fmaf(dvr, hc4.z, wc_acc[u].z);
+            wc_acc[u].w = fmaf(dvr, hc4.w, wc_acc[u].w);
+          }
+        }
+        if (lane < A) b_acc += dzr[lane];
+        else if (lane == A) b_acc += dvr;
+      }
+    }
+  }
+  if constexpr (FW) {
+    // combine the 4 waves' partials in wave order through LDS (the staged head weights and the
+    // log-prob scratch are dead now), then one coalesced partial per block
+    __syncthreads();
+    float *acc_sh = wsh;   // (A + 1) x D
+    float *bias_sh = lps;  // A + 1
+    for (int w = 0; w < 4; ++w) {
+      if (wid == w) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int c = lane + 64 * u;
+          if (c < 4 * NJ) {
+#pragma unroll
+            for (int a = 0; a <= AF; ++a) {
+              if (a <= A) {
+                const float4 v = (a == A || a == AF) ? wc_acc[u] : wa_acc[u][a < AF ? a : 0];
+                float4 *dst = reinterpret_cast<float4 *>(acc_sh + a * D) + c;
+                if (w == 0) {
+                  *dst = v;
+                } else {
+                  const float4 o = *dst;
+                  *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+                }
+              }
+            }
+          }
+        }
+        if (lane <= A) bias_sh[lane] = (w == 0) ? b_acc : bias_sh[lane] + b_acc;
+      }
+      __syncthreads();
+    }
+    float *dst = q.hw_part + static_cast<int64_t>(blockIdx.x) * q.hw_stride;
+    for (int i = tid; i < A * D / 4; i += 256)
+      reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(acc_sh)[i];
+    for (int i = tid; i < D / 4; i += 256)
+      reinterpret_cast<float4 *>(dst + q.off_wc)[i] =
+          reinterpret_cast<const float4 *>(acc_sh + A * D)[i];
+    if (tid < A && q.ba) dst[q.off_ba + tid] = bias_sh[tid];
+    if (tid == 0) dst[q.off_bc] = bias_sh[A];
   }
   // ---- fixed-order reductions: over the 16 rows of the wave (lane bits 2..5), then waves 0..3
 #pragma unroll
@@ -761,22 +865,50 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceArgs q) {
     const ReduceSeg &g = q.seg[s];
     const int64_t off = i - g.dst;
     const int k0 = (g.nsplit * chunk) / 4, k1 = (g.nsplit * (chunk + 1)) / 4;
+    // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per
+    // thread; the association is fixed, so the result is still deterministic run to run.
     if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
         reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
       const float *src = g.src + off;
+      float4 acc1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      int k = k0;
 #pragma unroll 4
-      for (int k = k0; k < k1; ++k) {
+      for (; k + 1 < k1; k += 2) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+        const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+        acc1.x += u.x;
+        acc1.y += u.y;
+        acc1.z += u.z;
+        acc1.w += u.w;
+      }
+      if (k < k1) {
         const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
         acc.x += v.x;
         acc.y += v.y;
         acc.z += v.z;
         acc.w += v.w;
       }
-    } else if (off >= 0) {  // tail of a tensor / unaligned source; padding stays zero
+      acc = make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
+    } else if (off >= 0) {  // tail of a tensor / unaligned source (logstd partials, 1-wide
+                            // biases); padding stays zero.  8 strided partial sums per element.
       float a4[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int e = 0; e < 4; ++e)
-        if (off + e < g.len)
-          for (int k = k0; k < k1; ++k) a4[e] += g.src[k * g.stride + off + e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (off + e >= g.len) continue;
+        const float *src = g.src + off + e;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int k = k0;
+        for (; k + 7 < k1; k += 8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += src[static_cast<int64_t>(k + j) * g.stride];
+        }
+        for (; k < k1; ++k) s[0] += src[static_cast<int64_t>(k) * g.stride];
+        a4[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+      }
       acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
     }
   }
@@ -835,50 +967,30 @@ struct NetDesc {
 };
 
 // ============================================================================================
-// Per-kernel-class timing: HIP events recorded around each launch ON the launch stream while
-// enabled (bench.py's live roofline), read back after the timed region.
+// Per-launch timing (timing.h): event pairs on each dispatch packet while enabled (bench.py's
+// live roofline), read back after the timed region.
 // ============================================================================================
-enum {
-  KC_GEMM_FWD = 0,
-  KC_GEMM_DGRAD,
-  KC_GEMM_WGRAD,
-  KC_UPDATE_HEAD,
-  KC_POLICY_HEAD,
-  KC_REDUCE,
-  KC_GATHER,
-  KC_COUNT
-};
-static const char *const kClassNames[KC_COUNT] = {"gemm_fwd",    "gemm_dgrad",  "gemm_wgrad",
-                                                  "update_head", "policy_head", "reduce_slabs",
-                                                  "gather_states"};
+static const char *const kClassNames[KC_COUNT] = {
+    "gemm_fwd",     "gemm_dgrad", "gemm_wgrad", "update_head", "policy_head", "reduce_slabs",
+    "gather_states", "gae",       "adam",       "normalize_rows", "obs", "minibatch_rows",
+    "env_harness"};
 
-struct Timing {
-  bool on = false;
-  int capacity = 0;
-  int used = 0;
-  hipEvent_t *ev = nullptr;  // 2 per record
-  int *cls = nullptr;
-  double *flops = nullptr, *bytes = nullptr;
-  double ms[KC_COUNT] = {}, fl[KC_COUNT] = {}, by[KC_COUNT] = {};
-  int64_t n[KC_COUNT] = {};
-};
+thread_local Timing *g_tim = nullptr;
+Timing *g_free_tim = nullptr;
 
-static thread_local Timing *g_tim = nullptr;  // set by the entry point for the call's duration
-
-static inline void tim_begin(hipStream_t st) {
-  Timing *t = g_tim;
-  if (t && t->used < t->capacity) (void)hipEventRecord(t->ev[2 * t->used], st);
-}
-
-static inline void tim_end(int cls, double flops, double bytes, hipStream_t st) {
-  Timing *t = g_tim;
-  if (t && t->used < t->capacity) {
-    (void)hipEventRecord(t->ev[2 * t->used + 1], st);
-    t->cls[t->used] = cls;
-    t->flops[t->used] = flops;
-    t->bytes[t->used] = bytes;
-    ++t->used;
-  }
+const char *intern_name(const char *fmt, ...) {
+  static std::mutex mu;
+  static std::deque<std::string> names;
+  char buf[160];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lock(mu);
+  for (const std::string &s : names)
+    if (s == buf) return s.c_str();
+  names.emplace_back(buf);
+  return names.back().c_str();
 }
 
 }  // namespace ppo
@@ -891,6 +1003,8 @@ struct ppo_ctx {
   float *params;
   float *slabs;          // (kSlabSplits, total_params)
   float *head_part;      // logstd partials (kHeadSplits, A) + loss partials (kHeadSplits, 2)
+  float *head_w_part;    // fused head dW/db partials (kHeadSplits, hw_stride), UpdateHeadArgs
+  int hw_stride, hw_off_ba, hw_off_wc, hw_off_bc;
   float *xg;             // gathered minibatch states (max_rows, ldx)
   int ldx;               // round_up(W*O, 4)
   void *arena;
@@ -934,35 +1048,39 @@ static bool vec4_ok(const GemmBatch &gb, int nprob, bool operand_a) {
   return true;
 }
 
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int NBUF, int VA, int VB>
+static void launch_gemm_v(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t st) {
+  TimRec rec{EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD),
+             nullptr, 0.0, 0.0};
+  if (tim_active()) {
+    rec.name = intern_name("gemm_f32_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", TM, TN,
+                           WM, WN, kGemmBK, AMODE, BMODE, EPI, VA, VB, NBUF);
+    rec.flops = gemm_flops(gb, nprob, EPI);
+    for (int i = 0; i < nprob; ++i) {  // algorithmic: A + B read once, C written once (f32)
+      const GemmProblem &p = gb.p[i];
+      rec.bytes += 4.0 * (static_cast<double>(p.m) * gb.k + static_cast<double>(gb.k) * p.n +
+                          static_cast<double>(p.m) * p.n * (EPI == EPI_DX ? 2 : 1));
+    }
+  }
+  launch_k(rec, gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, VA, VB, NBUF>, grid,
+           dim3(64 * WM * WN), 0, st, gb);
+}
+
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int NBUF = 2>
 static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   const int tiles = ceil_div(max_m, BM) * ceil_div(max_n, BN);
   dim3 grid(tiles, EPI == EPI_PARTIAL ? gb.splits : 1, nprob);
-  tim_begin(st);
   const bool va = vec4_ok(gb, nprob, true), vb = vec4_ok(gb, nprob, false);
-  constexpr int NTH = 64 * WM * WN;
   if (va && vb)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 4, NBUF>
-        <<<grid, NTH, 0, st>>>(gb);
+    launch_gemm_v<TM, TN, WM, WN, AMODE, BMODE, EPI, NBUF, 4, 4>(gb, nprob, grid, st);
   else if (va)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 4, 1, NBUF>
-        <<<grid, NTH, 0, st>>>(gb);
+    launch_gemm_v<TM, TN, WM, WN, AMODE, BMODE, EPI, NBUF, 4, 1>(gb, nprob, grid, st);
   else if (vb)
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 4, NBUF>
-        <<<grid, NTH, 0, st>>>(gb);
+    launch_gemm_v<TM, TN, WM, WN, AMODE, BMODE, EPI, NBUF, 1, 4>(gb, nprob, grid, st);
   else
-    gemm_f32_kernel<TM, TN, WM, WN, kGemmBK, AMODE, BMODE, EPI, 1, 1, NBUF>
-        <<<grid, NTH, 0, st>>>(gb);
+    launch_gemm_v<TM, TN, WM, WN, AMODE, BMODE, EPI, NBUF, 1, 1>(gb, nprob, grid, st);
   PPO_LAUNCHED();
-  const int cls = EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD);
-  double bytes = 0;
-  for (int i = 0; i < nprob; ++i) {  // algorithmic: A + B read once, C written once (f32)
-    const GemmProblem &p = gb.p[i];
-    bytes += 4.0 * (static_cast<double>(p.m) * gb.k + static_cast<double>(gb.k) * p.n +
-                    static_cast<double>(p.m) * p.n * (EPI == EPI_DX ? 2 : 1));
-  }
-  tim_end(cls, gemm_flops(gb, nprob, EPI), bytes, st);
   return 0;
 }
 
@@ -1117,6 +1235,16 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
   ctx->total_params = off;
   ws_floats += align_up(static_cast<int64_t>(kSlabSplits) * off, kWsAlign);
   ws_floats += align_up(static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2), kWsAlign);
+  {
+    const int A = cfg->act_dim;
+    const int da = ctx->net[0].layer[ctx->net[0].n_hidden].in;
+    const int dc = ctx->net[1].layer[ctx->net[1].n_hidden].in;
+    ctx->hw_off_ba = static_cast<int>(align_up(static_cast<int64_t>(A) * da, 4));
+    ctx->hw_off_wc = ctx->hw_off_ba + static_cast<int>(align_up(A, 4));
+    ctx->hw_off_bc = ctx->hw_off_wc + static_cast<int>(align_up(dc, 4));
+    ctx->hw_stride = ctx->hw_off_bc + 4;
+  }
+  ws_floats += align_up(static_cast<int64_t>(kHeadSplits) * ctx->hw_stride, kWsAlign);
   const int ldx = static_cast<int>(align_up(din, 4));
   ws_floats += align_up(R * ldx, kWsAlign);
   void *arena = nullptr;
@@ -1144,6 +1272,8 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
   p += align_up(static_cast<int64_t>(kSlabSplits) * off, kWsAlign);
   ctx->head_part = p;
   p += align_up(static_cast<int64_t>(kHeadSplits) * (cfg->act_dim + 2), kWsAlign);
+  ctx->head_w_part = p;
+  p += align_up(static_cast<int64_t>(kHeadSplits) * ctx->hw_stride, kWsAlign);
   ctx->xg = p;
   ctx->ldx = ldx;
   p += align_up(R * ldx, kWsAlign);
@@ -1161,9 +1291,11 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
 extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
   if (!ctx) return 0;
   (void)hipSetDevice(ctx->device);
+  if (g_free_tim == &ctx->tim) g_free_tim = nullptr;
   for (int i = 0; i < 2 * ctx->tim.capacity; ++i) (void)hipEventDestroy(ctx->tim.ev[i]);
   delete[] ctx->tim.ev;
   delete[] ctx->tim.cls;
+  delete[] ctx->tim.kname;
   delete[] ctx->tim.flops;
   delete[] ctx->tim.bytes;
   if (ctx->arena) (void)hipFree(ctx->arena);
@@ -1244,16 +1376,16 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   q.mean = mean_d;
   const int hpl = hpl_for(std::max(q.da, q.dc));
   const int grid = ceil_div(n, 4);
-  tim_begin(st);
-  if (hpl == 4) policy_head_kernel<4><<<grid, 256, 0, st>>>(q);
-  else if (hpl == 8) policy_head_kernel<8><<<grid, 256, 0, st>>>(q);
-  else policy_head_kernel<16><<<grid, 256, 0, st>>>(q);
-  PPO_LAUNCHED();
   const int na = q.act_dim;
-  tim_end(KC_POLICY_HEAD, 2.0 * n * (static_cast<double>(q.da) * na + q.dc),
-          4.0 * n * (q.da + q.dc + (eps_d ? na : 0) + (action_d ? na : 0) + (mean_d ? na : 0) +
-                     (logp_d ? 1 : 0) + (value_d ? 1 : 0)),
-          st);
+  const TimRec rec{KC_POLICY_HEAD,
+                   tim_active() ? intern_name("policy_head_kernel<%d>", hpl) : nullptr,
+                   2.0 * n * (static_cast<double>(q.da) * na + q.dc),
+                   4.0 * n * (q.da + q.dc + (eps_d ? na : 0) + (action_d ? na : 0) +
+                              (mean_d ? na : 0) + (logp_d ? 1 : 0) + (value_d ? 1 : 0))};
+  if (hpl == 4) launch_k(rec, policy_head_kernel<4>, dim3(grid), dim3(256), 0, st, q);
+  else if (hpl == 8) launch_k(rec, policy_head_kernel<8>, dim3(grid), dim3(256), 0, st, q);
+  else launch_k(rec, policy_head_kernel<16>, dim3(grid), dim3(256), 0, st, q);
+  PPO_LAUNCHED();
   return 0;
 }
 
@@ -1273,11 +1405,10 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   const bool both[2] = {true, true};
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
-  tim_begin(st);
-  gather_states_kernel<<<ceil_div(static_cast<int64_t>(b) * ctx->ldx, 256), 256, 0, st>>>(
-      states_d, rows_d, count_d, b, din, ctx->ldx, ctx->xg);
+  launch_k(TimRec{KC_GATHER, "gather_states_kernel", 0.0, 4.0 * b * (2.0 * din + 1)},
+           gather_states_kernel, dim3(ceil_div(static_cast<int64_t>(b) * ctx->ldx, 256)),
+           dim3(256), 0, st, states_d, rows_d, count_d, b, din, ctx->ldx, ctx->xg);
   PPO_LAUNCHED();
-  tim_end(KC_GATHER, 0.0, 4.0 * b * (2.0 * din + 1), st);
   if (int rc = forward_hidden(ctx, both, ctx->xg, nullptr, b, count_d, st, ctx->ldx)) return rc;
 
   // ---- heads: loss, dz, dH_L -------------------------------------------------------------
@@ -1317,39 +1448,58 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   u.loss_part = ctx->head_part + static_cast<int64_t>(kHeadSplits) * A;
   u.splits = head_splits;
   const int hpl = hpl_for(std::max(u.da, u.dc));
-  tim_begin(st);
   const int nj = (u.da == u.dc && u.da % 16 == 0) ? u.da / 16 : 0;
   const bool aligned = reinterpret_cast<uintptr_t>(u.ha) % 16 == 0 &&
                        reinterpret_cast<uintptr_t>(u.hc) % 16 == 0;
-  if (aligned && (nj == 2 || nj == 4 || nj == 8 || nj == 16 || nj == 32)) {
+  const bool q4 = aligned && (nj == 2 || nj == 4 || nj == 8 || nj == 16 || nj == 32);
+  const bool fused_head_w = q4 && A <= kFusedHeadAct;  // head dW/db inside the head kernel
+  u.hw_part = ctx->head_w_part;
+  u.hw_stride = ctx->hw_stride;
+  u.off_ba = ctx->hw_off_ba;
+  u.off_wc = ctx->hw_off_wc;
+  u.off_bc = ctx->hw_off_bc;
+  // algorithmic FLOPs: head forward + dH_L (+ head dW when fused); bytes per row: read H_L
+  // (actor, critic), action, 4 scalars + row index; write dH_L (actor, critic) and dz (A + 1)
+  const TimRec rec{KC_UPDATE_HEAD,
+                   !tim_active() ? nullptr
+                   : q4 ? intern_name("update_head_q4_kernel<%d, %s>", nj,
+                                      fused_head_w ? "true" : "false")
+                        : intern_name("update_head_kernel<%d>", hpl),
+                   2.0 * b * ((fused_head_w ? 3.0 : 2.0) * (A * u.da + u.dc)),
+                   4.0 * b * (2.0 * u.da + 2.0 * u.dc + 2.0 * A + 6.0)};
+  if (q4) {
     const size_t shm = sizeof(float) * ((A + 1) * static_cast<size_t>(u.da) + 2 * 4 * 16 * kMaxAct);
     auto launch = [&](auto kernel) -> int {
       if (shm > 64 * 1024)
         PPO_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
                                         hipFuncAttributeMaxDynamicSharedMemorySize,
                                         static_cast<int>(shm)));
-      kernel<<<head_splits, 256, shm, st>>>(u);
+      launch_k(rec, kernel, dim3(head_splits), dim3(256), static_cast<uint32_t>(shm), st, u);
       return 0;
     };
     int rc = 0;
-    if (nj == 2) rc = launch(update_head_q4_kernel<2>);
-    else if (nj == 4) rc = launch(update_head_q4_kernel<4>);
-    else if (nj == 8) rc = launch(update_head_q4_kernel<8>);
-    else if (nj == 16) rc = launch(update_head_q4_kernel<16>);
-    else rc = launch(update_head_q4_kernel<32>);
+    if (fused_head_w) {
+      if (nj == 2) rc = launch(update_head_q4_kernel<2, true>);
+      else if (nj == 4) rc = launch(update_head_q4_kernel<4, true>);
+      else if (nj == 8) rc = launch(update_head_q4_kernel<8, true>);
+      else if (nj == 16) rc = launch(update_head_q4_kernel<16, true>);
+      else rc = launch(update_head_q4_kernel<32, true>);
+    } else {
+      if (nj == 2) rc = launch(update_head_q4_kernel<2, false>);
+      else if (nj == 4) rc = launch(update_head_q4_kernel<4, false>);
+      else if (nj == 8) rc = launch(update_head_q4_kernel<8, false>);
+      else if (nj == 16) rc = launch(update_head_q4_kernel<16, false>);
+      else rc = launch(update_head_q4_kernel<32, false>);
+    }
     if (rc) return rc;
   } else if (hpl == 4) {
-    update_head_kernel<4><<<head_splits, 256, 0, st>>>(u);
+    launch_k(rec, update_head_kernel<4>, dim3(head_splits), dim3(256), 0, st, u);
   } else if (hpl == 8) {
-    update_head_kernel<8><<<head_splits, 256, 0, st>>>(u);
+    launch_k(rec, update_head_kernel<8>, dim3(head_splits), dim3(256), 0, st, u);
   } else {
-    update_head_kernel<16><<<head_splits, 256, 0, st>>>(u);
+    launch_k(rec, update_head_kernel<16>, dim3(head_splits), dim3(256), 0, st, u);
   }
   PPO_LAUNCHED();
-  // algorithmic bytes per row: read H_L (actor, critic), action, 4 scalars + row index;
-  // write dH_L (actor, critic) and dz (A + 1)
-  tim_end(KC_UPDATE_HEAD, 2.0 * b * (3.0 * A * u.da + 3.0 * u.dc),
-          4.0 * b * (2.0 * u.da + 2.0 * u.dc + 2.0 * A + 6.0), st);
 
   // ---- weight gradients, split-K over rows, deepest layer first ---------------------------
   const int splits = std::min(kSlabSplits, std::max(1, b / 64));
@@ -1426,7 +1576,9 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   };
   const int depth = std::max(NA.n_hidden, NC.n_hidden);
   for (int s = 0; s <= depth; ++s) {
-    if (int rc = partial(s)) return rc;       // dW of layer n_hidden - s (needs its input)
+    // dW of layer n_hidden - s (needs its input); the head's is already in head_w_part
+    if (!(s == 0 && fused_head_w))
+      if (int rc = partial(s)) return rc;
     if (int rc = input_grad(s)) return rc;    // then overwrite that input with its gradient
   }
 
@@ -1445,19 +1597,21 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
     }
     for (int l = 0; l <= nd.n_hidden; ++l) {
       const LayerDesc &L = nd.layer[l];
+      const bool head_fused = fused_head_w && l == nd.n_hidden;
       ReduceSeg &g = r.seg[ns++];
       g.dst = L.w_off;
       g.len = static_cast<int64_t>(L.out) * L.in;
-      g.src = ctx->slabs + L.w_off;
-      g.stride = P;
-      g.nsplit = splits;
+      g.src = head_fused ? ctx->head_w_part + (z == 0 ? 0 : ctx->hw_off_wc) : ctx->slabs + L.w_off;
+      g.stride = head_fused ? ctx->hw_stride : P;
+      g.nsplit = head_fused ? head_splits : splits;
       if (L.b_off >= 0) {
         ReduceSeg &gbs = r.seg[ns++];
         gbs.dst = L.b_off;
         gbs.len = L.out;
-        gbs.src = ctx->slabs + L.b_off;
-        gbs.stride = P;
-        gbs.nsplit = splits;
+        gbs.src = head_fused ? ctx->head_w_part + (z == 0 ? ctx->hw_off_ba : ctx->hw_off_bc)
+                             : ctx->slabs + L.b_off;
+        gbs.stride = head_fused ? ctx->hw_stride : P;
+        gbs.nsplit = head_fused ? head_splits : splits;
       }
     }
   }
@@ -1471,11 +1625,10 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   r.act_dim = A;
   r.ent_coef = entropy_coef;
   r.loss_out = loss_d;
-  tim_begin(st);
-  reduce_slabs_kernel<<<ceil_div(P, 256), 256, 0, st>>>(r);  // P % 16 == 0
+  launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(splits) * P,
+                  4.0 * (static_cast<double>(splits) + 1) * P},
+           reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);  // P % 16 == 0
   PPO_LAUNCHED();
-  tim_end(KC_REDUCE, static_cast<double>(splits) * P, 4.0 * (static_cast<double>(splits) + 1) * P,
-          st);
   return 0;
 }
 
@@ -1486,10 +1639,12 @@ extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
     for (int i = 0; i < 2 * t.capacity; ++i) (void)hipEventDestroy(t.ev[i]);
     delete[] t.ev;
     delete[] t.cls;
+    delete[] t.kname;
     delete[] t.flops;
     delete[] t.bytes;
     t.ev = new hipEvent_t[2 * capacity];
     t.cls = new int[capacity];
+    t.kname = new const char *[capacity];
     t.flops = new double[capacity];
     t.bytes = new double[capacity];
     for (int i = 0; i < 2 * capacity; ++i) PPO_HIP_TRY(hipEventCreate(&t.ev[i]));
@@ -1498,10 +1653,43 @@ extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
   if (enable) {
     t.used = 0;
     for (int c = 0; c < KC_COUNT; ++c) t.ms[c] = t.fl[c] = t.by[c] = 0, t.n[c] = 0;
+    t.per_kernel.clear();
   }
   t.on = enable != 0 && t.capacity > 0;
+  if (t.on) g_free_tim = &t;
+  else if (g_free_tim == &t) g_free_tim = nullptr;
   return 0;
 }
+
+namespace ppo {
+// Folds pending records into the per-class and per-kernel totals (host sync on their events).
+static int timing_fold(Timing &t) {
+  for (int i = 0; i < t.used; ++i) {
+    PPO_HIP_TRY(hipEventSynchronize(t.ev[2 * i + 1]));
+    float ms = 0.f;
+    PPO_HIP_TRY(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
+    const int c = t.cls[i];
+    t.ms[c] += ms;
+    t.fl[c] += t.flops[i];
+    t.by[c] += t.bytes[i];
+    t.n[c] += 1;
+    const char *name = t.kname[i] ? t.kname[i] : kClassNames[c];
+    KernelTotals *k = nullptr;
+    for (KernelTotals &e : t.per_kernel)
+      if (e.name == name) k = &e;
+    if (!k) {
+      t.per_kernel.push_back(KernelTotals{name, c, 0.0, 0.0, 0.0, 0});
+      k = &t.per_kernel.back();
+    }
+    k->ms += ms;
+    k->fl += t.flops[i];
+    k->by += t.bytes[i];
+    k->n += 1;
+  }
+  t.used = 0;
+  return 0;
+}
+}  // namespace ppo
 
 extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
                                    double *flops, double *bytes) {
@@ -1509,20 +1697,30 @@ extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, i
   if (kclass < 0) return KC_COUNT;
   PPO_REQUIRE(kclass < KC_COUNT, "ppo_ctx_timing_read: class %d out of range", kclass);
   Timing &t = ctx->tim;
-  for (int i = 0; i < t.used; ++i) {  // fold pending records (host sync on their events)
-    PPO_HIP_TRY(hipEventSynchronize(t.ev[2 * i + 1]));
-    float ms = 0.f;
-    PPO_HIP_TRY(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
-    t.ms[t.cls[i]] += ms;
-    t.fl[t.cls[i]] += t.flops[i];
-    t.by[t.cls[i]] += t.bytes[i];
-    t.n[t.cls[i]] += 1;
-  }
-  t.used = 0;
+  if (int rc = timing_fold(t)) return rc;
   if (total_ms) *total_ms = t.ms[kclass];
   if (launches) *launches = t.n[kclass];
   if (flops) *flops = t.fl[kclass];
   if (bytes) *bytes = t.by[kclass];
+  return 0;
+}
+
+extern "C" int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name, int *kclass,
+                                     double *total_ms, int64_t *launches, double *flops,
+                                     double *bytes) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_kernel: null ctx");
+  Timing &t = ctx->tim;
+  if (int rc = timing_fold(t)) return rc;
+  const int count = static_cast<int>(t.per_kernel.size());
+  if (index < 0) return count;
+  PPO_REQUIRE(index < count, "ppo_ctx_timing_kernel: index %d out of range [0, %d)", index, count);
+  const KernelTotals &k = t.per_kernel[index];
+  if (name) *name = k.name;
+  if (kclass) *kclass = k.cls;
+  if (total_ms) *total_ms = k.ms;
+  if (launches) *launches = k.n;
+  if (flops) *flops = k.fl;
+  if (bytes) *bytes = k.by;
   return 0;
 }
 

@@ -11,6 +11,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "timing.h"
 
 namespace ppo {
 
@@ -433,6 +434,11 @@ extern "C" int ppo_abi_version(void) { return PPO_ABI_VERSION; }
 
 extern "C" const char *ppo_last_error(void) { return g_err; }
 
+// algorithmic bytes: read V, V', reward, terminated (+ done when given), write adv, vtarget
+static double gae_bytes(size_t reward_bytes, bool has_done, int n, int t) {
+  return static_cast<double>(n) * t * (4 + 4 + reward_bytes + 1 + (has_done ? 1 : 0) + 4 + 4);
+}
+
 extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const void *reward_d,
                        int reward_is_f64, const uint8_t *done_d, const uint8_t *terminated_d,
                        int force_last_done, int n, int t, double gamma, double lmbda,
@@ -464,12 +470,13 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
     const int blocks = ceil_div(n, eb);
     const int it = ceil_div(static_cast<int64_t>(t) * eb, 256);
     hipStream_t st = as_stream(stream);
+    FreeTimingScope timing_scope;
     int rc = 0;
     auto pick_it = [&](auto rt_tag, auto eb_tag) {
       using RT = decltype(rt_tag);
       constexpr int EB = decltype(eb_tag)::value;
       const RT *r = static_cast<const RT *>(reward_d);
-      auto go = [&](auto kernel) {
+      auto go = [&](auto kernel, int it_max) {
         if (shm > 65536 &&
             hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -478,12 +485,19 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
           set_error("ppo_gae: cannot raise dynamic LDS to %zu bytes", shm);
           return;
         }
-        kernel<<<blocks, 256, shm, st>>>(value_d, next_value_d, r, done_d, terminated_d,
-                                         force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+        const TimRec rec{KC_GAE,
+                         tim_active() ? intern_name("gae_lds_kernel<%s, %d, %d>",
+                                                    sizeof(RT) == 8 ? "double" : "float", EB,
+                                                    it_max)
+                                      : nullptr,
+                         0.0, gae_bytes(sizeof(RT), done_d != nullptr, n, t)};
+        launch_k(rec, kernel, dim3(blocks), dim3(256), static_cast<uint32_t>(shm), st, value_d,
+                 next_value_d, r, done_d, terminated_d, force_last_done, n, t, gamma_f, lg_f,
+                 adv_d, vtarget_d);
       };
-      if (it <= 4) go(gae_lds_kernel<RT, EB, 4>);
-      else if (it <= 8) go(gae_lds_kernel<RT, EB, 8>);
-      else go(gae_lds_kernel<RT, EB, 16>);
+      if (it <= 4) go(gae_lds_kernel<RT, EB, 4>, 4);
+      else if (it <= 8) go(gae_lds_kernel<RT, EB, 8>, 8);
+      else go(gae_lds_kernel<RT, EB, 16>, 16);
     };
     auto pick_eb = [&](auto rt_tag) {
       switch (eb) {
@@ -502,14 +516,18 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
     return 0;
   }
   const int grid = ceil_div(n, 64);
+  FreeTimingScope timing_scope;
+  const TimRec rec{KC_GAE,
+                   reward_is_f64 ? "gae_kernel<double, 16>" : "gae_kernel<float, 16>", 0.0,
+                   gae_bytes(reward_is_f64 ? 8 : 4, done_d != nullptr, n, t)};
   if (reward_is_f64)
-    gae_kernel<double, 16><<<grid, 64, 0, as_stream(stream)>>>(
-        value_d, next_value_d, static_cast<const double *>(reward_d), done_d, terminated_d,
-        force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+    launch_k(rec, gae_kernel<double, 16>, dim3(grid), dim3(64), 0, as_stream(stream), value_d,
+             next_value_d, static_cast<const double *>(reward_d), done_d, terminated_d,
+             force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
   else
-    gae_kernel<float, 16><<<grid, 64, 0, as_stream(stream)>>>(
-        value_d, next_value_d, static_cast<const float *>(reward_d), done_d, terminated_d,
-        force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+    launch_k(rec, gae_kernel<float, 16>, dim3(grid), dim3(64), 0, as_stream(stream), value_d,
+             next_value_d, static_cast<const float *>(reward_d), done_d, terminated_d,
+             force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
   PPO_LAUNCHED();
   return 0;
 }
@@ -518,12 +536,16 @@ extern "C" int ppo_normalize_rows(void *x_d, int is_f64, int n, int t, double sc
                                   void *stream) {
   PPO_REQUIRE(x_d && n > 0 && t > 0, "ppo_normalize_rows: bad args");
   const int grid = ceil_div(n, 64);
+  FreeTimingScope timing_scope;
+  const double elems = static_cast<double>(n) * t;  // algorithmic: read once, write once
   if (is_f64)
-    normalize_rows_kernel<double><<<grid, 64, 0, as_stream(stream)>>>(static_cast<double *>(x_d),
-                                                                      n, t, scale);
+    launch_k(TimRec{KC_ROWS, "normalize_rows_kernel<double>", 0.0, 16.0 * elems},
+             normalize_rows_kernel<double>, dim3(grid), dim3(64), 0, as_stream(stream),
+             static_cast<double *>(x_d), n, t, scale);
   else
-    normalize_rows_kernel<float><<<grid, 64, 0, as_stream(stream)>>>(static_cast<float *>(x_d), n,
-                                                                     t, scale);
+    launch_k(TimRec{KC_ROWS, "normalize_rows_kernel<float>", 0.0, 8.0 * elems},
+             normalize_rows_kernel<float>, dim3(grid), dim3(64), 0, as_stream(stream),
+             static_cast<float *>(x_d), n, t, scale);
   PPO_LAUNCHED();
   return 0;
 }
@@ -534,12 +556,17 @@ extern "C" int ppo_obs_window_push(double *window_d, const void *obs_d, int obs_
   PPO_REQUIRE(window_d && obs_d && n > 0 && o > 0 && w > 0, "ppo_obs_window_push: bad args");
   const int64_t total = static_cast<int64_t>(n) * o;
   const int grid = ceil_div(total, 256);
+  FreeTimingScope timing_scope;
+  // algorithmic: read the new obs and the W-1 kept slots, write W slots (f64 window)
+  const double by = static_cast<double>(total) * ((obs_is_f64 ? 8 : 4) + 8.0 * (2 * w - 1));
   if (obs_is_f64)
-    obs_window_push_kernel<double><<<grid, 256, 0, as_stream(stream)>>>(
-        window_d, static_cast<const double *>(obs_d), reset_d, all_reset, n, o, w);
+    launch_k(TimRec{KC_OBS, "obs_window_push_kernel<double>", 0.0, by},
+             obs_window_push_kernel<double>, dim3(grid), dim3(256), 0, as_stream(stream),
+             window_d, static_cast<const double *>(obs_d), reset_d, all_reset, n, o, w);
   else
-    obs_window_push_kernel<float><<<grid, 256, 0, as_stream(stream)>>>(
-        window_d, static_cast<const float *>(obs_d), reset_d, all_reset, n, o, w);
+    launch_k(TimRec{KC_OBS, "obs_window_push_kernel<float>", 0.0, by},
+             obs_window_push_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
+             window_d, static_cast<const float *>(obs_d), reset_d, all_reset, n, o, w);
   PPO_LAUNCHED();
   return 0;
 }
@@ -559,8 +586,10 @@ extern "C" int ppo_obs_normalize(const double *window_d, float *state_d, int n, 
                 "ppo_obs_normalize: bounds must be ascending within [0, O]");
   }
   const int64_t total = static_cast<int64_t>(n) * w;
-  obs_normalize_kernel<<<ceil_div(total, 128), 128, 0, as_stream(stream)>>>(window_d, state_d, n,
-                                                                            o, w, tab, normalize);
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_OBS, "obs_normalize_kernel", 0.0, 12.0 * total * o}, obs_normalize_kernel,
+           dim3(ceil_div(total, 128)), dim3(128), 0, as_stream(stream), window_d, state_d, n, o,
+           w, tab, normalize);
   PPO_LAUNCHED();
   return 0;
 }
@@ -573,9 +602,12 @@ extern "C" int ppo_synthetic_env_step(const float *base_obs_d, const float *base
                   reward_out_d && term_out_d && n > 0 && o > 0 && a > 0,
               "ppo_synthetic_env_step: bad args");
   const int64_t total = static_cast<int64_t>(n) * o;
-  synthetic_env_step_kernel<<<ceil_div(total, 256), 256, 0, as_stream(stream)>>>(
-      base_obs_d, base_reward_d, base_term_d, action_d, n, o, a, obs_out_d, reward_out_d,
-      term_out_d);
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_ENV, "synthetic_env_step_kernel", 0.0,
+                  12.0 * total + 4.0 * n * a + 14.0 * n},
+           synthetic_env_step_kernel, dim3(ceil_div(total, 256)), dim3(256), 0,
+           as_stream(stream), base_obs_d, base_reward_d, base_term_d, action_d, n, o, a,
+           obs_out_d, reward_out_d, term_out_d);
   PPO_LAUNCHED();
   return 0;
 }
@@ -584,7 +616,9 @@ extern "C" int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, i
                                  void *stream) {
   PPO_REQUIRE(out_d && n >= 0, "ppo_philox_normal: bad args");
   if (n == 0) return 0;
-  philox_normal_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(seed, offset, out_d, n);
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_ENV, "philox_normal_kernel", 0.0, 4.0 * n}, philox_normal_kernel,
+           dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), seed, offset, out_d, n);
   PPO_LAUNCHED();
   return 0;
 }
@@ -597,12 +631,15 @@ extern "C" int ppo_perm_to_rows(const int64_t *perm_d, int64_t start, int b, int
   if (shard_lo < shard_hi) {
     PPO_REQUIRE(count_d && shard_lo >= 0 && shard_hi <= n_envs,
                 "ppo_perm_to_rows: bad shard [%d, %d)", shard_lo, shard_hi);
-    perm_to_rows_shard_kernel<<<1, 1024, 0, as_stream(stream)>>>(perm_d, start, b, n_envs, t,
-                                                                 shard_lo, shard_hi, rows_d,
-                                                                 count_d);
+    FreeTimingScope timing_scope;
+    launch_k(TimRec{KC_PERM, "perm_to_rows_shard_kernel", 0.0, 12.0 * b},
+             perm_to_rows_shard_kernel, dim3(1), dim3(1024), 0, as_stream(stream), perm_d, start,
+             b, n_envs, t, shard_lo, shard_hi, rows_d, count_d);
   } else {
-    perm_to_rows_kernel<<<ceil_div(b, 256), 256, 0, as_stream(stream)>>>(perm_d, start, b, n_envs,
-                                                                         t, rows_d);
+    FreeTimingScope timing_scope;
+    launch_k(TimRec{KC_PERM, "perm_to_rows_kernel", 0.0, 12.0 * b}, perm_to_rows_kernel,
+             dim3(ceil_div(b, 256)), dim3(256), 0, as_stream(stream), perm_d, start, b, n_envs,
+             t, rows_d);
   }
   PPO_LAUNCHED();
   return 0;
@@ -617,8 +654,10 @@ extern "C" int ppo_feistel_rows(uint64_t seed, uint64_t epoch, int64_t start, in
   int bits = 1;
   while ((1ll << bits) < total) ++bits;
   const int half = (bits + 1) / 2;
-  feistel_rows_kernel<<<ceil_div(b, 256), 256, 0, as_stream(stream)>>>(seed, epoch, start, b,
-                                                                       n_envs, t, half, rows_d);
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_PERM, "feistel_rows_kernel", 0.0, 4.0 * b}, feistel_rows_kernel,
+           dim3(ceil_div(b, 256)), dim3(256), 0, as_stream(stream), seed, epoch, start, b, n_envs,
+           t, half, rows_d);
   PPO_LAUNCHED();
   return 0;
 }
@@ -629,9 +668,11 @@ extern "C" int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, in
                         float eps, void *stream) {
   PPO_REQUIRE(p_d && g_d && m_d && v_d && n > 0 && n_actor >= 0 && n_actor <= n,
               "ppo_adam: bad args");
-  adam_kernel<<<ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
-      p_d, g_d, m_d, v_d, n, n_actor, neg_step_actor, neg_step_critic, one_minus_beta1, beta2,
-      one_minus_beta2, bc2_sqrt, eps);
+  FreeTimingScope timing_scope;
+  // algorithmic: read p, g, m, v and write p, m, v (f32) = 28 B/param
+  launch_k(TimRec{KC_ADAM, "adam_kernel", 0.0, 28.0 * n}, adam_kernel, dim3(ceil_div(n, 256)),
+           dim3(256), 0, as_stream(stream), p_d, g_d, m_d, v_d, n, n_actor, neg_step_actor,
+           neg_step_critic, one_minus_beta1, beta2, one_minus_beta2, bc2_sqrt, eps);
   PPO_LAUNCHED();
   return 0;
 }

@@ -143,6 +143,25 @@ class Engine:
                          "bytes": by.value}
         return out
 
+    def timing_kernels(self) -> dict:
+        """Same records per kernel instantiation, keyed by the rocprofv3 kernel name:
+        {name: {"class": ..., "ms", "launches", "flops", "bytes"}}."""
+        out = {}
+        n_k = self.lib.ppo_ctx_timing_kernel(self._ctx, -1, None, None, None, None, None, None)
+        check(min(n_k, 0))
+        for i in range(n_k):
+            name, cls = ctypes.c_char_p(), ctypes.c_int()
+            ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            cnt = ctypes.c_int64()
+            check(self.lib.ppo_ctx_timing_kernel(self._ctx, i, ctypes.byref(name),
+                                                 ctypes.byref(cls), ctypes.byref(ms),
+                                                 ctypes.byref(cnt), ctypes.byref(fl),
+                                                 ctypes.byref(by)))
+            out[name.value.decode()] = {
+                "class": self.lib.ppo_kernel_class_name(cls.value).decode(), "ms": ms.value,
+                "launches": cnt.value, "flops": fl.value, "bytes": by.value}
+        return out
+
     # ---- A11-A13 -------------------------------------------------------------------------
     def minibatch_grad(self, states, actions, old_logp, adv, vtarget, rows, b: int, grad, loss,
                        clip_lo: float, clip_hi: float, entropy_coef: float, inv_b: float,

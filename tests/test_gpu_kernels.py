@@ -301,3 +301,41 @@ def test_minibatch_grad_matches_autograd(gpu, hidden, act, rows_total, b):
         off += k
     torch.testing.assert_close(loss.cpu()[1], lc.detach(), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(loss.cpu()[0], la.detach(), rtol=1e-4, atol=1e-6)
+
+
+def test_per_kernel_timing_records(gpu):
+    """ppo_ctx_timing_kernel: one record per kernel instantiation, named as rocprofv3 spells it,
+    covering ctx entry points (GEMMs, heads) and ctx-free ones (GAE, Adam) while enabled."""
+    E = _E()
+    run, eng, ref, cfg = _agents(gpu, 4, num_envs=256, hidden=(64, 64), activation="relu",
+                                 batch_size=128)
+    g = torch.Generator().manual_seed(3)
+    n = 256
+    states = torch.randn(n, 17, generator=g).to(gpu)
+    actions = torch.randn(n, 6, generator=g).to(gpu)
+    vec = [torch.randn(n, generator=g).to(gpu) for _ in range(3)]
+    rows = torch.randperm(n, generator=g)[:128].to(torch.int32).to(gpu)
+    grad = torch.empty(eng.engine.n_params, device=gpu)
+    loss = torch.empty(2, device=gpu)
+    eng.engine.timing(True, capacity=1024)
+    eng.engine.minibatch_grad(states, actions, vec[0], vec[1], vec[2], rows, 128, grad, loss,
+                              0.9, 1.1, 1e-4, 1.0 / 128, 1.0 / (128 * 6))
+    v = torch.randn(16, 32, device=gpu)
+    r = torch.randn(16, 32, device=gpu, dtype=torch.float64)
+    term = torch.zeros(16, 32, device=gpu, dtype=torch.bool)
+    adv, vt = torch.empty_like(v), torch.empty_like(v)
+    E.gae(v, v, r, term, 0.99, 0.98, adv, vt)
+    kernels = eng.engine.timing_kernels()
+    eng.engine.timing(False)
+    classes = {rec["class"] for rec in kernels.values()}
+    assert {"gemm_fwd", "gemm_wgrad", "gemm_dgrad", "update_head", "reduce_slabs",
+            "gather_states", "gae"} <= classes, classes
+    gemms = [k for k, rec in kernels.items() if rec["class"].startswith("gemm")]
+    assert all(k.startswith("gemm_f32_kernel<") and k.count(",") == 10 for k in gemms), gemms
+    for k, rec in kernels.items():
+        assert rec["launches"] >= 1 and rec["ms"] > 0.0, (k, rec)
+    gae = [rec for rec in kernels.values() if rec["class"] == "gae"]
+    assert len(gae) == 1 and gae[0]["bytes"] == 16 * 32 * 25
+    # disabled timing records nothing further
+    E.gae(v, v, r, term, 0.99, 0.98, adv, vt)
+    assert eng.engine.timing_kernels() == kernels
