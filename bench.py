@@ -31,6 +31,7 @@ import torch  # noqa: E402
 
 METRIC = "env-steps/sec (whole node) HalfCheetah-v4 4096 envs at 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
+PEAK_BF16_MFMA_TFLOPS = 2516.6  # MI355X_MICROARCH.md: bf16 dense (2.5 PF; sparsity excluded)
 PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec
 
 
@@ -47,6 +48,9 @@ def parse():
     p.add_argument("--batch", type=int, default=65536)
     p.add_argument("--epochs", type=int, default=10)
     p.add_argument("--rng", choices=("philox", "torch"), default="philox")
+    p.add_argument("--precision", choices=("f32", "bf16"), default="f32",
+                   help="fc-layer GEMM precision: f32 (parity with the reference) or bf16 "
+                        "(bf16 operands, f32 accumulate; BASELINE.json configs[1])")
     p.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     p.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     p.add_argument("--cpu-rollout-steps", type=int, default=32)
@@ -67,13 +71,17 @@ def load_traffic(path):
 
 
 def roofline(name, c, traffic, force_hbm=False):
-    """Roofline of one kernel instantiation from its live event records: algorithmic FLOPs
-    (MFMA-bound GEMMs) or bytes (everything else) per launch / mean launch duration."""
+    """Roofline of one kernel instantiation from its live event records.  The bound is the roof
+    the kernel's own algorithmic work hits first: MFMA (FLOPs / dense peak of its dtype) or HBM
+    (bytes / 8 TB/s); achieved = that work per launch / mean launch duration."""
     launches = max(c["launches"], 1)
     avg_s = c["ms"] * 1e-3 / launches
-    mfma = c["class"].startswith("gemm") and not force_hbm
+    peak_f = PEAK_BF16_MFMA_TFLOPS if "bf16" in name else PEAK_FP32_MFMA_TFLOPS
+    t_mfma = c["flops"] / (peak_f * 1e12)
+    t_hbm = c["bytes"] / (PEAK_HBM_GBS * 1e9)
+    mfma = c["class"].startswith("gemm") and t_mfma >= t_hbm and not force_hbm
     if mfma:
-        achieved, peak, unit = c["flops"] / launches / avg_s / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        achieved, peak, unit = c["flops"] / launches / avg_s / 1e12, peak_f, "TFLOP/s"
     else:
         achieved, peak, unit = c["bytes"] / launches / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
     return {"bound": "mfma" if mfma else "hbm", "kernel": name, "achieved": achieved,
@@ -147,7 +155,7 @@ def main():
     n, t = args.num_envs, args.horizon
     run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
                    hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
-                   seed=rank)
+                   seed=rank, precision=args.precision)
     torch.manual_seed(0)  # identical initial parameters on every rank
     agent = PPOEngineAgent(run, device=dev)
     streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
@@ -182,7 +190,7 @@ def main():
     value = world * n * t * args.steps / elapsed
     line = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",
             "config": {"workload": (f"HalfCheetah-v4 shapes: {n} envs/GPU x {t} steps, obs "
                                     f"{args.obs_dim}, act {args.act_dim}, actor+critic "

@@ -39,6 +39,8 @@ extern "C" {
 #define PPO_EINVAL (-22)
 #define PPO_EHIP (-5)
 #define PPO_MAX_LAYERS 8
+#define PPO_PREC_F32 0  /* GEMMs on v_mfma_f32_32x32x2_f32: the reference's f32 (parity mode) */
+#define PPO_PREC_BF16 1 /* GEMM operands rounded to bf16, f32 accumulate (BASELINE configs[1]) */
 
 /* NetworkConfig.activation_class (features.py:41-54; main.py uses ReLU). */
 enum { PPO_ACT_RELU = 0, PPO_ACT_TANH = 1, PPO_ACT_ELU = 2 };
@@ -100,6 +102,17 @@ int ppo_obs_normalize(const double *window_d, float *state_d, int n, int o, int 
 int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                     uint64_t offset, float *action_d, float *logp_d, float *value_d, float *mean_d,
                     void *stream);
+/* Philox sampling in ppo_policy_step uses offset + *counter_d when counter_d (a device uint64)
+ * is set, read when the kernel runs rather than when it is launched: a rollout captured once in
+ * a hipGraph replays with fresh noise after the host bumps the counter.  NULL restores plain
+ * `offset`.  (No reference counterpart: the reference draws from the host generator.) */
+int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
+/* GEMM precision of every fc-layer GEMM the ctx launches (rollout forward, update forward,
+ * dgrad, wgrad): PPO_PREC_F32 (default; parity with the f32 reference) or PPO_PREC_BF16 (bf16
+ * operands on v_mfma_f32_32x32x16_bf16, f32 accumulation, f32 activations / params / Adam in
+ * HBM -- the "bf16 GEMMs with fp32 accumulate and fp32 master params" of SURVEY.md s8(d)).
+ * Heads, losses, GAE and Adam stay f32 either way. */
+int ppo_ctx_set_precision(ppo_ctx *ctx, int prec);
 
 /* ---- A6/A9: per-env standardisation over T (ppo.py:66-69 rewards, :81-88 advantage/target) ----
  * x_d: time-major (T, N) (element (n,t) at t*N+n), f32 or f64 (is_f64).  x <- (x-mean_T)/std_T*scale

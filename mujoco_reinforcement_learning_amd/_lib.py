@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 PPO_MAX_LAYERS = 8
 ACT_CODES = {"relu": 0, "tanh": 1, "elu": 2}
+PREC_CODES = {"f32": 0, "bf16": 1}  # PPO_PREC_* (include/ppo_engine.h)
 
 
 class NetCfg(ctypes.Structure):
@@ -62,6 +63,8 @@ _SIGNATURES = {
     "ppo_synthetic_env_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_philox_normal": (c_int, [c_uint64, c_uint64, c_void_p, c_int64, c_void_p]),
+    "ppo_ctx_set_rng_counter": (c_int, [c_void_p, c_void_p]),
+    "ppo_ctx_set_precision": (c_int, [c_void_p, c_int]),
     "ppo_ctx_timing": (c_int, [c_void_p, c_int, c_int]),
     "ppo_ctx_timing_read": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64),
                                     POINTER(c_double), POINTER(c_double)]),

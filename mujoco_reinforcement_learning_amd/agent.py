@@ -154,6 +154,7 @@ class PPOEngineAgent:
         self.flat_params = move_to_flat(self.networks, self.device, self.engine.param_offsets(),
                                         self.engine.n_params)
         self.engine.bind(self.flat_params)
+        self.engine.set_precision(getattr(run.engine_config, "precision", "f32"))
         self.flat_grad = torch.zeros_like(self.flat_params)
         self.flat_m = torch.zeros_like(self.flat_params)
         self.flat_v = torch.zeros_like(self.flat_params)

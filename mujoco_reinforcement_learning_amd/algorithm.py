@@ -53,6 +53,9 @@ class PPOEngine:
         self._rows = None
         self._count = None
         self._loss_buf = None
+        self._graph = None        # captured rollout (philox + graph_safe helper)
+        self._graph_warm = False
+        self._rng_counter = None
 
     # ---- helpers -----------------------------------------------------------------------------
     def _rng(self) -> str:
@@ -75,8 +78,40 @@ class PPOEngine:
         return None, None
 
     # ---- ppo.py:13-60 ----------------------------------------------------------------------
+    def _graph_ok(self) -> bool:
+        return (self._rng() == "philox" and
+                bool(getattr(self.run.engine_config, "rollout_graph", False)) and
+                bool(getattr(self.environment_helper, "graph_safe", False)) and
+                bool(getattr(self.environment_helper, "writes_into_buffer", False)))
+
     @torch.no_grad()
     def rollout(self) -> RolloutBuffer:
+        buf = self.buffer
+        n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        if not self._graph_ok():
+            return self._rollout_steps(base_off=self.iteration * (t_len * n * a))
+        # hipGraph path: the Philox offset base lives in a device counter that the policy head
+        # reads at run time, so one captured T-step rollout replays with fresh noise; the
+        # sampled values are identical to the eager path (offset = base + t*N*A either way).
+        eng = self.agent.engine
+        if self._rng_counter is None:
+            self._rng_counter = torch.zeros(1, dtype=torch.int64, device=self.agent.device)
+            eng.set_rng_counter(self._rng_counter)
+        self._rng_counter.fill_(self.iteration * (t_len * n * a))
+        if self._graph is None:
+            if not self._graph_warm:  # first call eager: lazy allocations happen outside capture
+                self._graph_warm = True
+                return self._rollout_steps(base_off=0)
+            torch.cuda.synchronize(self.agent.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_steps(base_off=0)
+            self._graph = g
+        self._graph.replay()
+        self.environment_helper.t = t_len  # the host-side step counter the replay skipped
+        return buf
+
+    def _rollout_steps(self, base_off: int) -> RolloutBuffer:
         helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
         helper.reset()
@@ -91,7 +126,6 @@ class PPOEngine:
                 buf.states[slot].copy_(helper.get_state(test_phase=False).reshape(n, -1))
 
         seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
-        base_off = self.iteration * (t_len * n * a)
         observe(0)
         eps, _ = self._eps(n, a)
         eng.policy_step(buf.states[0], eps=eps, seed=seed, offset=base_off, action=buf.actions[0],

@@ -79,7 +79,10 @@ template <typename F, typename... Args>
 inline void launch_k(const TimRec &rec, F kernel, dim3 grid, dim3 block, uint32_t shm,
                      hipStream_t st, Args... args) {
   Timing *t = g_tim;
-  if (t && t->used < t->capacity) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  // a launch being captured into a hipGraph (graph-replayed rollout) is not event-timed
+  if (t && t->used < t->capacity && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+      cap == hipStreamCaptureStatusNone) {
     const int i = t->used++;
     t->cls[i] = rec.cls;
     t->kname[i] = rec.name;

@@ -81,6 +81,7 @@ class Engine:
         self.n_critic = int(self.lib.ppo_param_count(self._ctx, 1))
         self.n_params = int(self.lib.ppo_param_count(self._ctx, -1))
         self._params = None
+        self.precision = "f32"
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
@@ -123,6 +124,22 @@ class Engine:
         check(self.lib.ppo_policy_step(self._ctx, ptr(state), n, ptr(eps), seed, offset,
                                        ptr(action), ptr(logp), ptr(value), ptr(mean),
                                        _stream(self.device)))
+
+    def set_precision(self, precision: str) -> None:
+        """GEMM precision: "f32" (parity with the reference, default) or "bf16" (bf16 operands,
+        f32 accumulation; activations, params and optimizer state stay f32)."""
+        if precision not in _lib.PREC_CODES:
+            raise ValueError(f"unknown precision {precision!r}; use one of {sorted(_lib.PREC_CODES)}")
+        check(self.lib.ppo_ctx_set_precision(self._ctx, _lib.PREC_CODES[precision]))
+        self.precision = precision
+
+    def set_rng_counter(self, counter: Optional[torch.Tensor]) -> None:
+        """Philox offset base read on the device at kernel run time (int64 scalar tensor on this
+        device, or None): lets a graph-captured rollout replay with fresh noise."""
+        if counter is not None:
+            _need(counter, "counter", torch.int64, (1,), self.device)
+        check(self.lib.ppo_ctx_set_rng_counter(self._ctx, ptr(counter)))
+        self._rng_counter = counter  # keep the buffer alive while the ctx may read it
 
     # ---- measurement ---------------------------------------------------------------------
     def timing(self, enable: bool, capacity: int = 65536) -> None:

@@ -51,6 +51,7 @@ class SyntheticVecEnvHelper:
     """EnvironmentHelper over the synthetic device VecEnv."""
 
     writes_into_buffer = True  # step(reward_out=, terminated_out=) / get_state(out=)
+    graph_safe = True          # every step is device work on fixed buffers (hipGraph-capturable)
 
     def __init__(self, streams: Optional[dict] = None, run: Optional[Run] = None,
                  device: Optional[torch.device] = None, seed: int = 0, p_terminate: float = 0.0):

@@ -126,11 +126,19 @@ class EngineConfig:
     seed: key of the philox streams.
     dp_mode: "local" (weak scaling: per-rank shuffles, loss / (B*world)) or "exact" (global
          reference permutation sharded across ranks, loss / B) -- distributed.py.
+    rollout_graph: with rng="philox" and a device-resident VecEnv helper (``graph_safe``),
+         capture the T-step rollout once as a hipGraph and replay it each iteration (no host
+         launch overhead per step; the Philox offset base is a device counter).
+    precision: "f32" (every GEMM in f32, parity with the reference) or "bf16" (fc-layer GEMM
+         operands rounded to bf16 with f32 accumulation; params, optimizer state, activations,
+         heads, losses and GAE stay f32) -- BASELINE.json configs[1].
     """
     rng: str = "torch"
     critic_hidden_shapes: Optional[List[int]] = None
     seed: int = 0
     dp_mode: str = "local"
+    rollout_graph: bool = True
+    precision: str = "f32"
 
 
 @dataclass

@@ -442,3 +442,38 @@ def adam_reference_step(p, g, m, v, step: int, lr: float, beta1=0.9, beta2=0.999
 
 def math_log_sqrt_2pi() -> float:
     return math.log(math.sqrt(2 * math.pi))
+
+
+# ---- bf16 GEMM emulation (engine precision "bf16"; not a reference behaviour) ----------------
+def _bf(x: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32) and back to f32."""
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+class _BF16Linear(torch.autograd.Function):
+    """y = bf16(x) @ bf16(W)^T + b with f32 accumulation; backward GEMMs also on bf16-rounded
+    operands (dx = bf16(dy) @ bf16(W), dW = bf16(dy)^T @ bf16(x)); db = sum dy in f32 (the
+    engine sums the f32 dY before rounding) -- what gemm_bf16_kernel computes for every hidden
+    fc layer."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        y = _bf(x) @ _bf(w).t()
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g = _bf(gy)
+        return g @ _bf(w), g.t() @ _bf(x), (gy.sum(0) if ctx.has_b else None)
+
+
+def use_bf16_hidden_gemms(agent: "RefAgent") -> None:
+    """Switch the hidden Linear layers of both nets to the bf16-operand GEMM (the heads stay f32,
+    as the engine's head kernels are f32)."""
+    for net in (agent.networks["actor"].actor, agent.networks["critic"].network):
+        for mod in net.first_layers:
+            if isinstance(mod, nn.Linear):
+                mod.forward = (lambda m: (lambda x: _BF16Linear.apply(x, m.weight, m.bias)))(mod)
