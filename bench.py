@@ -48,9 +48,10 @@ def parse():
     p.add_argument("--batch", type=int, default=65536)
     p.add_argument("--epochs", type=int, default=10)
     p.add_argument("--rng", choices=("philox", "torch"), default="philox")
-    p.add_argument("--precision", choices=("f32", "bf16"), default="f32",
-                   help="fc-layer GEMM precision: f32 (parity with the reference) or bf16 "
-                        "(bf16 operands, f32 accumulate; BASELINE.json configs[1])")
+    p.add_argument("--precision", choices=("f32", "bf16"), default="bf16",
+                   help="fc-layer GEMM precision: bf16 (default; bf16 operands, f32 accumulate, f32 "
+                        "master params -- BASELINE.json configs[1]) or f32 (bit-level parity "
+                        "mode with the reference's f32 CPU trainer)")
     p.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     p.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     p.add_argument("--cpu-rollout-steps", type=int, default=32)
