@@ -184,6 +184,13 @@ const char *ppo_kernel_class_name(int kclass);
 int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name, int *kclass,
                           double *total_ms, int64_t *launches, double *flops, double *bytes);
 
+/* Diagnostics (no reference counterpart): enable=1 makes the ctx's fused bf16 minibatch kernel
+ * run its stamped instantiation, which sums s_memtime deltas per phase segment (wave 0 of each
+ * workgroup, 11 slots) into a device buffer; enable=0 synchronises, copies the last launch's
+ * (2 nets, G workgroups, 11) uint64 cycle sums to host_out (up to max_values) and returns the
+ * number of values, then restores the product kernel.  ReLU networks only. */
+int ppo_ctx_phase_stamps(ppo_ctx *ctx, int enable, uint64_t *host_out, int max_values);
+
 /* ---- harness: synthetic VecEnv dynamics on device + Philox normals ---------------------------
  * The bench/test environment (physics is out of scope): obs' = base_obs + 0.1*a[:, o % A],
  * r = base_r - 0.01*sum_a a^2 (f64), terminated = base_term.  obs_out (N, O) f64, reward (N,) f64,

@@ -11,7 +11,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip"]
+SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 
@@ -25,14 +25,18 @@ def build_library(verbose: bool = True) -> str:
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs, procs = [], []
+    headers = [d for d in deps if d.endswith(".h")]
     for src in srcs:
         obj = os.path.join(HERE, "build", os.path.basename(src) + ".o")
         os.makedirs(os.path.dirname(obj), exist_ok=True)
+        objs.append(obj)
+        if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d)
+                                       for d in [src] + headers):
+            continue  # object up to date (per-source incremental rebuild)
         cmd = [hipcc, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, cwd=HERE)))
-        objs.append(obj)
     failed = [cmd for cmd, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])

@@ -72,6 +72,7 @@ _SIGNATURES = {
     "ppo_ctx_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
                                       POINTER(c_double), POINTER(c_int64), POINTER(c_double),
                                       POINTER(c_double)]),
+    "ppo_ctx_phase_stamps": (c_int, [c_void_p, c_int, c_void_p, c_int]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -1,0 +1,57 @@
+// Persistent fused minibatch update (precision mode bf16, two equal hidden layers): host-side
+// argument block and launchers, shared by mlp_engine.hip (ppo_minibatch_grad) and
+// fused_update.hip (the kernels).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "timing.h"
+
+namespace ppo {
+
+constexpr int kFusedRows = 64;      // minibatch rows per chunk (one LDS-resident tile)
+constexpr int kFusedKX = 32;        // layer-0 input width padded for the 32x32x16 MFMA
+constexpr int kFusedSP = 16;        // per-row scalar pitch: actions[A], old_logp, adv, vtarget
+constexpr int kFusedMaxAct = 8;
+constexpr int kFusedMaxWG = 128;    // workgroups (= partial-gradient slabs) per net
+
+struct FusedNet {
+  const __bf16 *w0b;   // (H, 32)  bf16(W0), input columns >= din zero
+  const __bf16 *w1b;   // (H, H)   bf16(W1)
+  const __bf16 *w1bt;  // (H, H)   bf16(W1)^T
+  const float *w0, *w1;        // f32 masters (prep kernel source)
+  const float *b0, *b1;        // hidden biases (nullable: NetworkConfig.use_bias = False)
+  const float *wh, *bh;        // head (A_net, H) f32, bias (A_net) (nullable)
+  int64_t off_w0, off_b0, off_w1, off_b1, off_wh, off_bh;  // flat offsets (b: -1 = none)
+};
+
+struct FusedArgs {
+  FusedNet net[2];             // 0 actor, 1 critic
+  const float *logstd;
+  int64_t off_logstd;
+  // minibatch staged by fused_prep_kernel (rows >= count are zero)
+  __bf16 *xb;                  // (b, 32) bf16 states
+  float *srow;                 // (b, 16) f32 actions[A], old_logp, adv, vtarget
+  // prep sources: time-major storage arrays gathered through rows
+  const float *states, *actions, *old_logp, *adv, *vtarget;
+  const int32_t *rows;
+  const int32_t *rows_n;       // device row count (exact data parallel), nullable -> b
+  int b, din, act_dim, act, hidden;
+  float omv, clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
+  float *slabs;                // (G, slab_stride) partial gradients in the flat layout
+  int64_t slab_stride;
+  float *loss_part;            // (G, 2): actor / critic loss-term sums per workgroup
+  int G;                       // workgroups per net
+  uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
+};
+
+// Gather the minibatch (bf16 states + row scalars) and refresh the bf16 weight images.
+int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
+// The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.
+int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
+// Supported hidden widths (compiled instantiations).
+bool fused_width_ok(int hidden);
+
+}  // namespace ppo

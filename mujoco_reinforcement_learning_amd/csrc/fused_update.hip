@@ -1,0 +1,862 @@
+// Persistent fused minibatch update for precision mode bf16:
+// actor/critic forward, Normal log-prob, clipped surrogate + entropy / Huber loss heads, and the
+// full backward of both networks (ppo.py:109-135) in ONE launch per minibatch.
+//
+// Scope: two hidden layers of equal width H (the MLP configs of BASELINE.json: 2x256; in_dim
+// = W*O <= 32, A <= 8).  Other shapes and precision f32 use the layered GEMM path.
+//
+// Layout.  grid = (G, 2): blockIdx.y picks the net (0 actor, 1 critic), each workgroup (8 waves)
+// owns one CU (LDS ~144 KB) and walks minibatch chunks of R = 64 rows, chunk = blockIdx.x + i*G.
+// Per chunk everything stays on chip:
+//   X   [64][32]  bf16 LDS image of the states (64-B rows)
+//   A1  [64][H]   bf16 layer-0 output a1, later overwritten with its gradient d1
+//   D2  [64][H]   bf16 gradient at layer 1's pre-activation (its first use: head partial sums)
+//   A2F [64][H]   f32 layer-1 output a2 (the head runs in f32 on it, like the emulation oracle)
+// Activations are written from the MFMA accumulators (column = batch row on the lane, rows =
+// features in registers -> 8-B stores of 4 features) and read back either row-wise (16-B
+// ds_read_b128: 8 consecutive features of one batch row, the operand of a product summing over
+// features) or column-wise (ds_read_b64_tr_b16: 8 consecutive batch rows of one feature, the
+// operand of a weight gradient summing over rows).  One XOR-swizzled image serves both reads
+// conflict-free (cdna_hip_programming.md T10 "one image for row reads AND transposed reads").
+// Weight gradients are summed over all chunks of the workgroup in registers (dW1: 8 32x32
+// tiles per wave; dW0: one tile per wave), so HBM sees only the bf16 minibatch inputs, the
+// L2-resident bf16 weights and, once per workgroup, one partial-gradient slab in the flat
+// parameter layout.  reduce_slabs_kernel then folds the G slabs in a fixed order.
+//
+// Numerics = oracle.use_bf16_hidden_gemms: every hidden-layer product takes bf16(RNE) operands
+// with f32 accumulation; the heads (forward, dH, head dW) and every bias gradient are f32 on the
+// f32 values.  act'(a1) for tanh / ELU uses the f32 a1, recomputed in the dgrad epilogue (the
+// image holds bf16(a1)); ReLU needs only its sign, which the bf16 image keeps.
+#include <cstdio>
+
+#include "common.h"
+#include "fused_update.h"
+
+namespace ppo {
+namespace fu {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int R = kFusedRows;
+constexpr int NW = 8;           // waves per workgroup (two per SIMD, 256 registers each)
+constexpr int NT = 64 * NW;
+constexpr int DZP = 12;         // dz row pitch (floats): 48-B rows, conflict-free row reads
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const f32x2 f = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
+}
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// ---- LDS images ----------------------------------------------------------------------------
+// H-wide bf16 image, pitch a multiple of 256 B: 16-B chunk c of row r lives at
+// r*pitch + 16*(c ^ swz(r)), swz(r) = ((r&3)<<2) | ((r>>2)&3) (XOR touches the low 4 chunk bits).
+__device__ __forceinline__ int img_off(int r, int c, int pitch) {
+  return r * pitch + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+// X image: 64-B rows (4 chunks), chunk c of row r at r*64 + 16*(c ^ ((r>>2)&3)).
+__device__ __forceinline__ int x_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 2) & 3)); }
+
+__device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
+
+__device__ __forceinline__ bf16x8 tr_pair(const char *a, const char *b) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(b));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// 32x32x16 operand whose k runs over image ROWS k0..k0+15 and whose m/n runs over image
+// COLUMNS col0..col0+31: lane (c = lane&31, h = lane>>5) gets rows k0+8h..+7 of column col0+c.
+// ds_read_b64_tr_b16: in 16-lane group g, lane 4q+p addresses block row q, columns 4p..4p+3.
+__device__ __forceinline__ bf16x8 tr_frag(const char *img, int pitch, int k0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * (g >> 1) + q;
+  const int c = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
+  return tr_pair(img + img_off(row, c, pitch) + 8 * (p & 1),
+                 img + img_off(row + 4, c, pitch) + 8 * (p & 1));
+}
+__device__ __forceinline__ bf16x8 tr_frag_x(const char *img, int k0, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * (g >> 1) + q;
+  const int c = 2 * (g & 1) + (p >> 1);
+  return tr_pair(img + x_off(row, c) + 8 * (p & 1), img + x_off(row + 4, c) + 8 * (p & 1));
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Fixed-order reduce-scatter of 16 per-lane values over the 32 lanes of a wave half: after the
+// xor-16/8/4/2 halvings and a final xor-1 add, lane m holds the full sum of value
+// q(m) = 8*b4(m) + 4*b3(m) + 2*b2(m) + b1(m) (bit k of m: bk), duplicated on lanes m, m^1.
+__device__ __forceinline__ float rs16(float (&v)[16], int lane) {
+  const int m = lane & 31;
+  {
+    const bool up = m & 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float send = up ? v[i] : v[i + 8];
+      const float keep = up ? v[i + 8] : v[i];
+      v[i] = keep + __shfl_xor(send, 16, 64);
+    }
+  }
+  {
+    const bool up = m & 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float send = up ? v[i] : v[i + 4];
+      const float keep = up ? v[i + 4] : v[i];
+      v[i] = keep + __shfl_xor(send, 8, 64);
+    }
+  }
+  {
+    const bool up = m & 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float send = up ? v[i] : v[i + 2];
+      const float keep = up ? v[i + 2] : v[i];
+      v[i] = keep + __shfl_xor(send, 4, 64);
+    }
+  }
+  {
+    const bool up = m & 2;
+    const float send = up ? v[0] : v[1];
+    const float keep = up ? v[1] : v[0];
+    v[0] = keep + __shfl_xor(send, 2, 64);
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+// feature (within a 32-wide tile, lane half h) whose sum rs16 leaves on lane m
+__device__ __forceinline__ int rs16_feature(int lane) {
+  const int m = lane & 31, h = lane >> 5;
+  const int q = 8 * ((m >> 4) & 1) + 4 * ((m >> 3) & 1) + 2 * ((m >> 2) & 1) + ((m >> 1) & 1);
+  return (q & 3) + 8 * (q >> 2) + 4 * h;
+}
+
+__device__ __forceinline__ int reg_feature(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// acc[t] += W[32w + r][:] . img[32t + r][:] over k = 0..H-1 for row tiles t = 0, 1.  A operand
+// = 16-B rows of the L2-resident bf16 weight image (wrow -> row 32w + r, column 8h), B operand
+// = 16-B row reads of the LDS activation image.  Weight fragments run through a ring of PD + 1
+// registers: the load for k-step s + PD is issued before the MFMAs of step s (the first PD by
+// wring_prime, a phase earlier), so L2 latency hides behind 2*PD MFMAs per wave; the B reads of
+// step s + 1 overlap step s; sched_barrier pins one k-step per scheduling region so the
+// compiler cannot hoist the whole pass's loads (register blow-up).
+constexpr int PD = 3;  // prefetch distance (k-steps); ring period PD + 1 = 4
+template <int H>
+__device__ __forceinline__ void wring_prime(const __bf16 *wrow, bf16x8 (&ring)[PD + 1]) {
+#pragma unroll
+  for (int s = 0; s < PD; ++s) ring[s] = *reinterpret_cast<const bf16x8 *>(wrow + 16 * s);
+}
+template <int H>
+__device__ __forceinline__ void mlp_pass(const __bf16 *wrow, const char *img, int r, int h,
+                                         bf16x8 (&ring)[PD + 1], f32x16 (&acc)[2]) {
+  constexpr int KS = H / 16;
+  static_assert(KS % (PD + 1) == 0, "ring period must divide the k-steps");
+  const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
+  const char *rowp = img + r * (2 * H);
+#pragma unroll 1
+  for (int s0 = 0; s0 < KS; s0 += PD + 1) {
+#pragma unroll
+    for (int u = 0; u <= PD; ++u) {
+      const int s = s0 + u;
+      const bf16x8 af = ring[u];
+      if (s + PD < KS)
+        ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wrow + 16 * (s + PD));
+      const char *p = rowp + 16 * ((2 * s + h) ^ swz);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
+    }
+  }
+}
+
+}  // namespace fu
+
+using namespace fu;
+
+// ============================================================================================
+// Prep: gather the minibatch rows once per minibatch into contiguous bf16 / f32 staging, and
+// refresh the bf16 weight images (row-major and transposed W1) from the f32 masters.
+// ============================================================================================
+__global__ __launch_bounds__(256) void fused_prep_kernel(FusedArgs q, int row_blocks) {
+  const int tid = threadIdx.x;
+  if (static_cast<int>(blockIdx.x) < row_blocks) {
+    const int j = blockIdx.x * 256 + tid;
+    if (j >= q.b) return;
+    const int count = q.rows_n ? *q.rows_n : q.b;
+    const int A = q.act_dim;
+    float x[kFusedKX];
+    float s[kFusedSP];
+#pragma unroll
+    for (int k = 0; k < kFusedKX; ++k) x[k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < kFusedSP; ++k) s[k] = 0.f;
+    if (j < count) {
+      const int64_t sr = q.rows[j];
+      const float *src = q.states + sr * q.din;
+#pragma unroll
+      for (int k = 0; k < kFusedKX; ++k)
+        if (k < q.din) x[k] = src[k];
+      const float old_lp = q.old_logp[sr], adv = q.adv[sr], vt = q.vtarget[sr];
+#pragma unroll
+      for (int k = 0; k < kFusedSP; ++k)
+        s[k] = k < A ? q.actions[sr * A + k]
+                     : (k == A ? old_lp : (k == A + 1 ? adv : (k == A + 2 ? vt : 0.f)));
+    }
+    uint4 *xd = reinterpret_cast<uint4 *>(q.xb + static_cast<int64_t>(j) * kFusedKX);
+#pragma unroll
+    for (int u = 0; u < kFusedKX / 8; ++u)
+      xd[u] = make_uint4(pack2(x[8 * u], x[8 * u + 1]), pack2(x[8 * u + 2], x[8 * u + 3]),
+                         pack2(x[8 * u + 4], x[8 * u + 5]), pack2(x[8 * u + 6], x[8 * u + 7]));
+    float4 *sd = reinterpret_cast<float4 *>(q.srow + static_cast<int64_t>(j) * kFusedSP);
+#pragma unroll
+    for (int u = 0; u < kFusedSP / 4; ++u)
+      sd[u] = make_float4(s[4 * u], s[4 * u + 1], s[4 * u + 2], s[4 * u + 3]);
+    return;
+  }
+  // weights: per net H*32 (W0 image) + H*H (W1 and its transpose) elements
+  const int H = q.hidden;
+  const int64_t per_net = static_cast<int64_t>(H) * kFusedKX + static_cast<int64_t>(H) * H;
+  const int64_t e = static_cast<int64_t>(blockIdx.x - row_blocks) * 256 + tid;
+  if (e >= 2 * per_net) return;
+  const int z = e >= per_net;
+  const FusedNet &N = z ? q.net[1] : q.net[0];
+  const int64_t i = e - z * per_net;
+  __bf16 *w0b = const_cast<__bf16 *>(N.w0b);
+  __bf16 *w1b = const_cast<__bf16 *>(N.w1b);
+  __bf16 *w1bt = const_cast<__bf16 *>(N.w1bt);
+  if (i < static_cast<int64_t>(H) * kFusedKX) {
+    const int f = static_cast<int>(i / kFusedKX), k = static_cast<int>(i % kFusedKX);
+    const float v = k < q.din ? N.w0[static_cast<int64_t>(f) * q.din + k] : 0.f;
+    w0b[i] = __builtin_bit_cast(__bf16, static_cast<uint16_t>(pack2(v, 0.f) & 0xffffu));
+  } else {
+    const int64_t t = i - static_cast<int64_t>(H) * kFusedKX;
+    const int o = static_cast<int>(t / H), c = static_cast<int>(t % H);
+    const __bf16 v = __builtin_bit_cast(__bf16, static_cast<uint16_t>(pack2(N.w1[t], 0.f) & 0xffffu));
+    w1b[t] = v;
+    w1bt[static_cast<int64_t>(c) * H + o] = v;
+  }
+}
+
+// ============================================================================================
+// The fused update kernel
+// ============================================================================================
+template <int H>
+struct Lds {
+  static constexpr int PITCH = 2 * H;          // A1 / D2 / D1 row pitch (bytes), multiple of 256
+  static constexpr int A2P = 4 * H + 16;       // A2F row pitch (bytes): +16 B -> conflict-free b128 stores
+  static constexpr int WH = 0;                                  // f32 head weights [8][H]
+  static constexpr int BIAS = WH + kFusedMaxAct * H * 4;        // f32 b0[H], b1[H]
+  static constexpr int X = BIAS + 2 * H * 4;                    // bf16 [64][32]
+  static constexpr int A1 = X + R * 64;                         // bf16 [64][H]
+  static constexpr int D2 = A1 + R * PITCH;                     // bf16 [64][H]; head partials alias
+  static constexpr int A2F = D2 + R * PITCH;                    // f32 [64][H]; D1 bf16 image aliases
+  static constexpr int DZ = A2F + R * A2P;                      // f32 [64][12]
+  static constexpr int RED = DZ + R * DZP * 4;                  // f32 [64][8] row-thread partials
+  static constexpr int HS = RED + R * 8 * 4;                    // f32 head bias[8], logstd[8]
+  static constexpr int TOTAL = HS + 16 * 4;
+  static_assert(TOTAL <= 163840, "LDS budget");
+  static_assert(NW * R * 8 * 4 <= R * PITCH, "head partials must fit in the D2 image");
+  static_assert(R * PITCH <= R * A2P, "D1 image must fit in the A2F region");
+};
+
+// STAMP (diagnostic build, ppo_ctx_phase_stamps): wave 0 sums s_memtime deltas per phase segment
+// over the chunks and writes them per workgroup; the product kernel has STAMP = false.
+constexpr int kStampSlots = 11;
+
+// One net's workgroup: 8 waves; wave w owns feature tile w (features 32w..32w+31) in every
+// feature-tiled phase, dW1 tiles (o-tiles 2(w&3)+{0,1}) x (i-tiles 4(w>>2)+{0..3}) and dW0 tile
+// w.  NH = head width (actor: act_dim padded to 2/4/6/8 with zero head rows, critic: 1),
+// compile-time so every per-action loop is branch-free.
+template <int H, int ACT, int NH, bool ACTOR, bool STAMP>
+__device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N, char *lds,
+                                           uint64_t *stamps) {
+  static_assert(H == 32 * NW, "wave w owns feature tile w");
+  using L = Lds<H>;
+  constexpr int z = ACTOR ? 0 : 1;
+  char *const ximg = lds + L::X;
+  char *const a1img = lds + L::A1;
+  char *const d2img = lds + L::D2;
+  char *const d1img = lds + L::A2F;
+  float *const whs = reinterpret_cast<float *>(lds + L::WH);
+  const float *const b0s = reinterpret_cast<const float *>(lds + L::BIAS);
+  const float *const b1s = b0s + H;
+  float *const dzs = reinterpret_cast<float *>(lds + L::DZ);
+  float *const zp = reinterpret_cast<float *>(lds + L::D2);  // [NW][R][8] head partials
+  const float *const a2f = reinterpret_cast<const float *>(lds + L::A2F);
+
+  const int tid0 = threadIdx.x, w = tid0 >> 6;
+  int tid = tid0, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  // Lane-derived LDS addresses are loop-invariant across chunks; re-deriving them from an
+  // opaque copy of the lane ids in every phase keeps the compiler from hoisting (and spilling)
+  // dozens of them out of the chunk loop.
+#define OPAQUE_LANE()             \
+  tid = tid0;                     \
+  asm volatile("" : "+v"(tid));   \
+  lane = tid & 63;                \
+  r = lane & 31;                  \
+  h = lane >> 5
+  const int A = q.act_dim;        // real actor width (NH >= A; rows A..NH-1 of whs are zero)
+  const int G = q.G;
+  const int nchunks = (q.b + R - 1) / R;
+  const int count = q.rows_n ? *q.rows_n : q.b;
+
+  for (int i = tid; i < NH * H; i += NT) {
+    const int a = i / H;
+    whs[i] = (ACTOR && a >= A) ? 0.f : N.wh[i];
+  }
+  for (int i = tid; i < 2 * H; i += NT) {
+    const float *b = i < H ? N.b0 : N.b1;
+    (reinterpret_cast<float *>(lds + L::BIAS))[i] = b ? b[i % H] : 0.f;
+  }
+  if (tid < 16) {
+    const int a = tid & 7;
+    const bool ok = a < (ACTOR ? A : 1);
+    (reinterpret_cast<float *>(lds + L::HS))[tid] =
+        tid < 8 ? ((ok && N.bh) ? N.bh[a] : 0.f) : ((ACTOR && ok) ? q.logstd[a] : 0.f);
+  }
+  const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
+  const float *const hlogstd = hbias + 8;
+
+  // ---- persistent accumulators ----
+  f32x16 gw1[2][4];   // dW1 tiles: o-tiles 2*(w&3)+{0,1}, i-tiles 4*(w>>2)+{0..3}
+  f32x16 gw0;         // dW0 tile: features 32w.., input columns 0..31
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) gw1[a][b][e] = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) gw0[e] = 0.f;
+  float gb1 = 0.f, gb0 = 0.f;                 // rs16-scattered bias grads (feature rs16_feature)
+  float gwh[NH];                              // head dW: feature fh = tid % H, rows group tid / H
+#pragma unroll
+  for (int a = 0; a < NH; ++a) gwh[a] = 0.f;
+  float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;  // row-thread (lrow, la) partials
+
+  // loss-phase thread -> (row lrow, action la); head-dW thread -> (feature fh, row group rg).
+  // Re-derived from the opaque lane id inside each phase (see OPAQUE_LANE).
+  int lrow = tid0 >> 3, la = tid0 & 7;
+  constexpr int RG = NT / H;
+  int fh = tid0 % H, rg = tid0 / H;
+#define OPAQUE_ROWS()  \
+  OPAQUE_LANE();       \
+  lrow = tid >> 3;     \
+  la = tid & 7;        \
+  fh = tid % H;        \
+  rg = tid / H
+
+  // X staging: thread -> 8 B (row tid>>3, unit tid&7) of the chunk's bf16 states
+  auto load_x = [&](int c) -> uint2 {
+    const int j = c * R + (tid0 >> 3);
+    if (c < nchunks && j < q.b)
+      return *reinterpret_cast<const uint2 *>(q.xb + static_cast<int64_t>(j) * kFusedKX + 4 * (tid0 & 7));
+    return make_uint2(0u, 0u);
+  };
+  int chunk = blockIdx.x;
+  uint2 xpre = load_x(chunk);
+  uint64_t t_prev = 0, t_acc[kStampSlots];
+  if constexpr (STAMP) {
+#pragma unroll
+    for (int p = 0; p < kStampSlots; ++p) t_acc[p] = 0;
+    t_prev = __builtin_amdgcn_s_memtime();
+  }
+#define STAMP_AT(p)                                       \
+  if constexpr (STAMP) {                                  \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();  \
+    t_acc[p] += t_now - t_prev;                           \
+    t_prev = t_now;                                       \
+  }
+
+  bf16x8 ring[PD + 1];
+  for (; chunk < nchunks; chunk += G) {
+    // ---- phase 0: X image; row scalars for the loss phase; W0 fragments ----
+    OPAQUE_ROWS();
+    *reinterpret_cast<uint2 *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xpre;
+    const int jrow = chunk * R + lrow;
+    const bool valid = jrow < count;
+    float s_act = 0.f, s_old = 0.f, s_adv = 0.f, s_vt = 0.f;
+    bf16x8 w0f[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      w0f[s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
+    __syncthreads();
+    STAMP_AT(0);
+
+    // ---- phase 1: a1 = act(W0 x + b0) -> A1 image ----
+    OPAQUE_LANE();
+    wring_prime<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, ring);  // for phase 2
+    {
+      f32x16 acc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc[t] = mfma(w0f[s], lds_b128(ximg + x_off(32 * t + r, 2 * s + h)), acc[t]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int f0 = 32 * w + 8 * g + 4 * h;
+        const float4 bv = *reinterpret_cast<const float4 *>(b0s + f0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float y0 = act_forward(acc[t][4 * g] + bv.x, ACT);
+          const float y1 = act_forward(acc[t][4 * g + 1] + bv.y, ACT);
+          const float y2 = act_forward(acc[t][4 * g + 2] + bv.z, ACT);
+          const float y3 = act_forward(acc[t][4 * g + 3] + bv.w, ACT);
+          *reinterpret_cast<uint2 *>(a1img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
+              make_uint2(pack2(y0, y1), pack2(y2, y3));
+        }
+      }
+    }
+    __syncthreads();
+    STAMP_AT(1);
+
+    // ---- phase 2: a2 = W1 a1 (f32 accumulators) ----
+    OPAQUE_LANE();
+    // the loss phase's row scalars: issued here, in flight behind this barrier-free MFMA pass
+    if (jrow < q.b) {
+      const float *sp = q.srow + static_cast<int64_t>(jrow) * kFusedSP;
+      if constexpr (ACTOR) {
+        if (la < A) s_act = sp[la];
+        s_old = sp[A];
+        s_adv = sp[A + 1];
+      } else {
+        s_vt = sp[A + 2];
+      }
+    }
+    {
+      f32x16 a2[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
+      mlp_pass<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, a1img, r, h, ring, a2);
+      STAMP_AT(2);
+
+      // ---- phase 3: bias + act -> A2F (f32); head partial sums over the wave's 32 features ----
+      OPAQUE_LANE();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int f0 = 32 * w + 8 * g + 4 * h;
+        const float4 bv = *reinterpret_cast<const float4 *>(b1s + f0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          *reinterpret_cast<float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0) =
+              make_float4(act_forward(a2[t][4 * g] + bv.x, ACT),
+                          act_forward(a2[t][4 * g + 1] + bv.y, ACT),
+                          act_forward(a2[t][4 * g + 2] + bv.z, ACT),
+                          act_forward(a2[t][4 * g + 3] + bv.w, ACT));
+      }
+    }
+    {
+      // a2 is dead from here on; the partial sums re-read this lane's own f32 values
+      float zpart[2][NH];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < NH; ++a) zpart[t][a] = 0.f;
+#pragma unroll 1
+      for (int g = 0; g < 4; ++g) {
+        const int f0 = 32 * w + 8 * g + 4 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float4 y = *reinterpret_cast<const float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0);
+#pragma unroll
+          for (int a = 0; a < NH; ++a) {
+            const float4 wv = *reinterpret_cast<const float4 *>(whs + a * H + f0);
+            float p = zpart[t][a];
+            p = fmaf(y.x, wv.x, p);
+            p = fmaf(y.y, wv.y, p);
+            p = fmaf(y.z, wv.z, p);
+            p = fmaf(y.w, wv.w, p);
+            zpart[t][a] = p;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one feature group per region (no load hoisting)
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int a = 0; a < NH; ++a) zpart[t][a] += __shfl_xor(zpart[t][a], 32, 64);
+        if (h == 0) {
+          float *dst = zp + (w * R + 32 * t + r) * 8;
+          if constexpr (NH == 1) {
+            dst[0] = zpart[t][0];
+          } else {
+#pragma unroll
+            for (int a = 0; a < NH; a += 2)
+              *reinterpret_cast<float2 *>(dst + a) = make_float2(zpart[t][a], zpart[t][a + 1]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    STAMP_AT(3);
+
+    // ---- phase 4: per-row loss head (thread = (row, action)), torch formulas as
+    //      update_head_q4_kernel ----
+    OPAQUE_ROWS();
+    {
+      float dzv = 0.f;
+      if constexpr (ACTOR) {
+        float y = 0.f, d = 0.f, var = 1.f, lp = 0.f;
+        const bool act_lane = la < A;
+        if (act_lane) {
+          float zz = 0.f;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) zz += zp[(v * R + lrow) * 8 + la];
+          if (N.bh) zz += hbias[la];
+          y = tanhf(zz);
+          const float mu = q.omv * y;
+          const float sd = expf(hlogstd[la]);
+          const float x = valid ? s_act : mu;
+          d = x - mu;
+          var = sd * sd;
+          lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+        }
+        float logp = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
+#pragma unroll
+        for (int a = 0; a < NH; ++a) {
+          const float t = __shfl(lp, (lane & ~7) + a, 64);
+          if (a < A) logp += t;
+        }
+        const float old_lp = valid ? s_old : logp;
+        const float adv = valid ? s_adv : 0.f;
+        const float ratio = expf(logp - old_lp);
+        const float s1 = ratio * adv;
+        const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+        const float s2 = cl * adv;
+        const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+        const float gg = -q.inv_b;
+        const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+        const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+        const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+        const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+        const float dlogp = valid ? dratio * ratio : 0.f;
+        if (act_lane) {
+          const float dmu = dlogp * (d / var);
+          dzv = (dmu * q.omv) * (1.f - y * y);
+          if (valid) {
+            g_ls += dlogp * ((d * d) / var - 1.f) - q.ent_coef * q.inv_ba;
+            g_bh += dzv;
+          }
+        }
+        if (valid && la == 0) g_loss += mn;
+      } else {
+        if (la == 0) {
+          float v = 0.f;
+#pragma unroll
+          for (int u = 0; u < NW; ++u) v += zp[(u * R + lrow) * 8];
+          if (N.bh) v += hbias[0];
+          const float vt = valid ? s_vt : v;
+          const float diff = v - vt;
+          const float ad = fabsf(diff);
+          if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+          dzv = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+          g_bh += dzv;
+        }
+      }
+      dzs[lrow * DZP + la] = dzv;
+    }
+    __syncthreads();
+    STAMP_AT(4);
+
+    // ---- phase 5a: d2 = (dz . Wh) * act'(a2) (f32) -> bias grad, bf16 -> D2 image ----
+    OPAQUE_LANE();
+    {
+      float bsum[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        float dz[NH];
+        if constexpr (NH == 1) {
+          dz[0] = dzs[(32 * t + r) * DZP];
+        } else {
+#pragma unroll
+          for (int a = 0; a < NH; a += 2) {
+            const float2 v = *reinterpret_cast<const float2 *>(dzs + (32 * t + r) * DZP + a);
+            dz[a] = v.x;
+            dz[a + 1] = v.y;
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int f0 = 32 * w + 8 * g + 4 * h;
+          float sx = 0.f, sy = 0.f, sz = 0.f, sw = 0.f;
+#pragma unroll
+          for (int a = 0; a < NH; ++a) {
+            const float4 wv = *reinterpret_cast<const float4 *>(whs + a * H + f0);
+            sx = fmaf(dz[a], wv.x, sx);
+            sy = fmaf(dz[a], wv.y, sy);
+            sz = fmaf(dz[a], wv.z, sz);
+            sw = fmaf(dz[a], wv.w, sw);
+          }
+          const float4 yv = *reinterpret_cast<const float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0);
+          const float d0 = act_backward(sx, yv.x, ACT);
+          const float d1 = act_backward(sy, yv.y, ACT);
+          const float d2 = act_backward(sz, yv.z, ACT);
+          const float d3 = act_backward(sw, yv.w, ACT);
+          bsum[4 * g] += d0;
+          bsum[4 * g + 1] += d1;
+          bsum[4 * g + 2] += d2;
+          bsum[4 * g + 3] += d3;
+          *reinterpret_cast<uint2 *>(d2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
+              make_uint2(pack2(d0, d1), pack2(d2, d3));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      gb1 += rs16(bsum, lane);
+    }
+    // ---- phase 5b: head dW += dz^T a2 (f32; thread = feature, row group) ----
+    OPAQUE_ROWS();
+    {
+      constexpr int RPG = R / RG;
+#pragma unroll 2
+      for (int rr = 0; rr < RPG; ++rr) {
+        const int row = rg * RPG + rr;
+        const float av = a2f[row * (L::A2P / 4) + fh];
+        if constexpr (NH == 1) {
+          gwh[0] = fmaf(dzs[row * DZP], av, gwh[0]);
+        } else {
+#pragma unroll
+          for (int a = 0; a < NH; a += 2) {
+            const float2 dv = *reinterpret_cast<const float2 *>(dzs + row * DZP + a);
+            gwh[a] = fmaf(dv.x, av, gwh[a]);
+            gwh[a + 1] = fmaf(dv.y, av, gwh[a + 1]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    STAMP_AT(5);
+
+    // ---- phase 6a: dW1 += D2^T A1 (k = the chunk's 64 rows) ----
+    // Rolled over the four 16-row k-steps (unrolled, the compiler hoists all 80 transposed
+    // reads and spills).  The dgrad weight ring is primed first so its L2 latency hides behind
+    // this LDS-only phase.
+    OPAQUE_LANE();
+    wring_prime<H>(N.w1bt + static_cast<int64_t>(32 * w + r) * H + 8 * h, ring);
+    xpre = load_x(chunk + G);  // next chunk's states: in flight until the next phase 0
+#pragma unroll 1
+    for (int ks = 0; ks < R / 16; ++ks) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = tr_frag(d2img, L::PITCH, 16 * ks, 32 * (2 * (w & 3) + a), lane);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const bf16x8 bv = tr_frag(a1img, L::PITCH, 16 * ks, 32 * (4 * (w >> 2) + b), lane);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) gw1[a][b] = mfma(af[a], bv, gw1[a][b]);
+      }
+    }
+    STAMP_AT(6);
+
+    // ---- phase 6b: d1 = (W1^T d2) * act'(a1) -> D1 image (the A2F region is free) ----
+    OPAQUE_LANE();
+    {
+      f32x16 acc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+      mlp_pass<H>(N.w1bt + static_cast<int64_t>(32 * w + r) * H + 8 * h, d2img, r, h, ring, acc);
+      STAMP_AT(7);
+      OPAQUE_LANE();
+      // act'(a1): ReLU needs only the sign, which the bf16 image keeps exactly; tanh / ELU
+      // recompute this wave's f32 a1 tile (the phase-1 product; X is still resident), one row
+      // tile at a time
+      float bsum[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x16 y1;
+        if constexpr (ACT != PPO_ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) y1[e] = 0.f;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 wf = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
+            y1 = mfma(wf, lds_b128(ximg + x_off(32 * t + r, 2 * s + h)), y1);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float ya, yb, yc, yd;
+          if constexpr (ACT == PPO_ACT_RELU) {
+            const uint2 yv = *reinterpret_cast<const uint2 *>(a1img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h);
+            ya = bf_lo(yv.x), yb = bf_hi(yv.x), yc = bf_lo(yv.y), yd = bf_hi(yv.y);
+          } else {
+            const float4 bv = *reinterpret_cast<const float4 *>(b0s + 32 * w + 8 * g + 4 * h);
+            ya = act_forward(y1[4 * g] + bv.x, ACT);
+            yb = act_forward(y1[4 * g + 1] + bv.y, ACT);
+            yc = act_forward(y1[4 * g + 2] + bv.z, ACT);
+            yd = act_forward(y1[4 * g + 3] + bv.w, ACT);
+          }
+          const float d0 = act_backward(acc[t][4 * g], ya, ACT);
+          const float d1 = act_backward(acc[t][4 * g + 1], yb, ACT);
+          const float d2 = act_backward(acc[t][4 * g + 2], yc, ACT);
+          const float d3 = act_backward(acc[t][4 * g + 3], yd, ACT);
+          bsum[4 * g] += d0;
+          bsum[4 * g + 1] += d1;
+          bsum[4 * g + 2] += d2;
+          bsum[4 * g + 3] += d3;
+          *reinterpret_cast<uint2 *>(d1img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
+              make_uint2(pack2(d0, d1), pack2(d2, d3));
+        }
+      }
+      gb0 += rs16(bsum, lane);
+    }
+    __syncthreads();
+    STAMP_AT(8);
+
+    // ---- phase 7: dW0 += D1^T X ----
+    OPAQUE_LANE();
+#pragma unroll
+    for (int ks = 0; ks < R / 16; ++ks) {
+      gw0 = mfma(tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane), tr_frag_x(ximg, 16 * ks, lane), gw0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    STAMP_AT(9);
+  }
+#undef STAMP_AT
+#undef OPAQUE_ROWS
+#undef OPAQUE_LANE
+
+  // ================= epilogue: one partial-gradient slab per workgroup =================
+  tid = tid0;
+  lane = tid & 63;
+  r = lane & 31;
+  h = lane >> 5;
+  lrow = tid >> 3;
+  la = tid & 7;
+  fh = tid % H;
+  rg = tid / H;
+  if constexpr (STAMP) {
+    if (tid0 == 0) {
+      uint64_t *dst = stamps + (static_cast<int64_t>(z) * gridDim.x + blockIdx.x) * kStampSlots;
+#pragma unroll
+      for (int p = 0; p < kStampSlots; ++p) dst[p] = t_acc[p];
+    }
+  }
+  float *slab = q.slabs + static_cast<int64_t>(blockIdx.x) * q.slab_stride;
+  // dW1 (o, i) row-major [H][H]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int o0 = 32 * (2 * (w & 3) + a), i0 = 32 * (4 * (w >> 2) + b);
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        slab[N.off_w1 + static_cast<int64_t>(o0 + reg_feature(e, h)) * H + i0 + r] = gw1[a][b][e];
+    }
+  // dW0 (f, k) row-major [H][din]
+  if (r < q.din) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      slab[N.off_w0 + static_cast<int64_t>(32 * w + reg_feature(e, h)) * q.din + r] = gw0[e];
+  }
+  if ((lane & 1) == 0) {
+    const int f = 32 * w + rs16_feature(lane);
+    if (N.b1) slab[N.off_b1 + f] = gb1;
+    if (N.b0) slab[N.off_b0 + f] = gb0;
+  }
+  // head dW: combine the RG row groups in order through LDS (the A2F region is free now)
+  float *red = reinterpret_cast<float *>(lds + L::A2F);  // [RG][8][H]
+#pragma unroll
+  for (int a = 0; a < NH; ++a) red[(rg * kFusedMaxAct + a) * H + fh] = gwh[a];
+  float *rrow = reinterpret_cast<float *>(lds + L::RED);   // [64 rows][8]
+  float *lrow_sh = reinterpret_cast<float *>(lds + L::DZ);  // [64 rows][8] (dz image is free)
+  rrow[lrow * 8 + la] = g_bh;
+  lrow_sh[lrow * 8 + la] = g_ls;
+  __syncthreads();
+  const int na = ACTOR ? A : 1;
+  for (int i = tid; i < na * H; i += NT) {
+    const int a = i / H, f = i % H;
+    float s = 0.f;
+    for (int g = 0; g < RG; ++g) s += red[(g * kFusedMaxAct + a) * H + f];
+    slab[N.off_wh + i] = s;
+  }
+  if (tid < na && N.bh) {
+    float s = 0.f;
+    for (int row = 0; row < R; ++row) s += rrow[row * 8 + tid];
+    slab[N.off_bh + tid] = s;
+  }
+  if (ACTOR && tid >= 64 && tid < 64 + A) {
+    float s = 0.f;
+    for (int row = 0; row < R; ++row) s += lrow_sh[row * 8 + tid - 64];
+    slab[q.off_logstd + tid - 64] = s;
+  }
+  __syncthreads();
+  rrow[lrow * 8 + la] = g_loss;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int row = 0; row < R; ++row) s += rrow[row * 8];
+    q.loss_part[2 * blockIdx.x + z] = s;
+  }
+}
+
+template <int H, int ACT, int NA, bool STAMP>
+__global__ __launch_bounds__(NT, 1) void fused_update_kernel(FusedArgs q, uint64_t *stamps) {
+  __shared__ __attribute__((aligned(16))) char lds[Lds<H>::TOTAL];
+  if (blockIdx.y == 0) fused_body<H, ACT, NA, true, STAMP>(q, q.net[0], lds, stamps);
+  else fused_body<H, ACT, 1, false, STAMP>(q, q.net[1], lds, stamps);
+}
+
+bool fused_width_ok(int hidden) { return hidden == 256; }
+
+int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  const int row_blocks = ceil_div(q.b, 256);
+  const int64_t per_net = static_cast<int64_t>(q.hidden) * (kFusedKX + q.hidden);
+  const int w_blocks = ceil_div(2 * per_net, 256);
+  launch_k(rec, fused_prep_kernel, dim3(row_blocks + w_blocks), dim3(256), 0, st, q, row_blocks);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+template <int ACT, int NA>
+static void launch_na(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  uint64_t *nul = nullptr;
+  if (ACT == PPO_ACT_RELU && q.stamps)
+    launch_k(rec, fused_update_kernel<256, ACT, NA, true>, dim3(q.G, 2), dim3(NT), 0, st, q, q.stamps);
+  else
+    launch_k(rec, fused_update_kernel<256, ACT, NA, false>, dim3(q.G, 2), dim3(NT), 0, st, q, nul);
+}
+
+template <int ACT>
+static void launch_act(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  if (q.act_dim <= 2) launch_na<ACT, 2>(q, rec, st);
+  else if (q.act_dim <= 4) launch_na<ACT, 4>(q, rec, st);
+  else if (q.act_dim <= 6) launch_na<ACT, 6>(q, rec, st);
+  else launch_na<ACT, 8>(q, rec, st);
+}
+
+int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  PPO_REQUIRE(q.hidden == 256, "fused update: hidden width %d not compiled", q.hidden);
+  PPO_REQUIRE(q.G >= 1 && q.G <= kFusedMaxWG, "fused update: bad workgroup count %d", q.G);
+  PPO_REQUIRE(q.act_dim >= 1 && q.act_dim <= kFusedMaxAct, "fused update: act_dim %d", q.act_dim);
+  PPO_REQUIRE(!q.stamps || q.act == PPO_ACT_RELU, "fused update: phase stamps only for ReLU");
+  if (q.act == PPO_ACT_RELU) launch_act<PPO_ACT_RELU>(q, rec, st);
+  else if (q.act == PPO_ACT_TANH) launch_act<PPO_ACT_TANH>(q, rec, st);
+  else launch_act<PPO_ACT_ELU>(q, rec, st);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+}  // namespace ppo

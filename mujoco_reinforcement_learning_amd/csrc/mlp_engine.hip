@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "common.h"
+#include "fused_update.h"
 #include "timing.h"
 
 namespace ppo {
@@ -1217,7 +1218,7 @@ struct NetDesc {
 static const char *const kClassNames[KC_COUNT] = {
     "gemm_fwd",     "gemm_dgrad", "gemm_wgrad", "update_head", "policy_head", "reduce_slabs",
     "gather_states", "gae",       "adam",       "normalize_rows", "obs", "minibatch_rows",
-    "env_harness"};
+    "env_harness", "fused_update"};
 
 thread_local Timing *g_tim = nullptr;
 Timing *g_free_tim = nullptr;
@@ -1254,6 +1255,17 @@ struct ppo_ctx {
   float *xg;             // gathered minibatch states (max_rows, ldx)
   int ldx;               // round_up(W*O, 4)
   void *arena;
+  // persistent fused update (bf16, two equal hidden layers; fused_update.hip)
+  bool fused_ok;                // network shapes the fused kernel supports
+  int fused_hidden;
+  __bf16 *fw[2][3];             // per net: bf16 W0 image (H, 32), W1 (H, H), W1^T (H, H)
+  __bf16 *fxb;                  // (max_rows, 32) staged bf16 states
+  float *fsrow;                 // (max_rows, 16) staged row scalars
+  float *fslabs;                // (kFusedMaxWG, total_params) partial gradients
+  float *floss;                 // (kFusedMaxWG, 2) loss-term partials
+  void *farena;
+  uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
+  int fstamp_on, fstamp_g;
   ppo::Timing tim;
 };
 
@@ -1447,6 +1459,129 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
   return 0;
 }
 
+static const int g_fused_enabled = env_knob("PPO_FUSED", 1);
+
+// Precision bf16 with supported shapes: gather + bf16 weight refresh, the persistent fused
+// forward/loss/backward kernel (one partial-gradient slab per workgroup), then the fixed-order
+// slab reduction.  Same contract as the layered path below.
+static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                                const float *old_logp_d, const float *adv_d,
+                                const float *vtarget_d, const int32_t *rows_d, int b,
+                                const int32_t *count_d, float clip_lo, float clip_hi,
+                                float entropy_coef, float inv_b, float inv_ba, float *grad_d,
+                                float *loss_d, hipStream_t st) {
+  const int H = ctx->fused_hidden;
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  const int A = ctx->cfg.act_dim;
+  const int64_t P = ctx->total_params;
+  FusedArgs q{};
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    FusedNet &fn = q.net[z];
+    fn.w0b = ctx->fw[z][0];
+    fn.w1b = ctx->fw[z][1];
+    fn.w1bt = ctx->fw[z][2];
+    fn.w0 = ctx->params + nd.layer[0].w_off;
+    fn.w1 = ctx->params + nd.layer[1].w_off;
+    fn.b0 = nd.layer[0].b_off >= 0 ? ctx->params + nd.layer[0].b_off : nullptr;
+    fn.b1 = nd.layer[1].b_off >= 0 ? ctx->params + nd.layer[1].b_off : nullptr;
+    fn.wh = ctx->params + nd.layer[2].w_off;
+    fn.bh = nd.layer[2].b_off >= 0 ? ctx->params + nd.layer[2].b_off : nullptr;
+    fn.off_w0 = nd.layer[0].w_off;
+    fn.off_b0 = nd.layer[0].b_off;
+    fn.off_w1 = nd.layer[1].w_off;
+    fn.off_b1 = nd.layer[1].b_off;
+    fn.off_wh = nd.layer[2].w_off;
+    fn.off_bh = nd.layer[2].b_off;
+  }
+  q.logstd = ctx->params + ctx->net[0].logstd_off;
+  q.off_logstd = ctx->net[0].logstd_off;
+  q.xb = ctx->fxb;
+  q.srow = ctx->fsrow;
+  q.states = states_d;
+  q.actions = actions_d;
+  q.old_logp = old_logp_d;
+  q.adv = adv_d;
+  q.vtarget = vtarget_d;
+  q.rows = rows_d;
+  q.rows_n = count_d;
+  q.b = b;
+  q.din = din;
+  q.act_dim = A;
+  q.act = ctx->cfg.activation;
+  q.hidden = H;
+  q.omv = ctx->cfg.output_max_value;
+  q.clip_lo = clip_lo;
+  q.clip_hi = clip_hi;
+  q.ent_coef = entropy_coef;
+  q.inv_b = inv_b;
+  q.inv_ba = inv_ba;
+  q.slabs = ctx->fslabs;
+  q.slab_stride = P;
+  q.loss_part = ctx->floss;
+  const int nchunks = ceil_div(b, kFusedRows);
+  q.G = std::min(kFusedMaxWG, nchunks);
+  q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
+  ctx->fstamp_g = q.G;
+  // algorithmic traffic: gather (row index, din + A + 3 floats in; 64 + 64 B out per row) and
+  // weight images (f32 in, 3 bf16 images out per net)
+  const double wbytes = 2.0 * (4.0 * H * (din + H) + 2.0 * H * (kFusedKX + 2.0 * H));
+  {
+    const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
+                     static_cast<double>(b) * (4.0 * (1 + din + A + 3) + 2.0 * kFusedKX + 4.0 * kFusedSP) + wbytes};
+    if (int rc = fused_prep_launch(q, rec, st)) return rc;
+  }
+  {
+    // FLOPs per row per net: forward (din*H + H*H + a*H), dgrad (H*H + a*H), wgrad (din*H +
+    // H*H + a*H), a = A (actor) / 1 (critic); bytes: staged rows + one slab per workgroup
+    double fl = 0.0;
+    for (int z = 0; z < 2; ++z) {
+      const double a = z == 0 ? A : 1;
+      fl += 2.0 * b * ((din * H + H * H + a * H) + (H * H + a * H) + (din * H + H * H + a * H));
+    }
+    const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
+                      4.0 * q.G * static_cast<double>(P) + 2.0 * q.G * 2.0 * H * (kFusedKX + 2.0 * H);
+    const TimRec rec{KC_FUSED,
+                     tim_active() ? intern_name("fused_update_kernel<%d, %d>", H, q.act) : nullptr,
+                     fl, by};
+    if (int rc = fused_update_launch(q, rec, st)) return rc;
+  }
+  ReduceArgs r{};
+  int ns = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    auto seg = [&](int64_t off, int64_t len) {
+      ReduceSeg &g = r.seg[ns++];
+      g.dst = off;
+      g.len = len;
+      g.src = ctx->fslabs + off;
+      g.stride = P;
+      g.nsplit = q.G;
+    };
+    if (z == 0) seg(nd.logstd_off, A);
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      seg(L.w_off, static_cast<int64_t>(L.out) * L.in);
+      if (L.b_off >= 0) seg(L.b_off, L.out);
+    }
+  }
+  r.nseg = ns;
+  r.total = P;
+  r.grad = grad_d;
+  r.loss_part = ctx->floss;
+  r.loss_splits = q.G;
+  r.inv_b = inv_b;
+  r.logstd = ctx->params + ctx->net[0].logstd_off;
+  r.act_dim = A;
+  r.ent_coef = entropy_coef;
+  r.loss_out = loss_d;
+  launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(q.G) * P,
+                  4.0 * (static_cast<double>(q.G) + 1) * P},
+           reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);
+  PPO_LAUNCHED();
+  return 0;
+}
+
 static int check_ctx(const ppo_ctx *ctx) {
   PPO_REQUIRE(ctx != nullptr, "null ppo_ctx");
   PPO_REQUIRE(ctx->params != nullptr, "ppo_ctx: parameters not bound (ppo_bind_params)");
@@ -1564,6 +1699,46 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
     return PPO_EHIP;
   }
   ctx->params = nullptr;
+  // fused bf16 update: both nets 2 hidden layers of one compiled width, W*O <= 32, A <= 8
+  {
+    const NetDesc &na = ctx->net[0], &nc = ctx->net[1];
+    const int H = na.layer[0].out;
+    ctx->fused_ok = na.n_hidden == 2 && nc.n_hidden == 2 && fused_width_ok(H) &&
+                    na.layer[1].out == H && nc.layer[0].out == H && nc.layer[1].out == H &&
+                    din <= kFusedKX && cfg->act_dim <= kFusedMaxAct;
+    ctx->fused_hidden = H;
+    if (ctx->fused_ok) {
+      const int64_t wimg = align_up(static_cast<int64_t>(H) * (kFusedKX + 2 * H), 128);
+      const int64_t bytes = 2 * wimg * 2 + align_up(R * kFusedKX * 2, 256) +
+                            align_up(R * kFusedSP * 4, 256) +
+                            static_cast<int64_t>(kFusedMaxWG) * off * 4 + kFusedMaxWG * 2 * 4 + 1024;
+      void *fa = nullptr;
+      e = hipMalloc(&fa, bytes);
+      if (e != hipSuccess) {
+        (void)hipFree(arena);
+        delete ctx;
+        set_error("ppo_ctx_create: hipMalloc(%lld bytes) for the fused workspace failed: %s",
+                  static_cast<long long>(bytes), hipGetErrorString(e));
+        return PPO_EHIP;
+      }
+      ctx->farena = fa;
+      char *c = static_cast<char *>(fa);
+      for (int z = 0; z < 2; ++z) {
+        __bf16 *wb = reinterpret_cast<__bf16 *>(c);
+        ctx->fw[z][0] = wb;
+        ctx->fw[z][1] = wb + static_cast<int64_t>(H) * kFusedKX;
+        ctx->fw[z][2] = wb + static_cast<int64_t>(H) * (kFusedKX + H);
+        c += wimg * 2;
+      }
+      ctx->fxb = reinterpret_cast<__bf16 *>(c);
+      c += align_up(R * kFusedKX * 2, 256);
+      ctx->fsrow = reinterpret_cast<float *>(c);
+      c += align_up(R * kFusedSP * 4, 256);
+      ctx->fslabs = reinterpret_cast<float *>(c);
+      c += static_cast<int64_t>(kFusedMaxWG) * off * 4;
+      ctx->floss = reinterpret_cast<float *>(c);
+    }
+  }
   *out = ctx;
   return 0;
 }
@@ -1579,6 +1754,8 @@ extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
   delete[] ctx->tim.flops;
   delete[] ctx->tim.bytes;
   if (ctx->arena) (void)hipFree(ctx->arena);
+  if (ctx->farena) (void)hipFree(ctx->farena);
+  if (ctx->fstamps) (void)hipFree(ctx->fstamps);
   delete ctx;
   return 0;
 }
@@ -1683,6 +1860,10 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
               b, ctx->cfg.max_rows);
   hipStream_t st = as_stream(stream);
   TimingScope timing_scope(ctx);
+  if (ctx->prec == PPO_PREC_BF16 && ctx->fused_ok && g_fused_enabled)
+    return fused_minibatch_grad(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d, b,
+                                count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
+                                loss_d, st);
   const bool both[2] = {true, true};
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
@@ -1913,6 +2094,27 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
            reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);  // P % 16 == 0
   PPO_LAUNCHED();
   return 0;
+}
+
+extern "C" int ppo_ctx_phase_stamps(ppo_ctx *ctx, int enable, uint64_t *host_out, int max_values) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_phase_stamps: null ctx");
+  PPO_REQUIRE(ctx->fused_ok, "ppo_ctx_phase_stamps: network shape has no fused kernel");
+  PPO_HIP_TRY(hipSetDevice(ctx->device));
+  const int n = 2 * kFusedMaxWG * 11;
+  if (enable) {
+    if (!ctx->fstamps) PPO_HIP_TRY(hipMalloc(&ctx->fstamps, sizeof(uint64_t) * n));
+    PPO_HIP_TRY(hipMemset(ctx->fstamps, 0, sizeof(uint64_t) * n));
+    ctx->fstamp_on = 1;
+    return 0;
+  }
+  ctx->fstamp_on = 0;
+  if (!ctx->fstamps) return 0;
+  PPO_HIP_TRY(hipDeviceSynchronize());
+  const int got = 2 * ctx->fstamp_g * 11;
+  if (host_out && max_values > 0)
+    PPO_HIP_TRY(hipMemcpy(host_out, ctx->fstamps, sizeof(uint64_t) * std::min(got, max_values),
+                          hipMemcpyDeviceToHost));
+  return got;
 }
 
 extern "C" int ppo_ctx_set_precision(ppo_ctx *ctx, int prec) {

@@ -27,6 +27,7 @@ enum {
   KC_OBS,    // observation window push + normalisation
   KC_PERM,   // minibatch row selection
   KC_ENV,    // synthetic VecEnv step + Philox normals (bench harness)
+  KC_FUSED,  // persistent fused minibatch forward + loss + backward (bf16)
   KC_COUNT
 };
 

@@ -342,10 +342,14 @@ def test_per_kernel_timing_records(gpu):
 
 
 # ------------------------------------------------------------- bf16 GEMM precision mode
-@pytest.mark.parametrize("hidden,act,rows_total,b", [((64, 64), "relu", 512, 128),
-                                                     ((256, 256), "relu", 8192, 4096),
-                                                     ((64, 32), "tanh", 300, 100)])
-def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b):
+@pytest.mark.parametrize("hidden,act,rows_total,b,obs,na", [
+    ((64, 64), "relu", 512, 128, 17, 6),
+    ((256, 256), "relu", 8192, 4096, 17, 6),        # fused kernel (fused_update.hip) from here on
+    ((256, 256), "tanh", 3000, 1000, 17, 6),        # ragged last chunk (1000 = 15*64 + 40)
+    ((256, 256), "elu", 2000, 300, 27, 8),          # Ant-v4 shapes (O=27, A=8)
+    ((256, 256), "relu", 70000, 65536, 17, 6),      # bench minibatch: 128 workgroups x 8 chunks
+    ((64, 32), "tanh", 300, 100, 17, 6)])
+def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b, obs, na):
     """precision="bf16": every hidden fc GEMM (forward, dgrad, wgrad) takes bf16-rounded operands
     with f32 accumulation.  Checked against torch autograd on the oracle nets with the same
     operand rounding (oracle.use_bf16_hidden_gemms); the residual is f32 summation order plus
@@ -353,11 +357,11 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b):
     tensor's largest gradient.  Against plain f32 autograd each tensor is within 10 % relative
     L2 (bf16 operand noise)."""
     run, eng, ref, cfg = _agents(gpu, 4, num_envs=rows_total, hidden=hidden, activation=act,
-                                 batch_size=b, precision="bf16")
+                                 batch_size=b, precision="bf16", obs_dim=obs, act_dim=na)
     assert eng.engine.precision == "bf16"
     g = torch.Generator().manual_seed(10)
-    states = torch.randn(rows_total, 17, generator=g)
-    actions = torch.randn(rows_total, 6, generator=g) * 0.5
+    states = torch.randn(rows_total, obs, generator=g)
+    actions = torch.randn(rows_total, na, generator=g) * 0.5
     adv = torch.randn(rows_total, generator=g)
     vt = torch.randn(rows_total, generator=g) * 2
     with torch.no_grad():
@@ -367,9 +371,15 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b):
     rows = torch.randperm(rows_total, generator=g)[:b].to(torch.int32)
     grad = torch.empty(eng.engine.n_params, device=gpu)
     loss = torch.empty(2, device=gpu)
+    eng.engine.timing(True)
     eng.engine.minibatch_grad(states.to(gpu), actions.to(gpu), old_logp.to(gpu), adv.to(gpu),
                               vt.to(gpu), rows.to(gpu), b, grad, loss, 0.9, 1.1, 1e-4, 1.0 / b,
-                              1.0 / (b * 6))
+                              1.0 / (b * na))
+    kernels = eng.engine.timing_kernels()
+    eng.engine.timing(False)
+    fused = hidden == (256, 256)
+    assert any(k.startswith("fused_update_kernel<256") for k in kernels) == fused, kernels
+    assert (not any(k.startswith("gemm_") for k in kernels)) == fused, kernels
     gd = eng.packed(grad).cpu()
 
     def ref_grad(bf16: bool):
@@ -389,8 +399,10 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b):
             - dist.entropy().mean() * 1e-4
         r.networks.zero_grad()
         (la + lc).backward()
+        losses.append((float(la), float(lc)))
         return [(n, p.grad.flatten().clone()) for n, p in r.networks.named_parameters()]
 
+    losses = []
     off = 0
     for name, r_ in ref_grad(True):
         k = r_.numel()
@@ -406,3 +418,8 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b):
         rel = float((a - r_).norm() / (r_.norm() + 1e-12))
         assert rel <= 0.1, (name, rel)
         off += k
+    # loss scalars (actor: surrogate + entropy, critic: Huber) against the bf16 emulation
+    la_ref, lc_ref = losses[0]
+    got = loss.cpu()
+    assert abs(float(got[0]) - la_ref) <= 1e-3 * (abs(la_ref) + 1e-2), (float(got[0]), la_ref)
+    assert abs(float(got[1]) - lc_ref) <= 1e-3 * (abs(lc_ref) + 1e-2), (float(got[1]), lc_ref)

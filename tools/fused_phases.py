@@ -1,0 +1,61 @@
+"""Per-phase cycle breakdown of the fused bf16 update kernel (diagnostic stamped build).
+
+Runs headline-shape minibatches (B=65536, 2x256 ReLU) through ppo_minibatch_grad with
+ppo_ctx_phase_stamps enabled and prints, for actor and critic workgroups, the mean s_memtime
+cycles per phase segment summed over a workgroup's chunks (wave 0's view: a segment that ends at
+a barrier includes waiting for the slowest wave).
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+SEGMENTS = ["0 X/rows stage", "1 L0 fwd", "2 L1 fwd MFMA", "3 head partial + A2F", "4 loss",
+            "5 (unused)", "6 d2 + head dW", "7 dW1 wgrad", "8 dgrad L1", "9 d1 store",
+            "10 dW0 wgrad"]
+
+
+def main():
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    from mujoco_reinforcement_learning_amd import engine as E
+    dev = torch.device("cuda", 0)
+    b, n, t = 65536, 4096, 128
+    run = make_run(hidden=(256, 256), rng="philox", precision="bf16")
+    torch.manual_seed(0)
+    agent = PPOEngineAgent(run, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    states = torch.randn(n * t, 17, device=dev, generator=g)
+    actions = torch.randn(n * t, 6, device=dev, generator=g)
+    logp = torch.randn(n * t, device=dev, generator=g) - 5
+    adv = torch.randn(n * t, device=dev, generator=g)
+    vt = torch.randn(n * t, device=dev, generator=g)
+    rows = torch.empty(b, dtype=torch.int32, device=dev)
+    loss = torch.empty(2, device=dev)
+    eng = agent.engine
+    res = {}
+    for rep in range(3):
+        E.feistel_rows(1, rep, 0, b, n, t, rows)
+        eng.phase_stamps(True)
+        eng.minibatch_grad(states, actions, logp, adv, vt, rows, b, agent.flat_grad, loss,
+                           0.9, 1.1, 1e-4, 1 / b, 1 / (b * 6))
+        st = eng.phase_stamps(False).double()
+        res = {"actor": st[0].mean(0).tolist(), "critic": st[1].mean(0).tolist(),
+               "actor_total_max": float(st[0].sum(1).max()),
+               "critic_total_max": float(st[1].sum(1).max())}
+    for k in ("actor", "critic"):
+        tot = sum(res[k])
+        print(f"{k}: total {tot:.0f} cycles/WG (max {res[k + '_total_max']:.0f})")
+        for name, v in zip(SEGMENTS, res[k]):
+            print(f"   {v:10.0f}  {100 * v / max(tot, 1):5.1f}%  {name}")
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "fused_phases.json"), "w") as f:
+        json.dump({"segments": SEGMENTS, **res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
