@@ -102,6 +102,22 @@ int ppo_obs_normalize(const double *window_d, float *state_d, int n, int o, int 
 int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                     uint64_t offset, float *action_d, float *logp_d, float *value_d, float *mean_d,
                     void *stream);
+/* Fused observe + act (A1-A4 in one launch in precision bf16 with the fused shapes; otherwise the
+ * A1 kernels followed by ppo_policy_step): replaces EnvironmentHelper.step's window push
+ * (running_gym_sequential_vectorized.py:120-125), get_state (:61-92) and PPOAgent.act /
+ * get_state_value (ppo.py:22-26, ppo_agent.py:24-43) for one rollout step.
+ * window_d (N, O, W) f64 is pushed with obs_d (N, O) f64 when obs_d != NULL (reset_d / all_reset as
+ * ppo_obs_window_push), standardised as ppo_obs_normalize into state_d (N, W*O) f32, then the
+ * policy outputs are produced as ppo_policy_step (each nullable; the actor runs when action, logp
+ * or mean is requested, the critic when value is). */
+int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint8_t *reset_d,
+                    int all_reset, const int32_t *bounds, int n_bounds, int normalize,
+                    float *state_d, int n, const float *eps_d, uint64_t seed, uint64_t offset,
+                    float *action_d, float *logp_d, float *value_d, float *mean_d, void *stream);
+/* Refresh the bf16 weight images the fused kernels read from the bound f32 parameters; call after
+ * the parameters change outside ppo_minibatch_grad (Adam steps, loads) and before
+ * ppo_observe_act.  No-op unless the fused bf16 path is active. */
+int ppo_pack_weights(ppo_ctx *ctx, void *stream);
 /* Philox sampling in ppo_policy_step uses offset + *counter_d when counter_d (a device uint64)
  * is set, read when the kernel runs rather than when it is launched: a rollout captured once in
  * a hipGraph replays with fresh noise after the host bumps the counter.  NULL restores plain

@@ -73,6 +73,10 @@ _SIGNATURES = {
                                       POINTER(c_double), POINTER(c_int64), POINTER(c_double),
                                       POINTER(c_double)]),
     "ppo_ctx_phase_stamps": (c_int, [c_void_p, c_int, c_void_p, c_int]),
+    "ppo_pack_weights": (c_int, [c_void_p, c_void_p]),
+    "ppo_observe_act": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                c_int, c_void_p, c_int, c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

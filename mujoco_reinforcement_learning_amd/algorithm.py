@@ -111,9 +111,40 @@ class PPOEngine:
         self.environment_helper.t = t_len  # the host-side step counter the replay skipped
         return buf
 
+    def _rollout_fused(self, base_off: int) -> RolloutBuffer:
+        """Rollout through ppo_observe_act: per step one env launch (helper.step_raw) and one
+        engine launch (window push + standardisation + actor/critic + sampling); same values as
+        the step / get_state / policy_step sequence below."""
+        helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
+        n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        helper.reset()
+        helper.reset_environment(test_phase=False)
+        eng.pack_weights()
+        window = helper.timestep.observation
+        norm = bool(self.run.normalize_observations)
+        seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
+        eps, _ = self._eps(n, a)
+        eng.observe_act(window, buf.states[0], normalize=norm, eps=eps, seed=seed,
+                        offset=base_off, action=buf.actions[0], logp=buf.logp[0],
+                        value=buf.values[0])
+        for t in range(t_len):
+            obs = helper.step_raw(buf.actions[t], buf.reward[t], buf.terminated[t])
+            if t + 1 < t_len:
+                eps, _ = self._eps(n, a)
+                eng.observe_act(window, buf.states[t + 1], obs=obs, reset=buf.terminated[t],
+                                normalize=norm, eps=eps, seed=seed,
+                                offset=base_off + (t + 1) * n * a, action=buf.actions[t + 1],
+                                logp=buf.logp[t + 1], value=buf.values[t + 1])
+            else:
+                eng.observe_act(window, buf.states[t_len], obs=obs, reset=buf.terminated[t],
+                                normalize=norm, value=buf.values[t_len])
+        return buf
+
     def _rollout_steps(self, base_off: int) -> RolloutBuffer:
         helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        if hasattr(helper, "step_raw") and getattr(self.run.engine_config, "fused_rollout", True):
+            return self._rollout_fused(base_off)
         helper.reset()
         helper.reset_environment(test_phase=False)
         # helpers that can write straight into the buffer (SyntheticVecEnvHelper) skip the copies

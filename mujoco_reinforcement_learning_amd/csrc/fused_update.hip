@@ -29,156 +29,9 @@
 // image holds bf16(a1)); ReLU needs only its sign, which the bf16 image keeps.
 #include <cstdio>
 
-#include "common.h"
-#include "fused_update.h"
+#include "fused_common.h"
 
 namespace ppo {
-namespace fu {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-constexpr int R = kFusedRows;
-constexpr int NW = 8;           // waves per workgroup (two per SIMD, 256 registers each)
-constexpr int NT = 64 * NW;
-constexpr int DZP = 12;         // dz row pitch (floats): 48-B rows, conflict-free row reads
-
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  const f32x2 f = {lo, hi};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2));
-}
-__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-
-// ---- LDS images ----------------------------------------------------------------------------
-// H-wide bf16 image, pitch a multiple of 256 B: 16-B chunk c of row r lives at
-// r*pitch + 16*(c ^ swz(r)), swz(r) = ((r&3)<<2) | ((r>>2)&3) (XOR touches the low 4 chunk bits).
-__device__ __forceinline__ int img_off(int r, int c, int pitch) {
-  return r * pitch + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
-}
-// X image: 64-B rows (4 chunks), chunk c of row r at r*64 + 16*(c ^ ((r>>2)&3)).
-__device__ __forceinline__ int x_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 2) & 3)); }
-
-__device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
-
-__device__ __forceinline__ bf16x8 tr_pair(const char *a, const char *b) {
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(b));
-  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// 32x32x16 operand whose k runs over image ROWS k0..k0+15 and whose m/n runs over image
-// COLUMNS col0..col0+31: lane (c = lane&31, h = lane>>5) gets rows k0+8h..+7 of column col0+c.
-// ds_read_b64_tr_b16: in 16-lane group g, lane 4q+p addresses block row q, columns 4p..4p+3.
-__device__ __forceinline__ bf16x8 tr_frag(const char *img, int pitch, int k0, int col0, int lane) {
-  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
-  const int row = k0 + 8 * (g >> 1) + q;
-  const int c = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
-  return tr_pair(img + img_off(row, c, pitch) + 8 * (p & 1),
-                 img + img_off(row + 4, c, pitch) + 8 * (p & 1));
-}
-__device__ __forceinline__ bf16x8 tr_frag_x(const char *img, int k0, int lane) {
-  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
-  const int row = k0 + 8 * (g >> 1) + q;
-  const int c = 2 * (g & 1) + (p >> 1);
-  return tr_pair(img + x_off(row, c) + 8 * (p & 1), img + x_off(row + 4, c) + 8 * (p & 1));
-}
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// Fixed-order reduce-scatter of 16 per-lane values over the 32 lanes of a wave half: after the
-// xor-16/8/4/2 halvings and a final xor-1 add, lane m holds the full sum of value
-// q(m) = 8*b4(m) + 4*b3(m) + 2*b2(m) + b1(m) (bit k of m: bk), duplicated on lanes m, m^1.
-__device__ __forceinline__ float rs16(float (&v)[16], int lane) {
-  const int m = lane & 31;
-  {
-    const bool up = m & 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float send = up ? v[i] : v[i + 8];
-      const float keep = up ? v[i + 8] : v[i];
-      v[i] = keep + __shfl_xor(send, 16, 64);
-    }
-  }
-  {
-    const bool up = m & 8;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float send = up ? v[i] : v[i + 4];
-      const float keep = up ? v[i + 4] : v[i];
-      v[i] = keep + __shfl_xor(send, 8, 64);
-    }
-  }
-  {
-    const bool up = m & 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float send = up ? v[i] : v[i + 2];
-      const float keep = up ? v[i + 2] : v[i];
-      v[i] = keep + __shfl_xor(send, 4, 64);
-    }
-  }
-  {
-    const bool up = m & 2;
-    const float send = up ? v[0] : v[1];
-    const float keep = up ? v[1] : v[0];
-    v[0] = keep + __shfl_xor(send, 2, 64);
-  }
-  return v[0] + __shfl_xor(v[0], 1, 64);
-}
-// feature (within a 32-wide tile, lane half h) whose sum rs16 leaves on lane m
-__device__ __forceinline__ int rs16_feature(int lane) {
-  const int m = lane & 31, h = lane >> 5;
-  const int q = 8 * ((m >> 4) & 1) + 4 * ((m >> 3) & 1) + 2 * ((m >> 2) & 1) + ((m >> 1) & 1);
-  return (q & 3) + 8 * (q >> 2) + 4 * h;
-}
-
-__device__ __forceinline__ int reg_feature(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
-
-// acc[t] += W[32w + r][:] . img[32t + r][:] over k = 0..H-1 for row tiles t = 0, 1.  A operand
-// = 16-B rows of the L2-resident bf16 weight image (wrow -> row 32w + r, column 8h), B operand
-// = 16-B row reads of the LDS activation image.  Weight fragments run through a ring of PD + 1
-// registers: the load for k-step s + PD is issued before the MFMAs of step s (the first PD by
-// wring_prime, a phase earlier), so L2 latency hides behind 2*PD MFMAs per wave; the B reads of
-// step s + 1 overlap step s; sched_barrier pins one k-step per scheduling region so the
-// compiler cannot hoist the whole pass's loads (register blow-up).
-constexpr int PD = 3;  // prefetch distance (k-steps); ring period PD + 1 = 4
-template <int H>
-__device__ __forceinline__ void wring_prime(const __bf16 *wrow, bf16x8 (&ring)[PD + 1]) {
-#pragma unroll
-  for (int s = 0; s < PD; ++s) ring[s] = *reinterpret_cast<const bf16x8 *>(wrow + 16 * s);
-}
-template <int H>
-__device__ __forceinline__ void mlp_pass(const __bf16 *wrow, const char *img, int r, int h,
-                                         bf16x8 (&ring)[PD + 1], f32x16 (&acc)[2]) {
-  constexpr int KS = H / 16;
-  static_assert(KS % (PD + 1) == 0, "ring period must divide the k-steps");
-  const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
-  const char *rowp = img + r * (2 * H);
-#pragma unroll 1
-  for (int s0 = 0; s0 < KS; s0 += PD + 1) {
-#pragma unroll
-    for (int u = 0; u <= PD; ++u) {
-      const int s = s0 + u;
-      const bf16x8 af = ring[u];
-      if (s + PD < KS)
-        ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wrow + 16 * (s + PD));
-      const char *p = rowp + 16 * ((2 * s + h) ^ swz);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
-    }
-  }
-}
-
-}  // namespace fu
 
 using namespace fu;
 

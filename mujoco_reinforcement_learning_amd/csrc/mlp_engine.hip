@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "common.h"
+#include "fused_policy.h"
 #include "fused_update.h"
 #include "timing.h"
 
@@ -1461,23 +1462,11 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
 
 static const int g_fused_enabled = env_knob("PPO_FUSED", 1);
 
-// Precision bf16 with supported shapes: gather + bf16 weight refresh, the persistent fused
-// forward/loss/backward kernel (one partial-gradient slab per workgroup), then the fixed-order
-// slab reduction.  Same contract as the layered path below.
-static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
-                                const float *old_logp_d, const float *adv_d,
-                                const float *vtarget_d, const int32_t *rows_d, int b,
-                                const int32_t *count_d, float clip_lo, float clip_hi,
-                                float entropy_coef, float inv_b, float inv_ba, float *grad_d,
-                                float *loss_d, hipStream_t st) {
-  const int H = ctx->fused_hidden;
-  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
-  const int A = ctx->cfg.act_dim;
-  const int64_t P = ctx->total_params;
-  FusedArgs q{};
+// Pointers of both nets for the fused kernels (bf16 images from ctx->fw, f32 masters in params).
+static void fused_nets(const ppo_ctx *ctx, FusedNet (&out)[2]) {
   for (int z = 0; z < 2; ++z) {
     const NetDesc &nd = ctx->net[z];
-    FusedNet &fn = q.net[z];
+    FusedNet &fn = out[z];
     fn.w0b = ctx->fw[z][0];
     fn.w1b = ctx->fw[z][1];
     fn.w1bt = ctx->fw[z][2];
@@ -1494,6 +1483,27 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
     fn.off_wh = nd.layer[2].w_off;
     fn.off_bh = nd.layer[2].b_off;
   }
+}
+
+static bool fused_active(const ppo_ctx *ctx) {
+  return ctx->prec == PPO_PREC_BF16 && ctx->fused_ok && g_fused_enabled;
+}
+
+// Precision bf16 with supported shapes: gather + bf16 weight refresh, the persistent fused
+// forward/loss/backward kernel (one partial-gradient slab per workgroup), then the fixed-order
+// slab reduction.  Same contract as the layered path below.
+static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                                const float *old_logp_d, const float *adv_d,
+                                const float *vtarget_d, const int32_t *rows_d, int b,
+                                const int32_t *count_d, float clip_lo, float clip_hi,
+                                float entropy_coef, float inv_b, float inv_ba, float *grad_d,
+                                float *loss_d, hipStream_t st) {
+  const int H = ctx->fused_hidden;
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  const int A = ctx->cfg.act_dim;
+  const int64_t P = ctx->total_params;
+  FusedArgs q{};
+  fused_nets(ctx, q.net);
   q.logstd = ctx->params + ctx->net[0].logstd_off;
   q.off_logstd = ctx->net[0].logstd_off;
   q.xb = ctx->fxb;
@@ -1542,7 +1552,9 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
     const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
                       4.0 * q.G * static_cast<double>(P) + 2.0 * q.G * 2.0 * H * (kFusedKX + 2.0 * H);
     const TimRec rec{KC_FUSED,
-                     tim_active() ? intern_name("fused_update_kernel<%d, %d>", H, q.act) : nullptr,
+                     tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act,
+                                                A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8)
+                                  : nullptr,
                      fl, by};
     if (int rc = fused_update_launch(q, rec, st)) return rc;
   }
@@ -1847,6 +1859,94 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   return 0;
 }
 
+extern "C" int ppo_pack_weights(ppo_ctx *ctx, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!fused_active(ctx)) return 0;  // the layered path reads the f32 masters directly
+  TimingScope timing_scope(ctx);
+  FusedArgs q{};
+  fused_nets(ctx, q.net);
+  q.b = 0;
+  q.din = ctx->cfg.obs_dim * ctx->cfg.window;
+  q.hidden = ctx->fused_hidden;
+  const double H = ctx->fused_hidden;
+  const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
+                   2.0 * (4.0 * H * (q.din + H) + 2.0 * H * (kFusedKX + 2.0 * H))};
+  return fused_prep_launch(q, rec, as_stream(stream));
+}
+
+extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d,
+                               const uint8_t *reset_d, int all_reset, const int32_t *bounds,
+                               int n_bounds, int normalize, float *state_d, int n,
+                               const float *eps_d, uint64_t seed, uint64_t offset,
+                               float *action_d, float *logp_d, float *value_d, float *mean_d,
+                               void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  const int o = ctx->cfg.obs_dim, w = ctx->cfg.window;
+  PPO_REQUIRE(window_d && state_d && n > 0, "ppo_observe_act: null window/state or n <= 0");
+  PPO_REQUIRE(n <= ctx->cfg.max_rows, "ppo_observe_act: n=%d exceeds max_rows=%d", n,
+              ctx->cfg.max_rows);
+  PPO_REQUIRE(n_bounds >= 0 && n_bounds < 16, "ppo_observe_act: too many slices (%d)", n_bounds);
+  PolicySlices tab{};
+  tab.count = normalize ? n_bounds : 0;
+  for (int i = 0; i <= n_bounds && normalize; ++i) {
+    PPO_REQUIRE(bounds != nullptr, "ppo_observe_act: null bounds");
+    PPO_REQUIRE(bounds[i] >= 0 && bounds[i] <= o && (i == 0 || bounds[i] >= bounds[i - 1]),
+                "ppo_observe_act: bounds must be ascending within [0, O]");
+    tab.edge[i] = bounds[i];
+  }
+  if (!fused_active(ctx) || w > kPolicyMaxWindow) {  // layered: A1 kernels, then GEMM policy step
+    if (obs_d) {
+      int rc = ppo_obs_window_push(window_d, obs_d, 1, reset_d, all_reset, n, o, w, stream);
+      if (rc) return rc;
+    }
+    if (int rc = ppo_obs_normalize(window_d, state_d, n, o, w, bounds, n_bounds, normalize, stream))
+      return rc;
+    return ppo_policy_step(ctx, state_d, n, eps_d, seed, offset, action_d, logp_d, value_d,
+                           mean_d, stream);
+  }
+  TimingScope timing_scope(ctx);
+  PolicyFusedArgs q{};
+  fused_nets(ctx, q.net);
+  q.logstd = ctx->params + ctx->net[0].logstd_off;
+  q.n = n;
+  q.obs_dim = o;
+  q.window = w;
+  q.act_dim = ctx->cfg.act_dim;
+  q.act = ctx->cfg.activation;
+  q.hidden = ctx->fused_hidden;
+  q.omv = ctx->cfg.output_max_value;
+  q.window_d = window_d;
+  q.obs_d = obs_d;
+  q.reset_d = reset_d;
+  q.all_reset = all_reset;
+  q.tab = tab;
+  q.normalize = normalize;
+  q.state_d = state_d;
+  q.do_actor = (action_d || logp_d || mean_d) ? 1 : 0;
+  q.do_critic = value_d ? 1 : 0;
+  q.eps = eps_d;
+  q.seed = seed;
+  q.offset = offset;
+  q.offset_base = ctx->rng_counter;
+  q.action = action_d;
+  q.logp = logp_d;
+  q.value = value_d;
+  q.mean = mean_d;
+  const double H = ctx->fused_hidden, A = ctx->cfg.act_dim, din = o * w;
+  const double fl = 2.0 * n * ((q.do_actor ? din * H + H * H + A * H : 0.0) +
+                               (q.do_critic ? din * H + H * H + H : 0.0));
+  const double by = static_cast<double>(n) *
+                    (8.0 * o * w * (obs_d ? 2.0 : 1.0) + (obs_d ? 8.0 * o : 0.0) + 4.0 * din +
+                     (eps_d ? 4.0 * A : 0.0) + (action_d ? 4.0 * A : 0.0) + (mean_d ? 4.0 * A : 0.0) +
+                     (logp_d ? 4.0 : 0.0) + (value_d ? 4.0 : 0.0));
+  const TimRec rec{KC_POLICY_HEAD,
+                   tim_active() ? intern_name("policy_fused_kernel<%d, %d, %d>", ctx->fused_hidden, q.act,
+                                             q.act_dim <= 2 ? 2 : q.act_dim <= 4 ? 4 : q.act_dim <= 6 ? 6 : 8)
+                                : nullptr,
+                   fl, by};
+  return policy_fused_launch(q, rec, as_stream(stream));
+}
+
 extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                                   const float *old_logp_d, const float *adv_d,
                                   const float *vtarget_d, const int32_t *rows_d, int b,
@@ -1860,7 +1960,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
               b, ctx->cfg.max_rows);
   hipStream_t st = as_stream(stream);
   TimingScope timing_scope(ctx);
-  if (ctx->prec == PPO_PREC_BF16 && ctx->fused_ok && g_fused_enabled)
+  if (fused_active(ctx))
     return fused_minibatch_grad(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d, b,
                                 count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
                                 loss_d, st);

@@ -125,6 +125,44 @@ class Engine:
                                        ptr(action), ptr(logp), ptr(value), ptr(mean),
                                        _stream(self.device)))
 
+    def pack_weights(self) -> None:
+        """Refresh the bf16 weight images of the fused kernels from the bound parameters (after
+        an optimizer step, before a rollout).  No-op outside the fused bf16 path."""
+        check(self.lib.ppo_pack_weights(self._ctx, _stream(self.device)))
+
+    def observe_act(self, window: torch.Tensor, state: torch.Tensor, obs: Optional[torch.Tensor] = None,
+                    reset: Optional[torch.Tensor] = None, all_reset: bool = False,
+                    normalize: bool = True, eps: Optional[torch.Tensor] = None, seed: int = 0,
+                    offset: int = 0, action=None, logp=None, value=None, mean=None) -> None:
+        """A1-A4 for one rollout step (ppo_observe_act): push ``obs`` (N, O) f64 into ``window``
+        (N, O, W) f64 (in place; skipped when obs is None), standardise into ``state`` (N, W*O)
+        f32, then sample / evaluate like :meth:`policy_step`."""
+        n, o, w = window.shape
+        _need(window, "window", torch.float64, device=self.device)
+        if (o, w) != (self.obs_dim, self.window):
+            raise RuntimeError(f"window is {(o, w)}, expected (O, W) = {(self.obs_dim, self.window)}")
+        _need(state, "state", torch.float32, device=self.device)
+        if state.numel() != n * o * w:
+            raise RuntimeError(f"state must hold (N, W*O) = {(n, o * w)} floats")
+        if obs is not None:
+            _need(obs, "obs", torch.float64, (n, o), self.device)
+        if reset is not None:
+            _need(reset, "reset", None, (n,), self.device)
+        if eps is not None:
+            _need(eps, "eps", torch.float32, (n, self.act_dim), self.device)
+        for name, t, k in (("action", action, self.act_dim), ("logp", logp, 1), ("value", value, 1),
+                           ("mean", mean, self.act_dim)):
+            if t is not None:
+                _need(t, name, torch.float32, device=self.device)
+                if t.numel() != n * k:
+                    raise RuntimeError(f"{name} has {t.numel()} elements, expected {n * k}")
+        edges = slice_edges(o)
+        arr = (ctypes.c_int32 * len(edges))(*edges)
+        check(self.lib.ppo_observe_act(self._ctx, ptr(window), ptr(obs), ptr(reset),
+                                       int(all_reset), arr, len(edges) - 1, int(normalize),
+                                       ptr(state), n, ptr(eps), seed, offset, ptr(action),
+                                       ptr(logp), ptr(value), ptr(mean), _stream(self.device)))
+
     def set_precision(self, precision: str) -> None:
         """GEMM precision: "f32" (parity with the reference, default) or "bf16" (bf16 operands,
         f32 accumulation; activations, params and optimizer state stay f32)."""

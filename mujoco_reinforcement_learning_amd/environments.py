@@ -128,6 +128,21 @@ class SyntheticVecEnvHelper:
         self.timestep.terminated = term
         self.t = t + 1
 
+    def step_raw(self, action: torch.Tensor, reward_out: torch.Tensor,
+                 terminated_out: torch.Tensor) -> torch.Tensor:
+        """The physics half of :meth:`step`: advance the envs and return the new observation
+        (N, O) f64 without pushing it into the window, so the engine's fused observe + act
+        (ppo_observe_act) can push, standardise and act in one launch."""
+        t = self.t
+        if t >= self.horizon:
+            raise RuntimeError("synthetic VecEnv: horizon exhausted; call reset_environment()")
+        E.synthetic_env_step(self.base_obs[t + 1], self.base_reward[t], self.base_terminated[t],
+                             action.contiguous(), self._obs_next, reward_out, terminated_out)
+        self.timestep.reward = reward_out
+        self.timestep.terminated = terminated_out
+        self.t = t + 1
+        return self._obs_next
+
     def get_state(self, test_phase: bool = False, out: Optional[torch.Tensor] = None):
         """(N, W, O) ``Run.dtype`` state (running_gym_sequential_vectorized.py:150-159)."""
         ts = self.test_timestep if test_phase else self.timestep

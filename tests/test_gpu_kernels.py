@@ -423,3 +423,98 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b, 
     got = loss.cpu()
     assert abs(float(got[0]) - la_ref) <= 1e-3 * (abs(la_ref) + 1e-2), (float(got[0]), la_ref)
     assert abs(float(got[1]) - lc_ref) <= 1e-3 * (abs(lc_ref) + 1e-2), (float(got[1]), lc_ref)
+
+
+# ------------------------------------------------------------- fused observe + act (A1-A4)
+@pytest.mark.parametrize("act,n,window,obs,na,reset_p", [("relu", 4096, 1, 17, 6, 0.0),
+                                                          ("tanh", 1000, 1, 17, 6, 0.1),
+                                                          ("elu", 300, 1, 27, 8, 0.5),
+                                                          ("relu", 77, 1, 11, 3, 0.3)])
+def test_observe_act_fused_matches_layered(gpu, act, n, window, obs, na, reset_p):
+    """precision="bf16", 2x256: ppo_observe_act (one fused launch: window push, f64
+    standardisation, both MLPs on bf16 MFMA, heads, sampling) against the A1 kernels + the
+    layered bf16 policy_step on the same context.  Window and state are bit-exact (same f64
+    arithmetic); actions / log-probs / values agree to f32 summation order of identical
+    bf16-operand products (rtol 2e-4 relative to each output's scale)."""
+    E = _E()
+    run, eng, ref, cfg = _agents(gpu, 7, num_envs=n, hidden=(256, 256), activation=act,
+                                 batch_size=n, precision="bf16", obs_dim=obs, act_dim=na)
+    e = eng.engine
+    g = torch.Generator().manual_seed(n + obs)
+    win0 = torch.randn(n, obs, window, generator=g, dtype=torch.float64)
+    new_obs = torch.randn(n, obs, generator=g, dtype=torch.float64)
+    reset = (torch.rand(n, generator=g) < reset_p).to(torch.uint8)
+    eps = torch.randn(n, na, generator=g)
+    outs = {}
+    for mode in ("fused", "layered"):
+        win = win0.clone().to(gpu)
+        st = torch.empty(n, window * obs, device=gpu)
+        act_, lp, val, mu = (torch.empty(n, na, device=gpu), torch.empty(n, device=gpu),
+                             torch.empty(n, device=gpu), torch.empty(n, na, device=gpu))
+        if mode == "fused":
+            e.pack_weights()
+            e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), eps=eps.to(gpu),
+                          action=act_, logp=lp, value=val, mean=mu)
+        else:
+            E.obs_window_push(win, new_obs.to(gpu), reset=reset.to(gpu))
+            E.obs_normalize(win, st)
+            e.policy_step(st, eps=eps.to(gpu), action=act_, logp=lp, value=val, mean=mu)
+        torch.cuda.synchronize()
+        outs[mode] = [x.cpu() for x in (win, st, act_, lp, val, mu)]
+    f, l = outs["fused"], outs["layered"]
+    assert torch.equal(f[0], l[0]), "window push differs"
+    assert torch.equal(f[1], l[1]), "standardised state differs"
+    for name, a, b in zip(("action", "logp", "value", "mean"), f[2:], l[2:]):
+        scale = float(b.abs().max()) + 1e-6
+        err = float((a - b).abs().max())
+        assert err <= 2e-4 * scale, (name, err, scale)
+    # value-only call (t = T) and action-only call
+    win = win0.clone().to(gpu)
+    st = torch.empty(n, window * obs, device=gpu)
+    val = torch.full((n,), float("nan"), device=gpu)
+    e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), value=val)
+    assert torch.allclose(val.cpu(), l[4], rtol=0, atol=2e-4 * (float(l[4].abs().max()) + 1e-6))
+    win = win0.clone().to(gpu)
+    act_ = torch.full((n, na), float("nan"), device=gpu)
+    e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), eps=eps.to(gpu), action=act_)
+    assert torch.isfinite(act_).all()
+
+
+def test_fused_kernels_bitwise_deterministic(gpu):
+    """The fused bf16 kernels reduce in a fixed order: repeating a call on the same inputs gives
+    bit-identical outputs (rollout policy step and minibatch gradient at the bench shapes)."""
+    n, t, b = 4096, 16, 65536 // 4
+    run, eng, ref, cfg = _agents(gpu, 11, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    g = torch.Generator().manual_seed(3)
+    win0 = torch.randn(n, 17, 1, generator=g, dtype=torch.float64).to(gpu)
+    obs = torch.randn(n, 17, generator=g, dtype=torch.float64).to(gpu)
+    eps = torch.randn(n, 6, generator=g).to(gpu)
+    e.pack_weights()
+    outs = []
+    for _ in range(6):
+        win = win0.clone()
+        st = torch.empty(n, 17, device=gpu)
+        a, lp, v, mu = (torch.empty(n, 6, device=gpu), torch.empty(n, device=gpu),
+                        torch.empty(n, device=gpu), torch.empty(n, 6, device=gpu))
+        e.observe_act(win, st, obs=obs, eps=eps, action=a, logp=lp, value=v, mean=mu)
+        outs.append(torch.cat([st.flatten(), a.flatten(), lp, v, mu.flatten(), win.flatten().float()]))
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), int((o != outs[0]).sum())
+    rows_total = n * t
+    states = torch.randn(rows_total, 17, generator=g).to(gpu)
+    actions = torch.randn(rows_total, 6, generator=g).to(gpu)
+    old_lp = torch.randn(rows_total, generator=g).to(gpu) - 5
+    adv = torch.randn(rows_total, generator=g).to(gpu)
+    vt = torch.randn(rows_total, generator=g).to(gpu)
+    rows = torch.randperm(rows_total, generator=g)[:b].to(torch.int32).to(gpu)
+    grads = []
+    for _ in range(4):
+        grad = torch.empty(e.n_params, device=gpu)
+        loss = torch.empty(2, device=gpu)
+        e.minibatch_grad(states, actions, old_lp, adv, vt, rows, b, grad, loss, 0.9, 1.1, 1e-4,
+                         1.0 / b, 1.0 / (b * 6))
+        grads.append(torch.cat([grad, loss]))
+    for gr in grads[1:]:
+        assert torch.equal(gr, grads[0]), int((gr != grads[0]).sum())
