@@ -57,6 +57,10 @@ def parse():
     p.add_argument("--cpu-rollout-steps", type=int, default=32)
     p.add_argument("--cpu-epochs", type=int, default=1)
     p.add_argument("--no-timing", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--timing-iters", type=int, default=2,
+                   help="eager iterations after the timed region that carry per-kernel events")
+    p.add_argument("--no-graphs", action="store_true",
+                   help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     return p.parse_args()
@@ -77,10 +81,13 @@ def roofline(name, c, traffic, force_hbm=False):
     (bytes / 8 TB/s); achieved = that work per launch / mean launch duration."""
     launches = max(c["launches"], 1)
     avg_s = c["ms"] * 1e-3 / launches
-    peak_f = PEAK_BF16_MFMA_TFLOPS if "bf16" in name else PEAK_FP32_MFMA_TFLOPS
+    # the fused update kernel is bf16-only; the layered GEMMs carry their dtype in the name
+    bf16 = "bf16" in name or c["class"] == "fused_update"
+    peak_f = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     t_mfma = c["flops"] / (peak_f * 1e12)
     t_hbm = c["bytes"] / (PEAK_HBM_GBS * 1e9)
-    mfma = c["class"].startswith("gemm") and t_mfma >= t_hbm and not force_hbm
+    mfma = (c["class"].startswith("gemm") or c["class"] == "fused_update") and t_mfma >= t_hbm \
+        and not force_hbm
     if mfma:
         achieved, peak, unit = c["flops"] / launches / avg_s / 1e12, peak_f, "TFLOP/s"
     else:
@@ -156,7 +163,8 @@ def main():
     n, t = args.num_envs, args.horizon
     run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
                    hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
-                   seed=rank, precision=args.precision)
+                   seed=rank, precision=args.precision, rollout_graph=not args.no_graphs,
+                   train_graph=not args.no_graphs)
     torch.manual_seed(0)  # identical initial parameters on every rank
     agent = PPOEngineAgent(run, device=dev)
     streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
@@ -165,11 +173,6 @@ def main():
 
     for _ in range(args.warmup):
         algo._iterate()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    if not args.no_timing:
-        agent.engine.timing(True, capacity=200000)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -184,9 +187,22 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt)
-    classes = agent.engine.timing_read() if not args.no_timing else {}
-    kernels = agent.engine.timing_kernels() if not args.no_timing else {}
-    agent.engine.timing(False)
+    classes, kernels = {}, {}
+    if not args.no_timing:
+        # Per-kernel durations: HIP event pairs on each dispatch packet, over --timing-iters
+        # iterations of the same workload run right after the timed region with the hipGraphs
+        # off (a replayed graph node cannot carry a per-dispatch event pair).
+        ec = run.engine_config
+        saved = (ec.rollout_graph, ec.train_graph)
+        ec.rollout_graph, ec.train_graph = False, False
+        agent.engine.timing(True, capacity=200000)
+        for _ in range(args.timing_iters):
+            algo._iterate()
+        torch.cuda.synchronize()
+        classes = agent.engine.timing_read()
+        kernels = agent.engine.timing_kernels()
+        agent.engine.timing(False)
+        ec.rollout_graph, ec.train_graph = saved
 
     value = world * n * t * args.steps / elapsed
     line = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
@@ -198,7 +214,7 @@ def main():
                                     f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
                                     f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
-                       "epochs": args.epochs, "rng": args.rng,
+                       "epochs": args.epochs, "rng": args.rng, "hipgraphs": not args.no_graphs,
                        "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
     if kernels:
         traffic = load_traffic(args.traffic)
@@ -208,9 +224,10 @@ def main():
         if gae:
             gname, gc = max(gae.items(), key=lambda kv: kv[1]["ms"])
             line["gae_roofline"] = roofline(gname, gc, traffic, force_hbm=True)
-        line["kernel_classes_ms_per_step"] = {k: v["ms"] / args.steps for k, v in classes.items()
+        ti = max(args.timing_iters, 1)
+        line["kernel_classes_ms_per_step"] = {k: v["ms"] / ti for k, v in classes.items()
                                               if v["launches"]}
-        line["kernels_ms_per_step"] = {k: round(v["ms"] / args.steps, 4) for k, v in
+        line["kernels_ms_per_step"] = {k: round(v["ms"] / ti, 4) for k, v in
                                        sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
     if rank == 0 and world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, hidden)

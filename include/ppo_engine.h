@@ -183,6 +183,13 @@ int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n, in
              float neg_step_actor, float neg_step_critic, float one_minus_beta1, float beta2,
              float one_minus_beta2, float bc2_sqrt, float eps, void *stream);
 
+/* ppo_adam with the step-dependent scalars in device memory: sched_d = {neg_step_actor,
+ * neg_step_critic, bc2_sqrt} (f32, computed by the host as for ppo_adam), read when the kernel
+ * runs -- lets a hipGraph-captured optimizer loop replay with a per-iteration schedule. */
+int ppo_adam_sched(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n,
+                   int64_t n_actor, const float *sched_d, float one_minus_beta1, float beta2,
+                   float one_minus_beta2, float eps, void *stream);
+
 /* ---- measurement: per-kernel-class timing (no reference counterpart; replaces @timeit,
  * error_handling_utils.py:5-17, with device-side timing) -----------------------------------------
  * enable=1 (re)starts recording a HIP event pair around every launch the ctx issues, on the

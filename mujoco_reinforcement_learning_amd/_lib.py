@@ -74,6 +74,9 @@ _SIGNATURES = {
                                       POINTER(c_double)]),
     "ppo_ctx_phase_stamps": (c_int, [c_void_p, c_int, c_void_p, c_int]),
     "ppo_pack_weights": (c_int, [c_void_p, c_void_p]),
+    "ppo_adam_sched": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                               ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                               c_void_p]),
     "ppo_observe_act": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                                 c_int, c_void_p, c_int, c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

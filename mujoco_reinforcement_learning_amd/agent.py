@@ -199,6 +199,26 @@ class PPOEngineAgent:
         E.adam(self.flat_params, self.flat_grad, self.flat_m, self.flat_v, self.engine.n_actor,
                neg_a, neg_c, 1 - beta1, beta2, 1 - beta2, bc2, oa.param_groups[0]["eps"])
 
+    def adam_schedule(self, steps: int):
+        """Host-computed Adam scalars for the next ``steps`` joint steps of both optimizers, as an
+        (steps, 4) f32 tensor of (neg_step_actor, neg_step_critic, bc2_sqrt, 0) rows (the values
+        step_both would pass to ppo_adam), advancing both step counters; None when the two
+        optimizers' hyper-parameters differ (then step_both's per-net path is required)."""
+        oa, oc = self.optimizers["actor"], self.optimizers["critic"]
+        ga, gc = oa.param_groups[0], oc.param_groups[0]
+        if ga["betas"] != gc["betas"] or ga["eps"] != gc["eps"] or oa.step_count != oc.step_count:
+            return None
+        rows = []
+        for k in range(oa.step_count + 1, oa.step_count + steps + 1):
+            neg_a, bc2 = oa.scalars(k)
+            neg_c, bc2c = oc.scalars(k)
+            if bc2 != bc2c:
+                return None
+            rows.append((neg_a, neg_c, bc2, 0.0))
+        oa.step_count += steps
+        oc.step_count += steps
+        return torch.tensor(rows, dtype=torch.float32)
+
     # ---- Agent API ---------------------------------------------------------------------------
     def _as_state(self, state: torch.Tensor) -> torch.Tensor:
         s = state.to(device=self.device, dtype=torch.float32)

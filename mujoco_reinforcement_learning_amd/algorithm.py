@@ -200,6 +200,63 @@ class PPOEngine:
             E.normalize_rows(buf.value_target, run.ppo_config.advantage_scaler)
 
     # ---- ppo.py:93-154 ---------------------------------------------------------------------
+    def _train_graph_ok(self) -> bool:
+        return (self._rng() == "philox" and not self.dp.active and
+                bool(getattr(self.run.engine_config, "train_graph", True)))
+
+    def _train_graphed(self, memory: RolloutBuffer, b: int, epochs: int, batches: int, clip_lo,
+                       clip_hi, inv_b, inv_ba):
+        """The E x M optimizer steps as one hipGraph replay (philox, single rank): the minibatch
+        rows of every epoch are drawn first (E Feistel launches), the Adam step sizes of the
+        iteration are uploaded as a device schedule, and the captured loop of M*E x (gather,
+        fused forward/backward, slab reduction, Adam) replays with them.  Same arithmetic as the
+        eager loop below."""
+        agent, eng, buf = self.agent, self.agent.engine, memory
+        n, t_len = buf.num_envs, buf.horizon
+        dev = agent.device
+        steps = epochs * batches
+        sched = agent.adam_schedule(steps)
+        if sched is None:
+            return None
+        key = (b, epochs, batches)
+        if getattr(self, "_tg_key", None) != key:
+            self._tg_key = key
+            self._tg_rows = torch.empty(epochs, batches * b, dtype=torch.int32, device=dev)
+            self._tg_sched = torch.empty(steps, 4, dtype=torch.float32, device=dev)
+            self._tg_graph = None
+            self._tg_warm = False
+        for epoch in range(epochs):
+            E.feistel_rows(self._seed(), self.iteration * epochs + epoch, 0, batches * b, n, t_len,
+                           self._tg_rows[epoch])
+        self._tg_sched.copy_(sched, non_blocking=True)
+        beta1, beta2 = agent.optimizers["actor"].param_groups[0]["betas"]
+        eps = agent.optimizers["actor"].param_groups[0]["eps"]
+        ppo = self.run.ppo_config
+
+        def body():
+            for epoch in range(epochs):
+                for i in range(batches):
+                    eng.minibatch_grad(buf.states, buf.actions, buf.logp, buf.advantage,
+                                       buf.value_target, self._tg_rows[epoch, i * b:(i + 1) * b],
+                                       b, agent.flat_grad, self._loss_buf[epoch, i], clip_lo,
+                                       clip_hi, ppo.entropy_eps, inv_b, inv_ba)
+                    E.adam_sched(agent.flat_params, agent.flat_grad, agent.flat_m, agent.flat_v,
+                                 eng.n_actor, self._tg_sched[epoch * batches + i], 1 - beta1, beta2,
+                                 1 - beta2, eps)
+
+        if self._tg_graph is None:
+            if not self._tg_warm:  # first call eager: lazy workspace / timing setup outside capture
+                self._tg_warm = True
+                body()
+                return self._loss_buf
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                body()
+            self._tg_graph = g
+        self._tg_graph.replay()
+        return self._loss_buf
+
     def train(self, memory: RolloutBuffer):
         run, agent, eng, buf = self.run, self.agent, self.agent.engine, memory
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
@@ -231,6 +288,14 @@ class PPOEngine:
         inv_b = 1.0 / b_global
         inv_ba = 1.0 / (b_global * a)
         states = buf.states
+        if self._train_graph_ok():
+            out = self._train_graphed(memory, b, epochs, batches_per_epoch, clip_lo, clip_hi,
+                                      inv_b, inv_ba)
+            if out is not None:
+                if run.dynamic_config.current_episode < 2500:
+                    for scheduler in agent.schedulers.values():
+                        scheduler.step()
+                return out
         for epoch in range(epochs):
             if self._rng() == "torch":
                 perm = torch.randperm((n_glob if exact else n) * t_len).to(dev, non_blocking=True)

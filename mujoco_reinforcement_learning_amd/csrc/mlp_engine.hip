@@ -1549,8 +1549,10 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
       const double a = z == 0 ? A : 1;
       fl += 2.0 * b * ((din * H + H * H + a * H) + (H * H + a * H) + (din * H + H * H + a * H));
     }
+    // HBM bytes: the staged rows once, the bf16 weight images once (every workgroup re-reads
+    // them from L2, which is not HBM traffic) and one partial-gradient slab per workgroup
     const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
-                      4.0 * q.G * static_cast<double>(P) + 2.0 * q.G * 2.0 * H * (kFusedKX + 2.0 * H);
+                      4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
     const TimRec rec{KC_FUSED,
                      tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act,
                                                 A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8)

@@ -423,6 +423,27 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
   v[i] = vi;
 }
 
+// Same update with the step-dependent scalars (neg_step_actor, neg_step_critic, bc2_sqrt) read
+// from device memory when the kernel runs: a hipGraph-captured optimizer loop replays with the
+// schedule the host uploads for each iteration.
+__global__ void adam_sched_kernel(float *__restrict__ p, const float *__restrict__ g,
+                                  float *__restrict__ m, float *__restrict__ v, int64_t n,
+                                  int64_t n_actor, const float *__restrict__ sched, float w1,
+                                  float b2, float omb2, float eps) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float neg_step_a = sched[0], neg_step_c = sched[1], bc2_sqrt = sched[2];
+  const float gi = g[i];
+  float mi = m[i];
+  mi = (w1 < 0.5f) ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.f, gi - mi, gi);
+  const float vi = fmaf(omb2 * gi, gi, v[i] * b2);
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  const float ns = (i < n_actor) ? neg_step_a : neg_step_c;
+  p[i] = p[i] + (ns * mi) / denom;
+  m[i] = mi;
+  v[i] = vi;
+}
+
 }  // namespace ppo
 
 // ==============================================================================================
@@ -673,6 +694,19 @@ extern "C" int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, in
   launch_k(TimRec{KC_ADAM, "adam_kernel", 0.0, 28.0 * n}, adam_kernel, dim3(ceil_div(n, 256)),
            dim3(256), 0, as_stream(stream), p_d, g_d, m_d, v_d, n, n_actor, neg_step_actor,
            neg_step_critic, one_minus_beta1, beta2, one_minus_beta2, bc2_sqrt, eps);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_adam_sched(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n,
+                              int64_t n_actor, const float *sched_d, float one_minus_beta1,
+                              float beta2, float one_minus_beta2, float eps, void *stream) {
+  PPO_REQUIRE(p_d && g_d && m_d && v_d && sched_d && n > 0 && n_actor >= 0 && n_actor <= n,
+              "ppo_adam_sched: bad args");
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_ADAM, "adam_sched_kernel", 0.0, 28.0 * n}, adam_sched_kernel,
+           dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), p_d, g_d, m_d, v_d, n, n_actor,
+           sched_d, one_minus_beta1, beta2, one_minus_beta2, eps);
   PPO_LAUNCHED();
   return 0;
 }

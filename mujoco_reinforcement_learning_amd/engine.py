@@ -360,3 +360,18 @@ def philox_normal(seed: int, offset: int, out: torch.Tensor) -> None:
     lib = _lib.load()
     _need(out, "out", torch.float32)
     check(lib.ppo_philox_normal(seed, offset, ptr(out), out.numel(), _stream(out.device)))
+
+
+def adam_sched(p, g, m, v, n_actor: int, sched: torch.Tensor, one_minus_beta1: float, beta2: float,
+               one_minus_beta2: float, eps: float) -> None:
+    """ppo_adam_sched: Adam with (neg_step_actor, neg_step_critic, bc2_sqrt) = sched[0:3] read
+    from device memory at run time (graph-captured optimizer loops)."""
+    lib = _lib.load()
+    n = p.numel()
+    for name, t in (("p", p), ("g", g), ("m", m), ("v", v)):
+        _need(t, name, torch.float32, (n,), p.device)
+    _need(sched, "sched", torch.float32, None, p.device)
+    if sched.numel() < 3:
+        raise RuntimeError("sched must hold 3 floats")
+    check(lib.ppo_adam_sched(ptr(p), ptr(g), ptr(m), ptr(v), n, int(n_actor), ptr(sched),
+                             one_minus_beta1, beta2, one_minus_beta2, eps, _stream(p.device)))

@@ -129,6 +129,9 @@ class EngineConfig:
     rollout_graph: with rng="philox" and a device-resident VecEnv helper (``graph_safe``),
          capture the T-step rollout once as a hipGraph and replay it each iteration (no host
          launch overhead per step; the Philox offset base is a device counter).
+    train_graph: with rng="philox" on a single rank, capture the E x M optimizer steps of an
+         iteration once as a hipGraph (minibatch rows of all epochs drawn up front, Adam step
+         sizes read from a device schedule) and replay it each iteration.
     precision: "f32" (every GEMM in f32, parity with the reference) or "bf16" (fc-layer GEMM
          operands rounded to bf16 with f32 accumulation; params, optimizer state, activations,
          heads, losses and GAE stay f32) -- BASELINE.json configs[1].
@@ -138,6 +141,7 @@ class EngineConfig:
     seed: int = 0
     dp_mode: str = "local"
     rollout_graph: bool = True
+    train_graph: bool = True
     precision: str = "f32"
 
 

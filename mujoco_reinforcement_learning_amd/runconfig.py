@@ -20,7 +20,8 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
              normalize_rewards: bool = False, normalize_observations: bool = True,
              advantage_scaler: float = 1.0, use_bias: bool = True, output_max_value: float = 1.0,
              rng: str = "torch", seed: int = 0, dp_mode: str = "local",
-             rollout_graph: bool = True, precision: str = "f32", experiment_path: str = "/tmp/ppo_engine_run",
+             rollout_graph: bool = True, train_graph: bool = True, precision: str = "f32",
+             experiment_path: str = "/tmp/ppo_engine_run",
              replace: bool = True) -> Run:
     """Defaults: the headline HalfCheetah config (BASELINE.json configs[1]) with main.py's PPO
     hyper-parameters (lr 1e-4, gamma 0.99, lambda 0.98, clip 0.1, entropy 1e-4, E=10)."""
@@ -52,4 +53,5 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
                                           critic_hidden_shapes=list(critic_hidden)
                                           if critic_hidden else None, seed=seed,
                                           dp_mode=dp_mode, rollout_graph=rollout_graph,
+                                          train_graph=train_graph,
                                           precision=precision))

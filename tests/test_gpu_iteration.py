@@ -120,24 +120,32 @@ def test_philox_mode_runs_and_is_reproducible(gpu):
     assert torch.equal(outs[0], outs[1]), "philox mode must be bit-reproducible"
 
 
-def test_graph_rollout_matches_eager(gpu):
-    """rollout_graph=True (captured once, replayed with the device Philox counter) produces the
-    same buffers and parameters, bit for bit, as the eager launch sequence over 3 iterations
-    (iteration 0 eager warm-up, 1 capture + replay, 2 replay)."""
+@pytest.mark.parametrize("prec,hidden,n,b", [("f32", (64, 64), 64, 256),
+                                             ("bf16", (256, 256), 128, 512)])
+def test_graphs_match_eager(gpu, prec, hidden, n, b):
+    """rollout_graph / train_graph (each captured once, replayed with the device Philox counter,
+    the pre-drawn minibatch rows and the device Adam schedule) produce the same buffers and
+    parameters, bit for bit, as the eager launch sequence over 3 iterations (iteration 0 eager
+    warm-up, 1 capture + replay, 2 replay).  bf16 at 2x256 runs the fused kernels."""
     res = []
     for graph in (False, True):
-        algo, agent, *_ = _setup(gpu, n=64, t=16, b=256, epochs=2, rng="philox", seed=4,
-                                 rollout_graph=graph)
+        algo, agent, *_ = _setup(gpu, n=n, t=16, b=b, epochs=2, hidden=hidden, rng="philox",
+                                 seed=4, rollout_graph=graph, train_graph=graph, precision=prec)
         snaps = []
         for _ in range(3):
             algo.iterate(verbose=False)
             torch.cuda.synchronize()
             snaps.append((algo.buffer.actions.cpu().clone(), algo.buffer.logp.cpu().clone(),
-                          algo.buffer.states.cpu().clone(), agent.packed_params().cpu().clone()))
+                          algo.buffer.states.cpu().clone(), agent.packed_params().cpu().clone(),
+                          agent.flat_m.cpu().clone(), agent.flat_v.cpu().clone(),
+                          torch.tensor(algo.last_losses)))
         assert (algo._graph is not None) == graph
+        assert (getattr(algo, "_tg_graph", None) is not None) == graph
+        assert agent.optimizers["actor"].step_count == 3 * 2 * (n * 16 // b)
         res.append(snaps)
+    names = ("actions", "logp", "states", "params", "adam m", "adam v", "losses")
     for it, (e, g) in enumerate(zip(*res)):
-        for name, x, y in zip(("actions", "logp", "states", "params"), e, g):
+        for name, x, y in zip(names, e, g):
             assert torch.equal(x, y), f"iteration {it}: {name} differs between graph and eager"
     # fresh noise every iteration (the counter advanced)
     assert not torch.equal(res[1][1][0], res[1][2][0])

@@ -14,9 +14,10 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-SEGMENTS = ["0 X/rows stage", "1 L0 fwd", "2 L1 fwd MFMA", "3 head partial + A2F", "4 loss",
-            "5 (unused)", "6 d2 + head dW", "7 dW1 wgrad", "8 dgrad L1", "9 d1 store",
-            "10 dW0 wgrad"]
+SEGMENTS = ["0 X stage + W0 frags", "1 L0 fwd (+ W1 ring prime)", "2 L1 fwd MFMA pass",
+            "3 bias/act + A2F + head partial sums", "4 loss heads (per row)",
+            "5 d2 = dz.Wh (VALU) + D2 image + head dW (VALU)", "6 dW1 wgrad (MFMA, tr reads)",
+            "7 dgrad MFMA pass", "8 dgrad epilogue (act', D1 image, bias)", "9 dW0 wgrad", "10 -"]
 
 
 def main():
