@@ -172,6 +172,25 @@ int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions
                        float clip_hi, float entropy_coef, float inv_b, float inv_ba,
                        float *grad_d, float *loss_d, void *stream);
 
+/* Staged minibatch path of the fused bf16 engine (ppo_ctx_fused_active != 0).  Same contract and
+ * same results as ppo_minibatch_grad over the same storage arrays, with the per-row gather
+ * reading one 128 B record per row instead of five scattered arrays:
+ *   ppo_stage_records packs rows [0, n_rows) of the time-major storage arrays (the arguments of
+ *   ppo_minibatch_grad) into ctx-owned records once per iteration (after GAE, before the epochs;
+ *   the first call for a given size allocates and must not be inside a graph capture);
+ *   ppo_minibatch_grad_staged(rows_d, b, count_d, ...) is ppo_minibatch_grad on those records.
+ *   flags PPO_STAGED_WEIGHTS_CURRENT: the bf16 weight images are already current (the previous
+ *   optimizer step was ppo_adam_pack), so the weight refresh is skipped. */
+#define PPO_STAGED_WEIGHTS_CURRENT 1
+int ppo_ctx_fused_active(const ppo_ctx *ctx);
+int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                      const float *old_logp_d, const float *adv_d, const float *vtarget_d,
+                      int64_t n_rows, void *stream);
+int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b, const int32_t *count_d,
+                              float clip_lo, float clip_hi, float entropy_coef, float inv_b,
+                              float inv_ba, float *grad_d, float *loss_d, int flags,
+                              void *stream);
+
 /* ---- A15: fused Adam over the flat buffer (torch.optim.Adam single-tensor path) ----------------
  * replaces optimizers['critic'].step() / optimizers['actor'].step() (ppo.py:122,135) and
  * torch.optim.Adam defaults (ppo_agent.py:15-18).  Elements [0, n_actor) use neg_step_actor,
@@ -189,6 +208,15 @@ int ppo_adam(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n, in
 int ppo_adam_sched(float *p_d, const float *g_d, float *m_d, float *v_d, int64_t n,
                    int64_t n_actor, const float *sched_d, float one_minus_beta1, float beta2,
                    float one_minus_beta2, float eps, void *stream);
+
+/* ppo_adam on the ctx's bound parameters (both nets, n_actor = ppo_param_count(ctx, 0)) that
+ * also writes the updated W0/W1 into the fused kernels' bf16 weight images (ppo_pack_weights'
+ * values), so the next ppo_minibatch_grad_staged may pass PPO_STAGED_WEIGHTS_CURRENT.  sched_d
+ * (nullable) as ppo_adam_sched; NULL -> the three host scalars.  Fused bf16 path only. */
+int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d, const float *sched_d,
+                  float neg_step_actor, float neg_step_critic, float bc2_sqrt,
+                  float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
+                  void *stream);
 
 /* ---- measurement: per-kernel-class timing (no reference counterpart; replaces @timeit,
  * error_handling_utils.py:5-17, with device-side timing) -----------------------------------------

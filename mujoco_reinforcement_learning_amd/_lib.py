@@ -80,6 +80,15 @@ _SIGNATURES = {
     "ppo_observe_act": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                                 c_int, c_void_p, c_int, c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ppo_ctx_fused_active": (c_int, [c_void_p]),
+    "ppo_stage_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_int64, c_void_p]),
+    "ppo_minibatch_grad_staged": (c_int, [c_void_p, c_void_p, c_int, c_void_p, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_float, c_void_p, c_void_p, c_int, c_void_p]),
+    "ppo_adam_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
+                              ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                              ctypes.c_float, ctypes.c_float, c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -183,21 +183,31 @@ class PPOEngineAgent:
         return torch.cat(out)
 
     # ---- fused optimizer step for both networks (ppo.py:122 + :135 in one launch) -------------
-    def step_both(self) -> None:
+    def step_both(self, pack: bool = False) -> bool:
+        """One Adam step of both optimizers in one launch.  pack=True (fused bf16 engine) also
+        refreshes the fused kernels' bf16 weight images (ppo_adam_pack); returns whether the
+        images are current afterwards."""
         oa, oc = self.optimizers["actor"], self.optimizers["critic"]
         oa.step_count += 1
         oc.step_count += 1
         beta1, beta2 = oa.param_groups[0]["betas"]
         neg_a, bc2 = oa.scalars(oa.step_count)
         neg_c, bc2c = oc.scalars(oc.step_count)
-        if bc2 != bc2c or oc.param_groups[0]["betas"] != (beta1, beta2):
+        if (bc2 != bc2c or oc.param_groups[0]["betas"] != (beta1, beta2) or
+                oc.param_groups[0]["eps"] != oa.param_groups[0]["eps"]):
             oa.step_count -= 1
             oc.step_count -= 1
             oa.step()
             oc.step()
-            return
+            return False
+        eps = oa.param_groups[0]["eps"]
+        if pack:
+            self.engine.adam_pack(self.flat_grad, self.flat_m, self.flat_v, None, neg_a, neg_c, bc2,
+                                  1 - beta1, beta2, 1 - beta2, eps)
+            return True
         E.adam(self.flat_params, self.flat_grad, self.flat_m, self.flat_v, self.engine.n_actor,
-               neg_a, neg_c, 1 - beta1, beta2, 1 - beta2, bc2, oa.param_groups[0]["eps"])
+               neg_a, neg_c, 1 - beta1, beta2, 1 - beta2, bc2, eps)
+        return False
 
     def adam_schedule(self, steps: int):
         """Host-computed Adam scalars for the next ``steps`` joint steps of both optimizers, as an

@@ -233,16 +233,29 @@ class PPOEngine:
         eps = agent.optimizers["actor"].param_groups[0]["eps"]
         ppo = self.run.ppo_config
 
+        staged = eng.fused
+        if staged:
+            eng.stage_records(buf.states, buf.actions, buf.logp, buf.advantage, buf.value_target)
+
         def body():
             for epoch in range(epochs):
                 for i in range(batches):
+                    rows = self._tg_rows[epoch, i * b:(i + 1) * b]
+                    sched = self._tg_sched[epoch * batches + i]
+                    if staged:
+                        eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
+                                                  clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
+                                                  weights_current=epoch + i > 0)
+                        eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
+                                      one_minus_beta1=1 - beta1, beta2=beta2,
+                                      one_minus_beta2=1 - beta2, eps=eps)
+                        continue
                     eng.minibatch_grad(buf.states, buf.actions, buf.logp, buf.advantage,
-                                       buf.value_target, self._tg_rows[epoch, i * b:(i + 1) * b],
-                                       b, agent.flat_grad, self._loss_buf[epoch, i], clip_lo,
-                                       clip_hi, ppo.entropy_eps, inv_b, inv_ba)
+                                       buf.value_target, rows, b, agent.flat_grad,
+                                       self._loss_buf[epoch, i], clip_lo, clip_hi,
+                                       ppo.entropy_eps, inv_b, inv_ba)
                     E.adam_sched(agent.flat_params, agent.flat_grad, agent.flat_m, agent.flat_v,
-                                 eng.n_actor, self._tg_sched[epoch * batches + i], 1 - beta1, beta2,
-                                 1 - beta2, eps)
+                                 eng.n_actor, sched, 1 - beta1, beta2, 1 - beta2, eps)
 
         if self._tg_graph is None:
             if not self._tg_warm:  # first call eager: lazy workspace / timing setup outside capture
@@ -296,6 +309,10 @@ class PPOEngine:
                     for scheduler in agent.schedulers.values():
                         scheduler.step()
                 return out
+        staged = eng.fused
+        if staged:  # one 128 B record per stored row: the minibatch gathers read one line a row
+            eng.stage_records(states, buf.actions, buf.logp, buf.advantage, buf.value_target)
+        current = False  # bf16 weight images refreshed by the last optimizer step
         for epoch in range(epochs):
             if self._rng() == "torch":
                 perm = torch.randperm((n_glob if exact else n) * t_len).to(dev, non_blocking=True)
@@ -312,11 +329,18 @@ class PPOEngine:
                 else:
                     E.feistel_rows(self._seed() + 7919 * self.dp.rank,
                                    self.iteration * epochs + epoch, i * b, b, n, t_len, self._rows)
-                eng.minibatch_grad(states, buf.actions, buf.logp, buf.advantage, buf.value_target,
-                                   self._rows, b, agent.flat_grad, self._loss_buf[epoch, i],
-                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba, count=count)
+                if staged:
+                    eng.minibatch_grad_staged(self._rows, b, agent.flat_grad,
+                                              self._loss_buf[epoch, i], clip_lo, clip_hi,
+                                              ppo.entropy_eps, inv_b, inv_ba, count=count,
+                                              weights_current=current)
+                else:
+                    eng.minibatch_grad(states, buf.actions, buf.logp, buf.advantage,
+                                       buf.value_target, self._rows, b, agent.flat_grad,
+                                       self._loss_buf[epoch, i], clip_lo, clip_hi,
+                                       ppo.entropy_eps, inv_b, inv_ba, count=count)
                 self.dp.allreduce_grad(agent.flat_grad)
-                agent.step_both()
+                current = agent.step_both(pack=staged)
         if run.dynamic_config.current_episode < 2500:
             for scheduler in agent.schedulers.values():
                 scheduler.step()

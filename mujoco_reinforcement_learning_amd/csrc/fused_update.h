@@ -38,6 +38,11 @@ struct FusedArgs {
   const float *states, *actions, *old_logp, *adv, *vtarget;
   const int32_t *rows;
   const int32_t *rows_n;       // device row count (exact data parallel), nullable -> b
+  // staged records (fused_records_launch): when set, the prep gather copies one 128 B record
+  // per row instead of reading the five storage arrays
+  const uint4 *rec;
+  int64_t n_rec;
+  bool pack_w;                 // prep also refreshes the bf16 weight images from the masters
   int b, din, act_dim, act, hidden;
   float omv, clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
   float *slabs;                // (G, slab_stride) partial gradients in the flat layout
@@ -47,8 +52,33 @@ struct FusedArgs {
   uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
 };
 
-// Gather the minibatch (bf16 states + row scalars) and refresh the bf16 weight images.
+// Gather the minibatch (bf16 states + row scalars) and, with q.pack_w, refresh the bf16 weight
+// images.
 int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
+
+// One 128 B record per stored row: bf16 state[32] (columns >= din zero) | f32 actions[A],
+// old_logp, adv, vtarget, zeros -- the per-row image the prep gather copies.
+constexpr int kRecordBytes = 2 * kFusedKX + 4 * kFusedSP;
+static_assert(kRecordBytes == 128, "one record per 128 B line");
+int fused_records_launch(uint4 *rec, const float *states, const float *actions,
+                         const float *old_logp, const float *adv, const float *vtarget,
+                         int64_t n_rows, int din, int act_dim, const TimRec &trec, hipStream_t st);
+
+// Adam over the flat parameters of both nets (adam_elem) that also writes the updated values
+// into the fused kernels' bf16 weight images, so the next minibatch needs no weight refresh.
+struct AdamPackArgs {
+  float *p;
+  const float *g;
+  float *m, *v;
+  int64_t n, n_actor;
+  const float *sched;          // device (neg_step_actor, neg_step_critic, bc2_sqrt), or null
+  float neg_a, neg_c, bc2;     // host scalars when sched is null
+  float w1, b2, omb2, eps;
+  __bf16 *w0b[2], *w1b[2], *w1bt[2];
+  int64_t off_w0[2], off_w1[2];
+  int din, H;
+};
+int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st);
 // The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.
 int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).

@@ -29,6 +29,7 @@
 // image holds bf16(a1)); ReLU needs only its sign, which the bf16 image keeps.
 #include <cstdio>
 
+#include "adam_elem.h"
 #include "fused_common.h"
 
 namespace ppo {
@@ -41,6 +42,21 @@ using namespace fu;
 // ============================================================================================
 __global__ __launch_bounds__(256) void fused_prep_kernel(FusedArgs q, int row_blocks) {
   const int tid = threadIdx.x;
+  if (static_cast<int>(blockIdx.x) < row_blocks && q.rec) {
+    // staged records: 8 lanes copy one 128 B record (4 x 16 B state image, 4 x 16 B scalars)
+    const int j = static_cast<int>((static_cast<int64_t>(blockIdx.x) * 256 + tid) >> 3);
+    const int u = tid & 7;
+    if (j >= q.b) return;
+    const int count = q.rows_n ? *q.rows_n : q.b;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (j < count) {
+      const int64_t sr = q.rows[j];
+      if (sr >= 0 && sr < q.n_rec) v = q.rec[sr * (kRecordBytes / 16) + u];
+    }
+    if (u < 4) reinterpret_cast<uint4 *>(q.xb + static_cast<int64_t>(j) * kFusedKX)[u] = v;
+    else reinterpret_cast<uint4 *>(q.srow + static_cast<int64_t>(j) * kFusedSP)[u - 4] = v;
+    return;
+  }
   if (static_cast<int>(blockIdx.x) < row_blocks) {
     const int j = blockIdx.x * 256 + tid;
     if (j >= q.b) return;
@@ -96,6 +112,106 @@ __global__ __launch_bounds__(256) void fused_prep_kernel(FusedArgs q, int row_bl
     const __bf16 v = __builtin_bit_cast(__bf16, static_cast<uint16_t>(pack2(N.w1[t], 0.f) & 0xffffu));
     w1b[t] = v;
     w1bt[static_cast<int64_t>(c) * H + o] = v;
+  }
+}
+
+// Records: thread = one stored row, written as 8 x 16 B (the prep row gather's exact values).
+__global__ __launch_bounds__(256) void fused_records_kernel(uint4 *__restrict__ rec,
+                                                            const float *__restrict__ states,
+                                                            const float *__restrict__ actions,
+                                                            const float *__restrict__ old_logp,
+                                                            const float *__restrict__ adv,
+                                                            const float *__restrict__ vtarget,
+                                                            int64_t n_rows, int din, int A) {
+  const int64_t sr = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (sr >= n_rows) return;
+  float x[kFusedKX];
+  float s[kFusedSP];
+  const float *src = states + sr * din;
+#pragma unroll
+  for (int k = 0; k < kFusedKX; ++k) x[k] = k < din ? src[k] : 0.f;
+  const float old_lp = old_logp[sr], ad = adv[sr], vt = vtarget[sr];
+#pragma unroll
+  for (int k = 0; k < kFusedSP; ++k)
+    s[k] = k < A ? actions[sr * A + k]
+                 : (k == A ? old_lp : (k == A + 1 ? ad : (k == A + 2 ? vt : 0.f)));
+  uint4 *d = rec + sr * (kRecordBytes / 16);
+#pragma unroll
+  for (int u = 0; u < kFusedKX / 8; ++u)
+    d[u] = make_uint4(pack2(x[8 * u], x[8 * u + 1]), pack2(x[8 * u + 2], x[8 * u + 3]),
+                      pack2(x[8 * u + 4], x[8 * u + 5]), pack2(x[8 * u + 6], x[8 * u + 7]));
+#pragma unroll
+  for (int u = 0; u < kFusedSP / 4; ++u)
+    d[kFusedKX / 8 + u] = make_uint4(__float_as_uint(s[4 * u]), __float_as_uint(s[4 * u + 1]),
+                                     __float_as_uint(s[4 * u + 2]), __float_as_uint(s[4 * u + 3]));
+}
+
+// ============================================================================================
+// Adam + weight images.  Blocks [0, gen_blocks): elementwise over the flat vector, skipping the
+// two W1 blocks (W0 elements also land in the W0 image).  Blocks [gen_blocks, ...): one 32x32
+// tile of one net's W1 each -- Adam on the tile, the row-major bf16 image written directly and
+// the transposed image through an LDS transpose, so both image writes are coalesced.
+// ============================================================================================
+constexpr int kPackTile = 32;
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(pack2(x, 0.f) & 0xffffu); }
+
+__global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a, int gen_blocks) {
+  const float ns_a = a.sched ? a.sched[0] : a.neg_a;
+  const float ns_c = a.sched ? a.sched[1] : a.neg_c;
+  const float bc2 = a.sched ? a.sched[2] : a.bc2;
+  const int tid = threadIdx.x;
+  const int H = a.H;
+  if (static_cast<int>(blockIdx.x) < gen_blocks) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid;
+    if (i >= a.n) return;
+#pragma unroll
+    for (int z = 0; z < 2; ++z)
+      if (i >= a.off_w1[z] && i < a.off_w1[z] + static_cast<int64_t>(H) * H) return;
+    float m = a.m[i], v = a.v[i];
+    const float p = adam_elem(a.p[i], a.g[i], m, v, i < a.n_actor ? ns_a : ns_c, a.w1, a.b2,
+                              a.omb2, bc2, a.eps);
+    a.p[i] = p;
+    a.m[i] = m;
+    a.v[i] = v;
+#pragma unroll
+    for (int z = 0; z < 2; ++z) {
+      const int64_t e = i - a.off_w0[z];
+      if (e >= 0 && e < static_cast<int64_t>(H) * a.din) {
+        const int f = static_cast<int>(e / a.din), k = static_cast<int>(e % a.din);
+        reinterpret_cast<uint16_t *>(a.w0b[z])[f * kFusedKX + k] = bf16_bits(p);
+      }
+    }
+    return;
+  }
+  __shared__ uint16_t tile[kPackTile][kPackTile + 2];
+  const int tiles = H / kPackTile;
+  const int tb = static_cast<int>(blockIdx.x) - gen_blocks;
+  const int z = tb / (tiles * tiles);
+  const int to = (tb % (tiles * tiles)) / tiles, tc = tb % tiles;
+  const int64_t base = a.off_w1[z];
+  const float ns = base < a.n_actor ? ns_a : ns_c;
+  uint16_t *w1b = reinterpret_cast<uint16_t *>(a.w1b[z]);
+  uint16_t *w1bt = reinterpret_cast<uint16_t *>(a.w1bt[z]);
+#pragma unroll 4
+  for (int k = 0; k < kPackTile * kPackTile / 256; ++k) {
+    const int idx = k * 256 + tid, lo = idx / kPackTile, lc = idx % kPackTile;
+    const int64_t t = static_cast<int64_t>(to * kPackTile + lo) * H + tc * kPackTile + lc;
+    const int64_t i = base + t;
+    float m = a.m[i], v = a.v[i];
+    const float p = adam_elem(a.p[i], a.g[i], m, v, ns, a.w1, a.b2, a.omb2, bc2, a.eps);
+    a.p[i] = p;
+    a.m[i] = m;
+    a.v[i] = v;
+    const uint16_t hb = bf16_bits(p);
+    w1b[t] = hb;
+    tile[lo][lc] = hb;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int k = 0; k < kPackTile * kPackTile / 256; ++k) {
+    const int idx = k * 256 + tid, lc = idx / kPackTile, lo = idx % kPackTile;
+    w1bt[static_cast<int64_t>(tc * kPackTile + lc) * H + to * kPackTile + lo] = tile[lo][lc];
   }
 }
 
@@ -675,10 +791,35 @@ __global__ __launch_bounds__(NT, 1) void fused_update_kernel(FusedArgs q, uint64
 bool fused_width_ok(int hidden) { return hidden == 256; }
 
 int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
-  const int row_blocks = ceil_div(q.b, 256);
+  const int row_blocks = q.rec ? static_cast<int>(ceil_div(static_cast<int64_t>(q.b) * 8, 256))
+                               : ceil_div(q.b, 256);
   const int64_t per_net = static_cast<int64_t>(q.hidden) * (kFusedKX + q.hidden);
-  const int w_blocks = ceil_div(2 * per_net, 256);
+  const int w_blocks = q.pack_w ? static_cast<int>(ceil_div(2 * per_net, 256)) : 0;
+  if (row_blocks + w_blocks == 0) return 0;
   launch_k(rec, fused_prep_kernel, dim3(row_blocks + w_blocks), dim3(256), 0, st, q, row_blocks);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+int fused_records_launch(uint4 *rec, const float *states, const float *actions,
+                         const float *old_logp, const float *adv, const float *vtarget,
+                         int64_t n_rows, int din, int act_dim, const TimRec &trec, hipStream_t st) {
+  PPO_REQUIRE(din >= 1 && din <= kFusedKX && act_dim >= 1 && act_dim + 3 <= kFusedSP,
+              "fused records: din %d / act_dim %d out of range", din, act_dim);
+  if (n_rows <= 0) return 0;
+  launch_k(trec, fused_records_kernel, dim3(ceil_div(n_rows, 256)), dim3(256), 0, st, rec, states,
+           actions, old_logp, adv, vtarget, n_rows, din, act_dim);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st) {
+  PPO_REQUIRE(a.H % kPackTile == 0 && a.din >= 1 && a.din <= kFusedKX && a.n > 0,
+              "adam_pack: H=%d din=%d", a.H, a.din);
+  const int gen_blocks = static_cast<int>(ceil_div(a.n, 256));
+  const int tiles = a.H / kPackTile;
+  launch_k(rec, adam_pack_kernel, dim3(gen_blocks + 2 * tiles * tiles), dim3(256), 0, st, a,
+           gen_blocks);
   PPO_LAUNCHED();
   return 0;
 }

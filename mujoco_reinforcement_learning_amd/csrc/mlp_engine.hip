@@ -1265,6 +1265,8 @@ struct ppo_ctx {
   float *fslabs;                // (kFusedMaxWG, total_params) partial gradients
   float *floss;                 // (kFusedMaxWG, 2) loss-term partials
   void *farena;
+  uint4 *frec;                  // (frec_cap, 128 B) staged records (ppo_stage_records)
+  int64_t frec_cap, frec_rows;
   uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
   int fstamp_on, fstamp_g;
   ppo::Timing tim;
@@ -1497,7 +1499,8 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
                                 const float *vtarget_d, const int32_t *rows_d, int b,
                                 const int32_t *count_d, float clip_lo, float clip_hi,
                                 float entropy_coef, float inv_b, float inv_ba, float *grad_d,
-                                float *loss_d, hipStream_t st) {
+                                float *loss_d, hipStream_t st, bool staged = false,
+                                bool pack_w = true) {
   const int H = ctx->fused_hidden;
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
@@ -1515,6 +1518,9 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   q.vtarget = vtarget_d;
   q.rows = rows_d;
   q.rows_n = count_d;
+  q.rec = staged ? ctx->frec : nullptr;
+  q.n_rec = staged ? ctx->frec_rows : 0;
+  q.pack_w = pack_w;
   q.b = b;
   q.din = din;
   q.act_dim = A;
@@ -1533,12 +1539,14 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   q.G = std::min(kFusedMaxWG, nchunks);
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
   ctx->fstamp_g = q.G;
-  // algorithmic traffic: gather (row index, din + A + 3 floats in; 64 + 64 B out per row) and
-  // weight images (f32 in, 3 bf16 images out per net)
-  const double wbytes = 2.0 * (4.0 * H * (din + H) + 2.0 * H * (kFusedKX + 2.0 * H));
+  // algorithmic traffic: gather (row index, din + A + 3 floats -- or one 128 B record -- in;
+  // 64 + 64 B out per row) and weight images (f32 in, 3 bf16 images out per net)
+  const double wbytes =
+      pack_w ? 2.0 * (4.0 * H * (din + H) + 2.0 * H * (kFusedKX + 2.0 * H)) : 0.0;
+  const double in_row = staged ? 4.0 + kRecordBytes : 4.0 * (1 + din + A + 3);
   {
     const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
-                     static_cast<double>(b) * (4.0 * (1 + din + A + 3) + 2.0 * kFusedKX + 4.0 * kFusedSP) + wbytes};
+                     static_cast<double>(b) * (in_row + 2.0 * kFusedKX + 4.0 * kFusedSP) + wbytes};
     if (int rc = fused_prep_launch(q, rec, st)) return rc;
   }
   {
@@ -1770,6 +1778,7 @@ extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
   if (ctx->arena) (void)hipFree(ctx->arena);
   if (ctx->farena) (void)hipFree(ctx->farena);
   if (ctx->fstamps) (void)hipFree(ctx->fstamps);
+  if (ctx->frec) (void)hipFree(ctx->frec);
   delete ctx;
   return 0;
 }
@@ -1868,12 +1877,111 @@ extern "C" int ppo_pack_weights(ppo_ctx *ctx, void *stream) {
   FusedArgs q{};
   fused_nets(ctx, q.net);
   q.b = 0;
+  q.pack_w = true;
   q.din = ctx->cfg.obs_dim * ctx->cfg.window;
   q.hidden = ctx->fused_hidden;
   const double H = ctx->fused_hidden;
   const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
                    2.0 * (4.0 * H * (q.din + H) + 2.0 * H * (kFusedKX + 2.0 * H))};
   return fused_prep_launch(q, rec, as_stream(stream));
+}
+
+extern "C" int ppo_ctx_fused_active(const ppo_ctx *ctx) {
+  return (ctx && fused_active(ctx)) ? 1 : 0;
+}
+
+extern "C" int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                                 const float *old_logp_d, const float *adv_d,
+                                 const float *vtarget_d, int64_t n_rows, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx), "ppo_stage_records: needs the fused bf16 path "
+                                 "(ppo_ctx_fused_active)");
+  PPO_REQUIRE(states_d && actions_d && old_logp_d && adv_d && vtarget_d && n_rows > 0,
+              "ppo_stage_records: null buffer or n_rows <= 0");
+  hipStream_t st = as_stream(stream);
+  if (n_rows > ctx->frec_cap) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    PPO_REQUIRE(hipStreamIsCapturing(st, &cap) == hipSuccess &&
+                    cap == hipStreamCaptureStatusNone,
+                "ppo_stage_records: first call for %lld rows inside a graph capture",
+                static_cast<long long>(n_rows));
+    (void)hipStreamSynchronize(st);
+    if (ctx->frec) (void)hipFree(ctx->frec);
+    ctx->frec = nullptr;
+    ctx->frec_cap = 0;
+    void *p = nullptr;
+    const hipError_t e = hipMalloc(&p, static_cast<size_t>(n_rows) * kRecordBytes);
+    PPO_REQUIRE(e == hipSuccess, "ppo_stage_records: hipMalloc(%lld records): %s",
+                static_cast<long long>(n_rows), hipGetErrorString(e));
+    ctx->frec = static_cast<uint4 *>(p);
+    ctx->frec_cap = n_rows;
+  }
+  ctx->frec_rows = n_rows;
+  TimingScope timing_scope(ctx);
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window, A = ctx->cfg.act_dim;
+  const TimRec rec{KC_GATHER, "fused_records_kernel", 0.0,
+                   static_cast<double>(n_rows) * (4.0 * (din + A + 3) + kRecordBytes)};
+  return fused_records_launch(ctx->frec, states_d, actions_d, old_logp_d, adv_d, vtarget_d,
+                              n_rows, din, A, rec, st);
+}
+
+extern "C" int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b,
+                                         const int32_t *count_d, float clip_lo, float clip_hi,
+                                         float entropy_coef, float inv_b, float inv_ba,
+                                         float *grad_d, float *loss_d, int flags, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx) && ctx->frec && ctx->frec_rows > 0,
+              "ppo_minibatch_grad_staged: no staged records (ppo_stage_records first)");
+  PPO_REQUIRE(rows_d && grad_d && loss_d, "ppo_minibatch_grad_staged: null buffer");
+  PPO_REQUIRE(b > 0 && b <= ctx->cfg.max_rows,
+              "ppo_minibatch_grad_staged: b=%d outside [1, max_rows=%d]", b, ctx->cfg.max_rows);
+  PPO_REQUIRE((flags & ~PPO_STAGED_WEIGHTS_CURRENT) == 0, "ppo_minibatch_grad_staged: flags %d",
+              flags);
+  TimingScope timing_scope(ctx);
+  return fused_minibatch_grad(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b,
+                              count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
+                              loss_d, as_stream(stream), true,
+                              (flags & PPO_STAGED_WEIGHTS_CURRENT) == 0);
+}
+
+extern "C" int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
+                             const float *sched_d, float neg_step_actor, float neg_step_critic,
+                             float bc2_sqrt, float one_minus_beta1, float beta2,
+                             float one_minus_beta2, float eps, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx), "ppo_adam_pack: needs the fused bf16 path");
+  PPO_REQUIRE(g_d && m_d && v_d, "ppo_adam_pack: null buffer");
+  TimingScope timing_scope(ctx);
+  AdamPackArgs a{};
+  a.p = ctx->params;
+  a.g = g_d;
+  a.m = m_d;
+  a.v = v_d;
+  a.n = ctx->total_params;
+  a.n_actor = ctx->net[0].count;
+  a.sched = sched_d;
+  a.neg_a = neg_step_actor;
+  a.neg_c = neg_step_critic;
+  a.bc2 = bc2_sqrt;
+  a.w1 = one_minus_beta1;
+  a.b2 = beta2;
+  a.omb2 = one_minus_beta2;
+  a.eps = eps;
+  FusedNet nets[2];
+  fused_nets(ctx, nets);
+  for (int z = 0; z < 2; ++z) {
+    a.w0b[z] = const_cast<__bf16 *>(nets[z].w0b);
+    a.w1b[z] = const_cast<__bf16 *>(nets[z].w1b);
+    a.w1bt[z] = const_cast<__bf16 *>(nets[z].w1bt);
+    a.off_w0[z] = nets[z].off_w0;
+    a.off_w1[z] = nets[z].off_w1;
+  }
+  a.din = ctx->cfg.obs_dim * ctx->cfg.window;
+  a.H = ctx->fused_hidden;
+  const double Hd = a.H;
+  const TimRec rec{KC_ADAM, "adam_pack_kernel", 0.0,
+                   28.0 * a.n + 2.0 * 2.0 * Hd * (a.din + 2.0 * Hd)};
+  return adam_pack_launch(a, rec, as_stream(stream));
 }
 
 extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d,

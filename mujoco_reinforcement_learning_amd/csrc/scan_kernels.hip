@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "adam_elem.h"
 #include "common.h"
 #include "timing.h"
 
@@ -411,14 +412,9 @@ __global__ void adam_kernel(float *__restrict__ p, const float *__restrict__ g,
                             float b2, float omb2, float bc2_sqrt, float eps) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float gi = g[i];
-  float mi = m[i];
-  mi = (w1 < 0.5f) ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.f, gi - mi, gi);
-  // torch's vectorised addcmul (self + value*t1*t2) is built with FP contraction: one FMA
-  const float vi = fmaf(omb2 * gi, gi, v[i] * b2);
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  const float ns = (i < n_actor) ? neg_step_a : neg_step_c;
-  p[i] = p[i] + (ns * mi) / denom;
+  float mi = m[i], vi = v[i];
+  p[i] = adam_elem(p[i], g[i], mi, vi, (i < n_actor) ? neg_step_a : neg_step_c, w1, b2, omb2,
+                   bc2_sqrt, eps);
   m[i] = mi;
   v[i] = vi;
 }
@@ -432,14 +428,9 @@ __global__ void adam_sched_kernel(float *__restrict__ p, const float *__restrict
                                   float b2, float omb2, float eps) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float neg_step_a = sched[0], neg_step_c = sched[1], bc2_sqrt = sched[2];
-  const float gi = g[i];
-  float mi = m[i];
-  mi = (w1 < 0.5f) ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.f, gi - mi, gi);
-  const float vi = fmaf(omb2 * gi, gi, v[i] * b2);
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  const float ns = (i < n_actor) ? neg_step_a : neg_step_c;
-  p[i] = p[i] + (ns * mi) / denom;
+  float mi = m[i], vi = v[i];
+  p[i] = adam_elem(p[i], g[i], mi, vi, (i < n_actor) ? sched[0] : sched[1], w1, b2, omb2,
+                   sched[2], eps);
   m[i] = mi;
   v[i] = vi;
 }

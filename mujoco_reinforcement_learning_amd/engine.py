@@ -242,6 +242,58 @@ class Engine:
             ptr(rows), int(b), ptr(count), clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
             ptr(grad), ptr(loss), _stream(self.device)))
 
+    # ---- staged minibatch path (fused bf16 engine) ---------------------------------------
+    @property
+    def fused(self) -> bool:
+        """True when the fused bf16 kernels run (precision bf16, two equal hidden layers of a
+        compiled width, W*O <= 32, A <= 8): the staged path below is available."""
+        return bool(self.lib.ppo_ctx_fused_active(self._ctx))
+
+    def stage_records(self, states, actions, old_logp, adv, vtarget) -> None:
+        """Pack the time-major storage arrays (rows = T*N) into the ctx's 128 B per-row records
+        that minibatch_grad_staged gathers (once per iteration, after GAE)."""
+        n_rows = old_logp.numel()
+        for name, t in (("states", states), ("actions", actions), ("old_logp", old_logp),
+                        ("adv", adv), ("vtarget", vtarget)):
+            _need(t, name, torch.float32, None, self.device)
+            width = t.shape[-1] if name in ("states", "actions") else 1
+            if t.numel() < n_rows * width:  # states may carry the extra slot T
+                raise RuntimeError(f"{name}: {t.numel()} elements for {n_rows} rows x {width}")
+        check(self.lib.ppo_stage_records(self._ctx, ptr(states), ptr(actions), ptr(old_logp),
+                                         ptr(adv), ptr(vtarget), int(n_rows),
+                                         _stream(self.device)))
+
+    def minibatch_grad_staged(self, rows, b: int, grad, loss, clip_lo: float, clip_hi: float,
+                              entropy_coef: float, inv_b: float, inv_ba: float,
+                              count: Optional[torch.Tensor] = None,
+                              weights_current: bool = False) -> None:
+        """minibatch_grad on the staged records; weights_current=True skips the bf16 weight
+        refresh (valid right after adam_pack)."""
+        _need(rows, "rows", torch.int32, device=self.device)
+        _need(grad, "grad", torch.float32, (self.n_params,), self.device)
+        _need(loss, "loss", torch.float32, device=self.device)
+        if loss.numel() != 2:
+            raise RuntimeError("loss must hold 2 floats")
+        check(self.lib.ppo_minibatch_grad_staged(
+            self._ctx, ptr(rows), int(b), ptr(count), clip_lo, clip_hi, entropy_coef, inv_b,
+            inv_ba, ptr(grad), ptr(loss), 1 if weights_current else 0, _stream(self.device)))
+
+    def adam_pack(self, g, m, v, sched: Optional[torch.Tensor] = None, neg_step_actor: float = 0.0,
+                  neg_step_critic: float = 0.0, bc2_sqrt: float = 1.0,
+                  one_minus_beta1: float = 0.1, beta2: float = 0.999,
+                  one_minus_beta2: float = 0.001, eps: float = 1e-8) -> None:
+        """ppo_adam on the bound parameters (ppo_adam_sched when sched is given) that also
+        refreshes the fused kernels' bf16 weight images."""
+        for name, t in (("g", g), ("m", m), ("v", v)):
+            _need(t, name, torch.float32, (self.n_params,), self.device)
+        if sched is not None:
+            _need(sched, "sched", torch.float32, None, self.device)
+            if sched.numel() < 3:
+                raise RuntimeError("sched must hold 3 floats")
+        check(self.lib.ppo_adam_pack(self._ctx, ptr(g), ptr(m), ptr(v), ptr(sched),
+                                     neg_step_actor, neg_step_critic, bc2_sqrt, one_minus_beta1,
+                                     beta2, one_minus_beta2, eps, _stream(self.device)))
+
 
 # ==============================================================================================
 # Context-free kernels

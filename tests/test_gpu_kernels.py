@@ -518,3 +518,65 @@ def test_fused_kernels_bitwise_deterministic(gpu):
         grads.append(torch.cat([grad, loss]))
     for gr in grads[1:]:
         assert torch.equal(gr, grads[0]), int((gr != grads[0]).sum())
+
+
+@pytest.mark.parametrize("with_count", [False, True])
+def test_staged_records_and_adam_pack_match_unstaged(gpu, with_count):
+    """ppo_stage_records + ppo_minibatch_grad_staged give the gradient and losses of
+    ppo_minibatch_grad bit for bit (also with a device row count, the exact-DP shard form); and
+    ppo_adam_pack updates p/m/v exactly like ppo_adam while leaving weight images that equal a
+    fresh ppo_pack_weights (the next staged gradient with weights_current=True is identical to
+    one that refreshes the images)."""
+    from mujoco_reinforcement_learning_amd import engine as E
+    n, t, b = 512, 16, 2048
+    run, eng, ref, cfg = _agents(gpu, 12, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    assert e.fused
+    g = torch.Generator().manual_seed(4)
+    rows_total = n * t
+    states = torch.randn(t + 1, n, 17, generator=g).to(gpu)  # buffer layout with slot T
+    actions = torch.randn(t, n, 6, generator=g).to(gpu)
+    old_lp = torch.randn(t, n, generator=g).to(gpu) - 5
+    adv = torch.randn(t, n, generator=g).to(gpu)
+    vt = torch.randn(t, n, generator=g).to(gpu)
+    rows = torch.randperm(rows_total, generator=g)[:b].to(torch.int32).to(gpu)
+    count = torch.tensor([b - 300], dtype=torch.int32, device=gpu) if with_count else None
+    args = (0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    e.pack_weights()
+    g0, l0 = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+    e.minibatch_grad(states, actions, old_lp, adv, vt, rows, b, g0, l0, *args, count=count)
+    e.stage_records(states, actions, old_lp, adv, vt)
+    g1, l1 = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+    e.minibatch_grad_staged(rows, b, g1, l1, *args, count=count)
+    torch.cuda.synchronize()
+    assert torch.equal(g0, g1), int((g0 != g1).sum())
+    assert torch.equal(l0, l1)
+    # Adam: pack variant vs plain kernel on copies of the same state
+    p0 = eng.flat_params.clone()
+    m = torch.rand(e.n_params, generator=g).to(gpu) * 1e-3
+    v = torch.rand(e.n_params, generator=g).to(gpu) * 1e-6
+    m2, v2 = m.clone(), v.clone()
+    sc = (-1e-3, -2e-3, 0.3, 0.1, 0.999, 0.001, 1e-8)
+    E.adam(p0, g1, m, v, e.n_actor, sc[0], sc[1], sc[3], sc[4], sc[5], sc[2], sc[6])
+    e.adam_pack(g1, m2, v2, None, *sc)
+    torch.cuda.synchronize()
+    assert torch.equal(p0, eng.flat_params)
+    assert torch.equal(m, m2) and torch.equal(v, v2)
+    # device-schedule variant on the next step
+    sched = torch.tensor([sc[0], sc[1], sc[2]], device=gpu)
+    p1 = eng.flat_params.clone()
+    E.adam(p1, g1, m, v, e.n_actor, sc[0], sc[1], sc[3], sc[4], sc[5], sc[2], sc[6])
+    e.adam_pack(g1, m2, v2, sched, one_minus_beta1=sc[3], beta2=sc[4], one_minus_beta2=sc[5],
+                eps=sc[6])
+    torch.cuda.synchronize()
+    assert torch.equal(p1, eng.flat_params)
+    # images left by adam_pack == a fresh refresh
+    g2, l2 = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+    e.minibatch_grad_staged(rows, b, g2, l2, *args, count=count, weights_current=True)
+    g3, l3 = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+    e.minibatch_grad_staged(rows, b, g3, l3, *args, count=count, weights_current=False)
+    torch.cuda.synchronize()
+    assert torch.equal(g2, g3), int((g2 != g3).sum())
+    assert torch.equal(l2, l3)
+    assert not torch.equal(g2, g1)  # the parameters did move
