@@ -10,8 +10,8 @@
 // (actor: act_dim padded to 2/4/6/8 with zero head rows; critic: 1).
 //
 // Window length 1 (every MLP config): the pushed window is the new observation itself, so both
-// nets' workgroups standardise the same values independently and only the actor's writes the
-// window and the state.  The standardisation is the A1 kernels' f64 loop (same order, bit-
+// nets' workgroups standardise the same values independently and only the actor's (the critic's
+// on a value-only call) write the window and the state.  The standardisation is the A1 kernels' f64 loop (same order, bit-
 // identical states).
 #include <type_traits>
 
@@ -65,6 +65,8 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   if (tid < 8) hs[tid] = (tid < (ACTOR ? A : 1) && N.bh) ? N.bh[tid] : 0.f;
   if (ACTOR && tid >= 8 && tid < 16) hs[tid] = (tid - 8 < A) ? q.logstd[tid - 8] : 0.f;
 
+  // the window / state writer: the actor's workgroups, or the critic's on a value-only call
+  const bool writer = ACTOR || !q.do_actor;
   // ---- observe (A1): thread per env row, the A1 kernels' f64 loops ----
   if (tid < R) {
     const int env = row0 + tid;
@@ -106,7 +108,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
             if (f >= lo && f < hi) dst[f] = static_cast<float>((x[f] - mean) / sd);
         }
       }
-      if (ACTOR && q.obs_d) {
+      if (writer && q.obs_d) {
         double *wrow = q.window_d + static_cast<int64_t>(env) * O;
 #pragma unroll
         for (int f = 0; f < kFusedKX; ++f)
@@ -118,8 +120,8 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
-  // states -> rollout buffer (actor workgroups; coalesced) and the bf16 X image
-  if (ACTOR) {
+  // states -> rollout buffer (writer workgroups; coalesced) and the bf16 X image
+  if (writer) {
     for (int idx = tid; idx < R * O; idx += NT) {
       const int lrow = idx / O, e = idx - lrow * O, env = row0 + lrow;
       if (env < q.n) q.state_d[static_cast<int64_t>(env) * O + e] = xs[lrow * kPolicyXsPitch + e];

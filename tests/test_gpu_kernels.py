@@ -468,12 +468,15 @@ def test_observe_act_fused_matches_layered(gpu, act, n, window, obs, na, reset_p
         scale = float(b.abs().max()) + 1e-6
         err = float((a - b).abs().max())
         assert err <= 2e-4 * scale, (name, err, scale)
-    # value-only call (t = T) and action-only call
+    # value-only call (t = T; only the critic's workgroups run, and they write window + state)
+    # and action-only call
     win = win0.clone().to(gpu)
-    st = torch.empty(n, window * obs, device=gpu)
+    st = torch.full((n, window * obs), float("nan"), device=gpu)
     val = torch.full((n,), float("nan"), device=gpu)
     e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), value=val)
     assert torch.allclose(val.cpu(), l[4], rtol=0, atol=2e-4 * (float(l[4].abs().max()) + 1e-6))
+    assert torch.equal(win.cpu(), l[0]), "value-only call: window push differs"
+    assert torch.equal(st.cpu(), l[1]), "value-only call: state differs"
     win = win0.clone().to(gpu)
     act_ = torch.full((n, na), float("nan"), device=gpu)
     e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), eps=eps.to(gpu), action=act_)
