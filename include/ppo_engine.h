@@ -182,6 +182,7 @@ int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions
  *   flags PPO_STAGED_WEIGHTS_CURRENT: the bf16 weight images are already current (the previous
  *   optimizer step was ppo_adam_pack), so the weight refresh is skipped. */
 #define PPO_STAGED_WEIGHTS_CURRENT 1
+#define PPO_STAGED_ROWS_GATHERED 2
 int ppo_ctx_fused_active(const ppo_ctx *ctx);
 int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                       const float *old_logp_d, const float *adv_d, const float *vtarget_d,
@@ -190,6 +191,21 @@ int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b, const 
                               float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                               float inv_ba, float *grad_d, float *loss_d, int flags,
                               void *stream);
+
+/* One whole optimizer step of the staged single-rank path (ppo.py:109-135 for one minibatch,
+ * then both optimizers' step()), in at most three launches: [row gather / weight refresh],
+ * the fused forward/backward, and a tail that folds the slabs into grad_d, applies Adam (as
+ * ppo_adam_pack; sched_d or the host scalars) with the weight-image refresh, and gathers the
+ * NEXT minibatch's rows next_rows_d[0, next_b) (NULL / 0: none).  flags:
+ * PPO_STAGED_WEIGHTS_CURRENT (the images are current) | PPO_STAGED_ROWS_GATHERED (the previous
+ * step gathered rows_d already).  Results equal ppo_minibatch_grad_staged + ppo_adam_pack. */
+int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b, const int32_t *next_rows_d,
+                           int next_b, float clip_lo, float clip_hi, float entropy_coef,
+                           float inv_b, float inv_ba, float *grad_d, float *loss_d, float *m_d,
+                           float *v_d, const float *sched_d, float neg_step_actor,
+                           float neg_step_critic, float bc2_sqrt, float one_minus_beta1,
+                           float beta2, float one_minus_beta2, float eps, int flags,
+                           void *stream);
 
 /* ---- A15: fused Adam over the flat buffer (torch.optim.Adam single-tensor path) ----------------
  * replaces optimizers['critic'].step() / optimizers['actor'].step() (ppo.py:122,135) and

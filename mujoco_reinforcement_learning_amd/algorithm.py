@@ -200,17 +200,18 @@ class PPOEngine:
             E.normalize_rows(buf.value_target, run.ppo_config.advantage_scaler)
 
     # ---- ppo.py:93-154 ---------------------------------------------------------------------
-    def _train_graph_ok(self) -> bool:
-        return (self._rng() == "philox" and not self.dp.active and
-                bool(getattr(self.run.engine_config, "train_graph", True)))
+    def _scheduled_ok(self) -> bool:
+        return self._rng() == "philox" and not self.dp.active
 
-    def _train_graphed(self, memory: RolloutBuffer, b: int, epochs: int, batches: int, clip_lo,
-                       clip_hi, inv_b, inv_ba):
-        """The E x M optimizer steps as one hipGraph replay (philox, single rank): the minibatch
-        rows of every epoch are drawn first (E Feistel launches), the Adam step sizes of the
-        iteration are uploaded as a device schedule, and the captured loop of M*E x (gather,
-        fused forward/backward, slab reduction, Adam) replays with them.  Same arithmetic as the
-        eager loop below."""
+    def _train_scheduled(self, memory: RolloutBuffer, b: int, epochs: int, batches: int, clip_lo,
+                         clip_hi, inv_b, inv_ba):
+        """The E x M optimizer steps of a single-rank philox iteration with everything known up
+        front: the minibatch rows of every epoch are drawn first (E Feistel launches) and the Adam
+        step sizes come from a device schedule.  Per step: on the fused bf16 path one
+        ppo_update_step_staged (fused forward/backward + a tail that reduces, steps Adam, refreshes
+        the weight images and gathers the next minibatch's rows); otherwise minibatch_grad +
+        adam_sched.  With engine_config.train_graph the loop is captured once as a hipGraph and
+        replayed (same launches, bit-identical results)."""
         agent, eng, buf = self.agent, self.agent.engine, memory
         n, t_len = buf.num_envs, buf.horizon
         dev = agent.device
@@ -237,18 +238,24 @@ class PPOEngine:
         if staged:
             eng.stage_records(buf.states, buf.actions, buf.logp, buf.advantage, buf.value_target)
 
+        def rows_of(k):
+            e, i = divmod(k, batches)
+            return self._tg_rows[e, i * b:(i + 1) * b]
+
         def body():
             for epoch in range(epochs):
                 for i in range(batches):
-                    rows = self._tg_rows[epoch, i * b:(i + 1) * b]
-                    sched = self._tg_sched[epoch * batches + i]
+                    k = epoch * batches + i
+                    rows = rows_of(k)
+                    sched = self._tg_sched[k]
                     if staged:
-                        eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
-                                                  clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
-                                                  weights_current=epoch + i > 0)
-                        eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
-                                      one_minus_beta1=1 - beta1, beta2=beta2,
-                                      one_minus_beta2=1 - beta2, eps=eps)
+                        eng.update_step_staged(
+                            rows, b, agent.flat_grad, self._loss_buf[epoch, i], agent.flat_m,
+                            agent.flat_v, clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
+                            sched=sched, one_minus_beta1=1 - beta1, beta2=beta2,
+                            one_minus_beta2=1 - beta2, eps=eps,
+                            next_rows=rows_of(k + 1) if k + 1 < steps else None,
+                            weights_current=k > 0, rows_gathered=k > 0)
                         continue
                     eng.minibatch_grad(buf.states, buf.actions, buf.logp, buf.advantage,
                                        buf.value_target, rows, b, agent.flat_grad,
@@ -257,6 +264,9 @@ class PPOEngine:
                     E.adam_sched(agent.flat_params, agent.flat_grad, agent.flat_m, agent.flat_v,
                                  eng.n_actor, sched, 1 - beta1, beta2, 1 - beta2, eps)
 
+        if not getattr(self.run.engine_config, "train_graph", True):
+            body()
+            return self._loss_buf
         if self._tg_graph is None:
             if not self._tg_warm:  # first call eager: lazy workspace / timing setup outside capture
                 self._tg_warm = True
@@ -301,9 +311,9 @@ class PPOEngine:
         inv_b = 1.0 / b_global
         inv_ba = 1.0 / (b_global * a)
         states = buf.states
-        if self._train_graph_ok():
-            out = self._train_graphed(memory, b, epochs, batches_per_epoch, clip_lo, clip_hi,
-                                      inv_b, inv_ba)
+        if self._scheduled_ok():
+            out = self._train_scheduled(memory, b, epochs, batches_per_epoch, clip_lo, clip_hi,
+                                        inv_b, inv_ba)
             if out is not None:
                 if run.dynamic_config.current_episode < 2500:
                     for scheduler in agent.schedulers.values():

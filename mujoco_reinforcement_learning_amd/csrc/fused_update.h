@@ -7,6 +7,7 @@
 
 #include <cstdint>
 
+#include "reduce_slabs.h"
 #include "timing.h"
 
 namespace ppo {
@@ -79,6 +80,21 @@ struct AdamPackArgs {
   int din, H;
 };
 int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st);
+
+// The single-rank optimizer-step tail of a staged minibatch, in one launch: blocks
+// [0, ceil(P/256)) fold the slabs (reduce_slab_block) and apply Adam + the weight-image refresh
+// to the parameters they just reduced (a.g is the reduced gradient, also written); the remaining
+// blocks gather the NEXT minibatch's rows from the staged records (b = 0: none).
+struct TailArgs {
+  AdamPackArgs a;
+  const int32_t *rows;
+  const uint4 *rec;
+  int64_t n_rec;
+  __bf16 *xb;
+  float *srow;
+  int b;
+};
+int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st);
 // The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.
 int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).

@@ -216,6 +216,65 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a, int gen_
 }
 
 // ============================================================================================
+// Optimizer-step tail: slab reduction + Adam + weight images, and the next rows' gather
+// ============================================================================================
+__device__ __forceinline__ void tail_gather(const TailArgs &t, int64_t blk, int tid) {
+  const int j = static_cast<int>((blk * 256 + tid) >> 3);
+  const int u = tid & 7;
+  if (j >= t.b) return;
+  const int64_t sr = t.rows[j];
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (sr >= 0 && sr < t.n_rec) v = t.rec[sr * (kRecordBytes / 16) + u];
+  if (u < 4) reinterpret_cast<uint4 *>(t.xb + static_cast<int64_t>(j) * kFusedKX)[u] = v;
+  else reinterpret_cast<uint4 *>(t.srow + static_cast<int64_t>(j) * kFusedSP)[u - 4] = v;
+}
+
+__global__ __launch_bounds__(256) void step_tail_kernel(ReduceArgs r, TailArgs t, int red_blocks) {
+  const int tid = threadIdx.x;
+  if (static_cast<int>(blockIdx.x) >= red_blocks) {
+    tail_gather(t, static_cast<int64_t>(blockIdx.x) - red_blocks, tid);
+    return;
+  }
+  const float4 g4 = reduce_slab_block(r, blockIdx.x);
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * (tid & 63);
+  if ((tid >> 6) != 0 || i >= r.total) return;
+  const AdamPackArgs &a = t.a;
+  const float ns = i < a.n_actor ? (a.sched ? a.sched[0] : a.neg_a) : (a.sched ? a.sched[1] : a.neg_c);
+  const float bc2 = a.sched ? a.sched[2] : a.bc2;
+  float4 p4 = *reinterpret_cast<const float4 *>(a.p + i);
+  float4 m4 = *reinterpret_cast<const float4 *>(a.m + i);
+  float4 v4 = *reinterpret_cast<const float4 *>(a.v + i);
+  p4.x = adam_elem(p4.x, g4.x, m4.x, v4.x, ns, a.w1, a.b2, a.omb2, bc2, a.eps);
+  p4.y = adam_elem(p4.y, g4.y, m4.y, v4.y, ns, a.w1, a.b2, a.omb2, bc2, a.eps);
+  p4.z = adam_elem(p4.z, g4.z, m4.z, v4.z, ns, a.w1, a.b2, a.omb2, bc2, a.eps);
+  p4.w = adam_elem(p4.w, g4.w, m4.w, v4.w, ns, a.w1, a.b2, a.omb2, bc2, a.eps);
+  *reinterpret_cast<float4 *>(a.p + i) = p4;
+  *reinterpret_cast<float4 *>(a.m + i) = m4;
+  *reinterpret_cast<float4 *>(a.v + i) = v4;
+  const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+  const int H = a.H;
+#pragma unroll
+  for (int z = 0; z < 2; ++z) {
+    const int64_t e1 = i - a.off_w1[z];
+    if (e1 >= 0 && e1 < static_cast<int64_t>(H) * H) {  // 4 columns of one W1 row (H % 4 == 0)
+      const int o = static_cast<int>(e1 / H), c = static_cast<int>(e1 % H);
+      *reinterpret_cast<uint2 *>(a.w1b[z] + e1) = make_uint2(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]));
+      uint16_t *wt = reinterpret_cast<uint16_t *>(a.w1bt[z]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wt[static_cast<int64_t>(c + e) * H + o] = bf16_bits(pv[e]);
+    }
+    const int64_t e0 = i - a.off_w0[z];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e0 + e >= 0 && e0 + e < static_cast<int64_t>(H) * a.din) {
+        const int f = static_cast<int>((e0 + e) / a.din), k = static_cast<int>((e0 + e) % a.din);
+        reinterpret_cast<uint16_t *>(a.w0b[z])[f * kFusedKX + k] = bf16_bits(pv[e]);
+      }
+    }
+  }
+}
+
+// ============================================================================================
 // The fused update kernel
 // ============================================================================================
 template <int H>
@@ -820,6 +879,17 @@ int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st) {
   const int tiles = a.H / kPackTile;
   launch_k(rec, adam_pack_kernel, dim3(gen_blocks + 2 * tiles * tiles), dim3(256), 0, st, a,
            gen_blocks);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st) {
+  PPO_REQUIRE(t.a.H % 4 == 0 && t.a.din >= 1 && t.a.din <= kFusedKX && r.total == t.a.n,
+              "step tail: H=%d din=%d", t.a.H, t.a.din);
+  const int red_blocks = static_cast<int>(ceil_div(r.total, 256));
+  const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, 256));
+  launch_k(rec, step_tail_kernel, dim3(red_blocks + gather_blocks), dim3(256), 0, st, r, t,
+           red_blocks);
   PPO_LAUNCHED();
   return 0;
 }

@@ -30,6 +30,7 @@
 #include "common.h"
 #include "fused_policy.h"
 #include "fused_update.h"
+#include "reduce_slabs.h"
 #include "timing.h"
 
 namespace ppo {
@@ -1074,124 +1075,8 @@ __global__ void gather_states_kernel(const float *__restrict__ states, const int
 // ============================================================================================
 // Split-K reduction of the slabs into the flat gradient + loss scalars
 // ============================================================================================
-constexpr int kMaxSegs = 48;
-struct ReduceSeg {
-  int64_t dst, len;
-  const float *src;
-  int64_t stride;
-  int nsplit;
-};
-struct ReduceArgs {
-  ReduceSeg seg[kMaxSegs];
-  int nseg;
-  int64_t total;
-  float *grad;
-  const float *loss_part;
-  int loss_splits;
-  float inv_b;           // actor loss = -(sum min)*inv_b - ent_coef*H ; critic = sum*inv_b
-  const float *logstd;   // H = mean_a(0.5 + 0.5 log 2pi + log(exp(logstd_a))) (Normal.entropy)
-  int act_dim;
-  float ent_coef;
-  float *loss_out;
-};
-
-// Block = 64 float4 groups x 4 split-chunks (one wave per chunk): each thread sums a quarter of
-// the splits for 4 consecutive parameters (tensors start 16-float aligned, so a group never
-// straddles two tensors), then the chunks combine in a fixed order through LDS.  Block 0 also
-// reduces the per-split loss partials with a fixed-shape tree.  Deterministic run to run.
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceArgs q) {
-  __shared__ float4 part[4][64];
-  __shared__ float lred[2][256];
-  const int tid = threadIdx.x, grp = tid & 63, chunk = tid >> 6;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * grp;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < q.total) {
-    int s = 0;
-    while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
-    const ReduceSeg &g = q.seg[s];
-    const int64_t off = i - g.dst;
-    const int k0 = (g.nsplit * chunk) / 4, k1 = (g.nsplit * (chunk + 1)) / 4;
-    // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per
-    // thread; the association is fixed, so the result is still deterministic run to run.
-    if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
-        reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
-      const float *src = g.src + off;
-      float4 acc1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      int k = k0;
-#pragma unroll 4
-      for (; k + 1 < k1; k += 2) {
-        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
-        const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-        acc1.x += u.x;
-        acc1.y += u.y;
-        acc1.z += u.z;
-        acc1.w += u.w;
-      }
-      if (k < k1) {
-        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-      }
-      acc = make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
-    } else if (off >= 0) {  // tail of a tensor / unaligned source (logstd partials, 1-wide
-                            // biases); padding stays zero.  8 strided partial sums per element.
-      float a4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (off + e >= g.len) continue;
-        const float *src = g.src + off + e;
-        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int k = k0;
-        for (; k + 7 < k1; k += 8) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += src[static_cast<int64_t>(k + j) * g.stride];
-        }
-        for (; k < k1; ++k) s[0] += src[static_cast<int64_t>(k) * g.stride];
-        a4[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-      }
-      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
-    }
-  }
-  part[chunk][grp] = acc;
-  __syncthreads();
-  if (chunk == 0 && i < q.total) {
-    const float4 a = part[0][grp], b = part[1][grp], c = part[2][grp], d = part[3][grp];
-    *reinterpret_cast<float4 *>(q.grad + i) =
-        make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
-                    ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
-  }
-  if (blockIdx.x == 0 && q.loss_out) {
-    float la = 0.f, lc = 0.f;
-    for (int k = tid; k < q.loss_splits; k += 256) {
-      la += q.loss_part[2 * k];
-      lc += q.loss_part[2 * k + 1];
-    }
-    lred[0][tid] = la;
-    lred[1][tid] = lc;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (tid < w) {
-        lred[0][tid] += lred[0][tid + w];
-        lred[1][tid] += lred[1][tid + w];
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      float h = 0.f;
-      if (q.logstd) {
-        for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
-        h = h / static_cast<float>(q.act_dim);
-      }
-      q.loss_out[0] = -(lred[0][0] * q.inv_b) - h * q.ent_coef;
-      q.loss_out[1] = lred[1][0] * q.inv_b;
-    }
-  }
+  (void)reduce_slab_block(q, blockIdx.x);
 }
 
 // ============================================================================================
@@ -1494,17 +1379,11 @@ static bool fused_active(const ppo_ctx *ctx) {
 // Precision bf16 with supported shapes: gather + bf16 weight refresh, the persistent fused
 // forward/loss/backward kernel (one partial-gradient slab per workgroup), then the fixed-order
 // slab reduction.  Same contract as the layered path below.
-static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
-                                const float *old_logp_d, const float *adv_d,
-                                const float *vtarget_d, const int32_t *rows_d, int b,
-                                const int32_t *count_d, float clip_lo, float clip_hi,
-                                float entropy_coef, float inv_b, float inv_ba, float *grad_d,
-                                float *loss_d, hipStream_t st, bool staged = false,
-                                bool pack_w = true) {
-  const int H = ctx->fused_hidden;
-  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
-  const int A = ctx->cfg.act_dim;
-  const int64_t P = ctx->total_params;
+static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                            const float *old_logp_d, const float *adv_d, const float *vtarget_d,
+                            const int32_t *rows_d, int b, const int32_t *count_d, float clip_lo,
+                            float clip_hi, float entropy_coef, float inv_b, float inv_ba,
+                            bool staged, bool pack_w) {
   FusedArgs q{};
   fused_nets(ctx, q.net);
   q.logstd = ctx->params + ctx->net[0].logstd_off;
@@ -1522,10 +1401,10 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   q.n_rec = staged ? ctx->frec_rows : 0;
   q.pack_w = pack_w;
   q.b = b;
-  q.din = din;
-  q.act_dim = A;
+  q.din = ctx->cfg.obs_dim * ctx->cfg.window;
+  q.act_dim = ctx->cfg.act_dim;
   q.act = ctx->cfg.activation;
-  q.hidden = H;
+  q.hidden = ctx->fused_hidden;
   q.omv = ctx->cfg.output_max_value;
   q.clip_lo = clip_lo;
   q.clip_hi = clip_hi;
@@ -1533,41 +1412,54 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   q.inv_b = inv_b;
   q.inv_ba = inv_ba;
   q.slabs = ctx->fslabs;
-  q.slab_stride = P;
+  q.slab_stride = ctx->total_params;
   q.loss_part = ctx->floss;
-  const int nchunks = ceil_div(b, kFusedRows);
-  q.G = std::min(kFusedMaxWG, nchunks);
+  q.G = std::min(kFusedMaxWG, ceil_div(b, kFusedRows));
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
-  ctx->fstamp_g = q.G;
+  return q;
+}
+
+// gather (q.b rows; 0 = none) and, with q.pack_w, the weight-image refresh
+static int fused_prep(const ppo_ctx *ctx, const FusedArgs &q, hipStream_t st) {
+  const double H = ctx->fused_hidden;
+  const int din = q.din, A = q.act_dim;
   // algorithmic traffic: gather (row index, din + A + 3 floats -- or one 128 B record -- in;
   // 64 + 64 B out per row) and weight images (f32 in, 3 bf16 images out per net)
   const double wbytes =
-      pack_w ? 2.0 * (4.0 * H * (din + H) + 2.0 * H * (kFusedKX + 2.0 * H)) : 0.0;
-  const double in_row = staged ? 4.0 + kRecordBytes : 4.0 * (1 + din + A + 3);
-  {
-    const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
-                     static_cast<double>(b) * (in_row + 2.0 * kFusedKX + 4.0 * kFusedSP) + wbytes};
-    if (int rc = fused_prep_launch(q, rec, st)) return rc;
+      q.pack_w ? 2.0 * (4.0 * H * (din + H) + 2.0 * H * (kFusedKX + 2.0 * H)) : 0.0;
+  const double in_row = q.rec ? 4.0 + kRecordBytes : 4.0 * (1 + din + A + 3);
+  const TimRec rec{KC_GATHER, "fused_prep_kernel", 0.0,
+                   static_cast<double>(q.b) * (in_row + 2.0 * kFusedKX + 4.0 * kFusedSP) + wbytes};
+  return fused_prep_launch(q, rec, st);
+}
+
+static int fused_forward_backward(ppo_ctx *ctx, const FusedArgs &q, hipStream_t st) {
+  const int H = ctx->fused_hidden, din = q.din, A = q.act_dim, b = q.b;
+  const int64_t P = ctx->total_params;
+  ctx->fstamp_g = q.G;
+  // FLOPs per row per net: forward (din*H + H*H + a*H), dgrad (H*H + a*H), wgrad (din*H +
+  // H*H + a*H), a = A (actor) / 1 (critic); bytes: staged rows + one slab per workgroup
+  double fl = 0.0;
+  for (int z = 0; z < 2; ++z) {
+    const double a = z == 0 ? A : 1;
+    fl += 2.0 * b * ((din * H + H * H + a * H) + (H * H + a * H) + (din * H + H * H + a * H));
   }
-  {
-    // FLOPs per row per net: forward (din*H + H*H + a*H), dgrad (H*H + a*H), wgrad (din*H +
-    // H*H + a*H), a = A (actor) / 1 (critic); bytes: staged rows + one slab per workgroup
-    double fl = 0.0;
-    for (int z = 0; z < 2; ++z) {
-      const double a = z == 0 ? A : 1;
-      fl += 2.0 * b * ((din * H + H * H + a * H) + (H * H + a * H) + (din * H + H * H + a * H));
-    }
-    // HBM bytes: the staged rows once, the bf16 weight images once (every workgroup re-reads
-    // them from L2, which is not HBM traffic) and one partial-gradient slab per workgroup
-    const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
-                      4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
-    const TimRec rec{KC_FUSED,
-                     tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act,
-                                                A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8)
-                                  : nullptr,
-                     fl, by};
-    if (int rc = fused_update_launch(q, rec, st)) return rc;
-  }
+  // HBM bytes: the staged rows once, the bf16 weight images once (every workgroup re-reads
+  // them from L2, which is not HBM traffic) and one partial-gradient slab per workgroup
+  const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
+                    4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
+  const TimRec rec{KC_FUSED,
+                   tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act,
+                                              A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8)
+                                : nullptr,
+                   fl, by};
+  return fused_update_launch(q, rec, st);
+}
+
+static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, float *grad_d,
+                                    float *loss_d) {
+  const int A = q.act_dim;
+  const int64_t P = ctx->total_params;
   ReduceArgs r{};
   int ns = 0;
   for (int z = 0; z < 2; ++z) {
@@ -1592,16 +1484,66 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   r.grad = grad_d;
   r.loss_part = ctx->floss;
   r.loss_splits = q.G;
-  r.inv_b = inv_b;
+  r.inv_b = q.inv_b;
   r.logstd = ctx->params + ctx->net[0].logstd_off;
   r.act_dim = A;
-  r.ent_coef = entropy_coef;
+  r.ent_coef = q.ent_coef;
   r.loss_out = loss_d;
+  return r;
+}
+
+static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                                const float *old_logp_d, const float *adv_d,
+                                const float *vtarget_d, const int32_t *rows_d, int b,
+                                const int32_t *count_d, float clip_lo, float clip_hi,
+                                float entropy_coef, float inv_b, float inv_ba, float *grad_d,
+                                float *loss_d, hipStream_t st, bool staged = false,
+                                bool pack_w = true) {
+  const FusedArgs q = fused_args(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d,
+                                 b, count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
+                                 staged, pack_w);
+  if (int rc = fused_prep(ctx, q, st)) return rc;
+  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
+  const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
+  const int64_t P = ctx->total_params;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(q.G) * P,
                   4.0 * (static_cast<double>(q.G) + 1) * P},
            reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);
   PPO_LAUNCHED();
   return 0;
+}
+
+// AdamPackArgs for the ctx's bound parameters (both nets) and the fused weight images
+static AdamPackArgs adam_pack_args(const ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
+                                   const float *sched_d, float neg_a, float neg_c, float bc2,
+                                   float omb1, float b2, float omb2, float eps) {
+  AdamPackArgs a{};
+  a.p = ctx->params;
+  a.g = g_d;
+  a.m = m_d;
+  a.v = v_d;
+  a.n = ctx->total_params;
+  a.n_actor = ctx->net[0].count;
+  a.sched = sched_d;
+  a.neg_a = neg_a;
+  a.neg_c = neg_c;
+  a.bc2 = bc2;
+  a.w1 = omb1;
+  a.b2 = b2;
+  a.omb2 = omb2;
+  a.eps = eps;
+  FusedNet nets[2];
+  fused_nets(ctx, nets);
+  for (int z = 0; z < 2; ++z) {
+    a.w0b[z] = const_cast<__bf16 *>(nets[z].w0b);
+    a.w1b[z] = const_cast<__bf16 *>(nets[z].w1b);
+    a.w1bt[z] = const_cast<__bf16 *>(nets[z].w1bt);
+    a.off_w0[z] = nets[z].off_w0;
+    a.off_w1[z] = nets[z].off_w1;
+  }
+  a.din = ctx->cfg.obs_dim * ctx->cfg.window;
+  a.H = ctx->fused_hidden;
+  return a;
 }
 
 static int check_ctx(const ppo_ctx *ctx) {
@@ -1952,36 +1894,61 @@ extern "C" int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *
   PPO_REQUIRE(fused_active(ctx), "ppo_adam_pack: needs the fused bf16 path");
   PPO_REQUIRE(g_d && m_d && v_d, "ppo_adam_pack: null buffer");
   TimingScope timing_scope(ctx);
-  AdamPackArgs a{};
-  a.p = ctx->params;
-  a.g = g_d;
-  a.m = m_d;
-  a.v = v_d;
-  a.n = ctx->total_params;
-  a.n_actor = ctx->net[0].count;
-  a.sched = sched_d;
-  a.neg_a = neg_step_actor;
-  a.neg_c = neg_step_critic;
-  a.bc2 = bc2_sqrt;
-  a.w1 = one_minus_beta1;
-  a.b2 = beta2;
-  a.omb2 = one_minus_beta2;
-  a.eps = eps;
-  FusedNet nets[2];
-  fused_nets(ctx, nets);
-  for (int z = 0; z < 2; ++z) {
-    a.w0b[z] = const_cast<__bf16 *>(nets[z].w0b);
-    a.w1b[z] = const_cast<__bf16 *>(nets[z].w1b);
-    a.w1bt[z] = const_cast<__bf16 *>(nets[z].w1bt);
-    a.off_w0[z] = nets[z].off_w0;
-    a.off_w1[z] = nets[z].off_w1;
-  }
-  a.din = ctx->cfg.obs_dim * ctx->cfg.window;
-  a.H = ctx->fused_hidden;
+  const AdamPackArgs a = adam_pack_args(ctx, g_d, m_d, v_d, sched_d, neg_step_actor,
+                                        neg_step_critic, bc2_sqrt, one_minus_beta1, beta2,
+                                        one_minus_beta2, eps);
   const double Hd = a.H;
   const TimRec rec{KC_ADAM, "adam_pack_kernel", 0.0,
                    28.0 * a.n + 2.0 * 2.0 * Hd * (a.din + 2.0 * Hd)};
   return adam_pack_launch(a, rec, as_stream(stream));
+}
+
+extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b,
+                                      const int32_t *next_rows_d, int next_b, float clip_lo,
+                                      float clip_hi, float entropy_coef, float inv_b,
+                                      float inv_ba, float *grad_d, float *loss_d, float *m_d,
+                                      float *v_d, const float *sched_d, float neg_step_actor,
+                                      float neg_step_critic, float bc2_sqrt,
+                                      float one_minus_beta1, float beta2, float one_minus_beta2,
+                                      float eps, int flags, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx) && ctx->frec && ctx->frec_rows > 0,
+              "ppo_update_step_staged: no staged records (ppo_stage_records first)");
+  PPO_REQUIRE(rows_d && grad_d && loss_d && m_d && v_d, "ppo_update_step_staged: null buffer");
+  PPO_REQUIRE(b > 0 && b <= ctx->cfg.max_rows && next_b >= 0 && next_b <= ctx->cfg.max_rows &&
+                  (next_b == 0) == (next_rows_d == nullptr),
+              "ppo_update_step_staged: b=%d next_b=%d (max_rows %d)", b, next_b,
+              ctx->cfg.max_rows);
+  PPO_REQUIRE((flags & ~(PPO_STAGED_WEIGHTS_CURRENT | PPO_STAGED_ROWS_GATHERED)) == 0,
+              "ppo_update_step_staged: flags %d", flags);
+  hipStream_t st = as_stream(stream);
+  TimingScope timing_scope(ctx);
+  const bool gathered = flags & PPO_STAGED_ROWS_GATHERED;
+  const bool current = flags & PPO_STAGED_WEIGHTS_CURRENT;
+  FusedArgs q = fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b, nullptr,
+                           clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, true, !current);
+  if (!gathered || !current) {
+    FusedArgs p = q;
+    p.b = gathered ? 0 : b;
+    if (int rc = fused_prep(ctx, p, st)) return rc;
+  }
+  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
+  // tail: slab reduction + Adam + weight images, and the next minibatch's row gather
+  const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
+  TailArgs t{};
+  t.a = adam_pack_args(ctx, grad_d, m_d, v_d, sched_d, neg_step_actor, neg_step_critic, bc2_sqrt,
+                       one_minus_beta1, beta2, one_minus_beta2, eps);
+  t.rows = next_rows_d;
+  t.rec = ctx->frec;
+  t.n_rec = ctx->frec_rows;
+  t.xb = ctx->fxb;
+  t.srow = ctx->fsrow;
+  t.b = next_b;
+  const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
+  const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
+                   4.0 * (q.G + 1.0) * P + 24.0 * P + 2.0 * 2.0 * H * (q.din + 2.0 * H) +
+                       static_cast<double>(next_b) * (4.0 + 2.0 * kRecordBytes)};
+  return step_tail_launch(r, t, rec, st);
 }
 
 extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d,

@@ -1,0 +1,138 @@
+// Deterministic split-K reduction of per-workgroup partial-gradient slabs into the flat
+// gradient, plus the minibatch loss scalars (ppo.py:121,133 `loss.item()` values).  Shared by
+// reduce_slabs_kernel (mlp_engine.hip) and step_tail_kernel (fused_update.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+namespace ppo {
+
+constexpr int kMaxSegs = 48;
+struct ReduceSeg {
+  int64_t dst, len;
+  const float *src;
+  int64_t stride;
+  int nsplit;
+};
+struct ReduceArgs {
+  ReduceSeg seg[kMaxSegs];
+  int nseg;
+  int64_t total;
+  float *grad;
+  const float *loss_part;
+  int loss_splits;
+  float inv_b;           // actor loss = -(sum min)*inv_b - ent_coef*H ; critic = sum*inv_b
+  const float *logstd;   // H = mean_a(0.5 + 0.5 log 2pi + log(exp(logstd_a))) (Normal.entropy)
+  int act_dim;
+  float ent_coef;
+  float *loss_out;
+};
+
+// Block = 64 float4 groups x 4 split-chunks (one wave per chunk): each thread sums a quarter of
+// the splits for 4 consecutive parameters (tensors start 16-float aligned, so a group never
+// straddles two tensors), then the chunks combine in a fixed order through LDS.  Block 0 also
+// reduces the per-split loss partials with a fixed-shape tree.  Deterministic run to run.
+// Returns, on the chunk-0 threads (i < total), the final sums of parameters i..i+3 (also stored
+// to q.grad); other threads get zeros.
+__device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t block) {
+  __shared__ float4 part[4][64];
+  __shared__ float lred[2][256];
+  const int tid = threadIdx.x, grp = tid & 63, chunk = tid >> 6;
+  const int64_t i = block * 256 + 4 * grp;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < q.total) {
+    int s = 0;
+    while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
+    const ReduceSeg &g = q.seg[s];
+    const int64_t off = i - g.dst;
+    const int k0 = (g.nsplit * chunk) / 4, k1 = (g.nsplit * (chunk + 1)) / 4;
+    // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per
+    // thread; the association is fixed, so the result is still deterministic run to run.
+    if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
+        reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
+      const float *src = g.src + off;
+      float4 acc1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      int k = k0;
+#pragma unroll 4
+      for (; k + 1 < k1; k += 2) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+        const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+        acc1.x += u.x;
+        acc1.y += u.y;
+        acc1.z += u.z;
+        acc1.w += u.w;
+      }
+      if (k < k1) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      acc = make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
+    } else if (off >= 0) {  // tail of a tensor / unaligned source (logstd partials, 1-wide
+                            // biases); padding stays zero.  8 strided partial sums per element.
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (off + e >= g.len) continue;
+        const float *src = g.src + off + e;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int k = k0;
+        for (; k + 7 < k1; k += 8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += src[static_cast<int64_t>(k + j) * g.stride];
+        }
+        for (; k < k1; ++k) s[0] += src[static_cast<int64_t>(k) * g.stride];
+        a4[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+      }
+      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
+    }
+  }
+  part[chunk][grp] = acc;
+  __syncthreads();
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (chunk == 0 && i < q.total) {
+    const float4 a = part[0][grp], b = part[1][grp], c = part[2][grp], d = part[3][grp];
+    out = make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
+                      ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
+    *reinterpret_cast<float4 *>(q.grad + i) = out;
+  }
+  if (block == 0 && q.loss_out) {
+    float la = 0.f, lc = 0.f;
+    for (int k = tid; k < q.loss_splits; k += 256) {
+      la += q.loss_part[2 * k];
+      lc += q.loss_part[2 * k + 1];
+    }
+    lred[0][tid] = la;
+    lred[1][tid] = lc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w) {
+        lred[0][tid] += lred[0][tid + w];
+        lred[1][tid] += lred[1][tid + w];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      float h = 0.f;
+      if (q.logstd) {
+        for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
+        h = h / static_cast<float>(q.act_dim);
+      }
+      q.loss_out[0] = -(lred[0][0] * q.inv_b) - h * q.ent_coef;
+      q.loss_out[1] = lred[1][0] * q.inv_b;
+    }
+  }
+  return out;
+}
+
+}  // namespace ppo

@@ -278,6 +278,36 @@ class Engine:
             self._ctx, ptr(rows), int(b), ptr(count), clip_lo, clip_hi, entropy_coef, inv_b,
             inv_ba, ptr(grad), ptr(loss), 1 if weights_current else 0, _stream(self.device)))
 
+    def update_step_staged(self, rows, b: int, grad, loss, m, v, clip_lo: float, clip_hi: float,
+                           entropy_coef: float, inv_b: float, inv_ba: float,
+                           sched: Optional[torch.Tensor] = None, neg_step_actor: float = 0.0,
+                           neg_step_critic: float = 0.0, bc2_sqrt: float = 1.0,
+                           one_minus_beta1: float = 0.1, beta2: float = 0.999,
+                           one_minus_beta2: float = 0.001, eps: float = 1e-8,
+                           next_rows: Optional[torch.Tensor] = None, weights_current: bool = False,
+                           rows_gathered: bool = False) -> None:
+        """One optimizer step on the staged records (single rank): minibatch_grad_staged, then
+        adam_pack, with the next minibatch's row gather (next_rows) folded into the last launch.
+        rows_gathered=True: the previous step's next_rows were these rows."""
+        _need(rows, "rows", torch.int32, device=self.device)
+        for name, t in (("grad", grad), ("m", m), ("v", v)):
+            _need(t, name, torch.float32, (self.n_params,), self.device)
+        _need(loss, "loss", torch.float32, device=self.device)
+        if loss.numel() != 2:
+            raise RuntimeError("loss must hold 2 floats")
+        if sched is not None:
+            _need(sched, "sched", torch.float32, None, self.device)
+        nb = 0
+        if next_rows is not None:
+            _need(next_rows, "next_rows", torch.int32, device=self.device)
+            nb = next_rows.numel()
+        flags = (1 if weights_current else 0) | (2 if rows_gathered else 0)
+        check(self.lib.ppo_update_step_staged(
+            self._ctx, ptr(rows), int(b), ptr(next_rows), nb, clip_lo, clip_hi, entropy_coef,
+            inv_b, inv_ba, ptr(grad), ptr(loss), ptr(m), ptr(v), ptr(sched), neg_step_actor,
+            neg_step_critic, bc2_sqrt, one_minus_beta1, beta2, one_minus_beta2, eps, flags,
+            _stream(self.device)))
+
     def adam_pack(self, g, m, v, sched: Optional[torch.Tensor] = None, neg_step_actor: float = 0.0,
                   neg_step_critic: float = 0.0, bc2_sqrt: float = 1.0,
                   one_minus_beta1: float = 0.1, beta2: float = 0.999,

@@ -583,3 +583,56 @@ def test_staged_records_and_adam_pack_match_unstaged(gpu, with_count):
     assert torch.equal(g2, g3), int((g2 != g3).sum())
     assert torch.equal(l2, l3)
     assert not torch.equal(g2, g1)  # the parameters did move
+
+
+def test_update_step_staged_matches_grad_plus_adam_pack(gpu):
+    """ppo_update_step_staged (fused forward/backward + one tail launch: slab reduction, Adam,
+    weight images, next-minibatch gather) gives bit-identical gradient, losses, p, m and v to
+    ppo_minibatch_grad_staged + ppo_adam_pack, for two chained steps (the second consuming the
+    rows and weight images the first left behind) and with host or device Adam scalars."""
+    n, t, b = 512, 16, 2048
+    run, eng, ref, cfg = _agents(gpu, 13, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    g = torch.Generator().manual_seed(5)
+    rows_total = n * t
+    states = torch.randn(t + 1, n, 17, generator=g).to(gpu)
+    actions = torch.randn(t, n, 6, generator=g).to(gpu)
+    old_lp = torch.randn(t, n, generator=g).to(gpu) - 5
+    adv = torch.randn(t, n, generator=g).to(gpu)
+    vt = torch.randn(t, n, generator=g).to(gpu)
+    rows = [torch.randperm(rows_total, generator=g)[:b].to(torch.int32).to(gpu) for _ in range(2)]
+    args = (0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    sc = [(-1e-3, -2e-3, 0.3), (-1.5e-3, -2.5e-3, 0.4)]
+    hyper = dict(one_minus_beta1=0.1, beta2=0.999, one_minus_beta2=0.001, eps=1e-8)
+    p0 = eng.flat_params.clone()
+    m0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-3
+    v0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-6
+    e.stage_records(states, actions, old_lp, adv, vt)
+    outs = {}
+    for mode in ("separate", "fused_host", "fused_sched"):
+        eng.flat_params.copy_(p0)
+        m, v = m0.clone(), v0.clone()
+        e.pack_weights()
+        grads, losses = [], []
+        for k in range(2):
+            grad, loss = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+            s = dict(zip(("neg_step_actor", "neg_step_critic", "bc2_sqrt"), sc[k]), **hyper)
+            if mode == "separate":
+                e.minibatch_grad_staged(rows[k], b, grad, loss, *args, weights_current=k > 0)
+                e.adam_pack(grad, m, v, None, **s)
+            else:
+                sched = torch.tensor(sc[k], device=gpu) if mode == "fused_sched" else None
+                if sched is not None:
+                    s = dict(hyper)
+                e.update_step_staged(rows[k], b, grad, loss, m, v, *args, sched=sched,
+                                     next_rows=rows[1] if k == 0 else None,
+                                     weights_current=k > 0, rows_gathered=k > 0, **s)
+            grads.append(grad.clone())
+            losses.append(loss.clone())
+        torch.cuda.synchronize()
+        outs[mode] = (torch.cat(grads), torch.cat(losses), eng.flat_params.clone(), m, v)
+    for mode in ("fused_host", "fused_sched"):
+        for name, x, y in zip(("grad", "loss", "params", "m", "v"), outs["separate"], outs[mode]):
+            assert torch.equal(x, y), (mode, name, int((x != y).sum()))
+    assert not torch.equal(outs["separate"][2], p0)
