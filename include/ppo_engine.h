@@ -180,7 +180,8 @@ int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions
  *   the first call for a given size allocates and must not be inside a graph capture);
  *   ppo_minibatch_grad_staged(rows_d, b, count_d, ...) is ppo_minibatch_grad on those records.
  *   flags PPO_STAGED_WEIGHTS_CURRENT: the bf16 weight images are already current (the previous
- *   optimizer step was ppo_adam_pack), so the weight refresh is skipped. */
+ *   optimizer step was ppo_adam_pack), so the weight refresh is skipped; PPO_STAGED_ROWS_GATHERED:
+ *   the previous step (ppo_adam_pack_gather) gathered rows_d already (count_d must be NULL). */
 #define PPO_STAGED_WEIGHTS_CURRENT 1
 #define PPO_STAGED_ROWS_GATHERED 2
 int ppo_ctx_fused_active(const ppo_ctx *ctx);
@@ -191,6 +192,16 @@ int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b, const 
                               float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                               float inv_ba, float *grad_d, float *loss_d, int flags,
                               void *stream);
+
+/* ppo_adam_pack that also gathers the NEXT minibatch's rows next_rows_d[0, next_b) from the
+ * staged records (the data-parallel form of ppo_update_step_staged's tail: grad_d is the
+ * all-reduced gradient).  The next ppo_minibatch_grad_staged then passes
+ * PPO_STAGED_ROWS_GATHERED | PPO_STAGED_WEIGHTS_CURRENT. */
+int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
+                         const float *sched_d, float neg_step_actor, float neg_step_critic,
+                         float bc2_sqrt, float one_minus_beta1, float beta2,
+                         float one_minus_beta2, float eps, const int32_t *next_rows_d,
+                         int next_b, void *stream);
 
 /* One whole optimizer step of the staged single-rank path (ppo.py:109-135 for one minibatch,
  * then both optimizers' step()), in at most three launches: [row gather / weight refresh],

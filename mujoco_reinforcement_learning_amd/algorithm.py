@@ -201,7 +201,7 @@ class PPOEngine:
 
     # ---- ppo.py:93-154 ---------------------------------------------------------------------
     def _scheduled_ok(self) -> bool:
-        return self._rng() == "philox" and not self.dp.active
+        return self._rng() == "philox" and (not self.dp.active or self.dp.mode == "local")
 
     def _train_scheduled(self, memory: RolloutBuffer, b: int, epochs: int, batches: int, clip_lo,
                          clip_hi, inv_b, inv_ba):
@@ -210,7 +210,9 @@ class PPOEngine:
         step sizes come from a device schedule.  Per step: on the fused bf16 path one
         ppo_update_step_staged (fused forward/backward + a tail that reduces, steps Adam, refreshes
         the weight images and gathers the next minibatch's rows); otherwise minibatch_grad +
-        adam_sched.  With engine_config.train_graph the loop is captured once as a hipGraph and
+        adam_sched.  Data parallel ("local" mode): the fused gradient, the all-reduce, then
+        Adam + weight images + the next minibatch's gather (adam_pack(next_rows=...)).  With
+        engine_config.train_graph (single rank) the loop is captured once as a hipGraph and
         replayed (same launches, bit-identical results)."""
         agent, eng, buf = self.agent, self.agent.engine, memory
         n, t_len = buf.num_envs, buf.horizon
@@ -227,8 +229,8 @@ class PPOEngine:
             self._tg_graph = None
             self._tg_warm = False
         for epoch in range(epochs):
-            E.feistel_rows(self._seed(), self.iteration * epochs + epoch, 0, batches * b, n, t_len,
-                           self._tg_rows[epoch])
+            E.feistel_rows(self._seed() + 7919 * self.dp.rank, self.iteration * epochs + epoch, 0,
+                           batches * b, n, t_len, self._tg_rows[epoch])
         self._tg_sched.copy_(sched, non_blocking=True)
         beta1, beta2 = agent.optimizers["actor"].param_groups[0]["betas"]
         eps = agent.optimizers["actor"].param_groups[0]["eps"]
@@ -248,24 +250,34 @@ class PPOEngine:
                     k = epoch * batches + i
                     rows = rows_of(k)
                     sched = self._tg_sched[k]
+                    nxt = rows_of(k + 1) if k + 1 < steps else None
+                    if staged and self.dp.active:
+                        eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
+                                                  clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
+                                                  weights_current=k > 0, rows_gathered=k > 0)
+                        self.dp.allreduce_grad(agent.flat_grad)
+                        eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
+                                      one_minus_beta1=1 - beta1, beta2=beta2,
+                                      one_minus_beta2=1 - beta2, eps=eps, next_rows=nxt)
+                        continue
                     if staged:
                         eng.update_step_staged(
                             rows, b, agent.flat_grad, self._loss_buf[epoch, i], agent.flat_m,
                             agent.flat_v, clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
                             sched=sched, one_minus_beta1=1 - beta1, beta2=beta2,
                             one_minus_beta2=1 - beta2, eps=eps,
-                            next_rows=rows_of(k + 1) if k + 1 < steps else None,
-                            weights_current=k > 0, rows_gathered=k > 0)
+                            next_rows=nxt, weights_current=k > 0, rows_gathered=k > 0)
                         continue
                     eng.minibatch_grad(buf.states, buf.actions, buf.logp, buf.advantage,
                                        buf.value_target, rows, b, agent.flat_grad,
                                        self._loss_buf[epoch, i], clip_lo, clip_hi,
                                        ppo.entropy_eps, inv_b, inv_ba)
+                    self.dp.allreduce_grad(agent.flat_grad)
                     E.adam_sched(agent.flat_params, agent.flat_grad, agent.flat_m, agent.flat_v,
                                  eng.n_actor, sched, 1 - beta1, beta2, 1 - beta2, eps)
 
-        if not getattr(self.run.engine_config, "train_graph", True):
-            body()
+        if self.dp.active or not getattr(self.run.engine_config, "train_graph", True):
+            body()  # collectives stay outside hipGraphs
             return self._loss_buf
         if self._tg_graph is None:
             if not self._tg_warm:  # first call eager: lazy workspace / timing setup outside capture

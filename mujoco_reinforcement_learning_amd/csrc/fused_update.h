@@ -93,6 +93,7 @@ struct TailArgs {
   __bf16 *xb;
   float *srow;
   int b;
+  bool reduce;  // false: no slab reduction, Adam on the gradient already in a.g (data parallel)
 };
 int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st);
 // The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.

@@ -235,10 +235,16 @@ __global__ __launch_bounds__(256) void step_tail_kernel(ReduceArgs r, TailArgs t
     tail_gather(t, static_cast<int64_t>(blockIdx.x) - red_blocks, tid);
     return;
   }
-  const float4 g4 = reduce_slab_block(r, blockIdx.x);
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * (tid & 63);
-  if ((tid >> 6) != 0 || i >= r.total) return;
   const AdamPackArgs &a = t.a;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * (tid & 63);
+  float4 g4;
+  if (t.reduce) {
+    g4 = reduce_slab_block(r, blockIdx.x);
+    if ((tid >> 6) != 0 || i >= r.total) return;
+  } else {
+    if ((tid >> 6) != 0 || i >= a.n) return;
+    g4 = *reinterpret_cast<const float4 *>(a.g + i);
+  }
   const float ns = i < a.n_actor ? (a.sched ? a.sched[0] : a.neg_a) : (a.sched ? a.sched[1] : a.neg_c);
   const float bc2 = a.sched ? a.sched[2] : a.bc2;
   float4 p4 = *reinterpret_cast<const float4 *>(a.p + i);
@@ -884,9 +890,10 @@ int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st) {
 }
 
 int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st) {
-  PPO_REQUIRE(t.a.H % 4 == 0 && t.a.din >= 1 && t.a.din <= kFusedKX && r.total == t.a.n,
+  PPO_REQUIRE(t.a.H % 4 == 0 && t.a.din >= 1 && t.a.din <= kFusedKX &&
+                  (!t.reduce || r.total == t.a.n),
               "step tail: H=%d din=%d", t.a.H, t.a.din);
-  const int red_blocks = static_cast<int>(ceil_div(r.total, 256));
+  const int red_blocks = static_cast<int>(ceil_div(t.a.n, 256));
   const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, 256));
   launch_k(rec, step_tail_kernel, dim3(red_blocks + gather_blocks), dim3(256), 0, st, r, t,
            red_blocks);

@@ -1498,11 +1498,15 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
                                 const int32_t *count_d, float clip_lo, float clip_hi,
                                 float entropy_coef, float inv_b, float inv_ba, float *grad_d,
                                 float *loss_d, hipStream_t st, bool staged = false,
-                                bool pack_w = true) {
+                                bool pack_w = true, bool gathered = false) {
   const FusedArgs q = fused_args(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d,
                                  b, count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
                                  staged, pack_w);
-  if (int rc = fused_prep(ctx, q, st)) return rc;
+  if (!gathered || pack_w) {
+    FusedArgs p = q;
+    p.b = gathered ? 0 : b;
+    if (int rc = fused_prep(ctx, p, st)) return rc;
+  }
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
   const int64_t P = ctx->total_params;
@@ -1877,13 +1881,47 @@ extern "C" int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, in
   PPO_REQUIRE(rows_d && grad_d && loss_d, "ppo_minibatch_grad_staged: null buffer");
   PPO_REQUIRE(b > 0 && b <= ctx->cfg.max_rows,
               "ppo_minibatch_grad_staged: b=%d outside [1, max_rows=%d]", b, ctx->cfg.max_rows);
-  PPO_REQUIRE((flags & ~PPO_STAGED_WEIGHTS_CURRENT) == 0, "ppo_minibatch_grad_staged: flags %d",
-              flags);
+  PPO_REQUIRE((flags & ~(PPO_STAGED_WEIGHTS_CURRENT | PPO_STAGED_ROWS_GATHERED)) == 0,
+              "ppo_minibatch_grad_staged: flags %d", flags);
+  PPO_REQUIRE(!(flags & PPO_STAGED_ROWS_GATHERED) || count_d == nullptr,
+              "ppo_minibatch_grad_staged: pre-gathered rows take no device count");
   TimingScope timing_scope(ctx);
   return fused_minibatch_grad(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b,
                               count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
                               loss_d, as_stream(stream), true,
-                              (flags & PPO_STAGED_WEIGHTS_CURRENT) == 0);
+                              (flags & PPO_STAGED_WEIGHTS_CURRENT) == 0,
+                              (flags & PPO_STAGED_ROWS_GATHERED) != 0);
+}
+
+extern "C" int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
+                                    const float *sched_d, float neg_step_actor,
+                                    float neg_step_critic, float bc2_sqrt, float one_minus_beta1,
+                                    float beta2, float one_minus_beta2, float eps,
+                                    const int32_t *next_rows_d, int next_b, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx) && ctx->frec && ctx->frec_rows > 0,
+              "ppo_adam_pack_gather: no staged records (ppo_stage_records first)");
+  PPO_REQUIRE(g_d && m_d && v_d, "ppo_adam_pack_gather: null buffer");
+  PPO_REQUIRE(next_b >= 0 && next_b <= ctx->cfg.max_rows && (next_b == 0) == (next_rows_d == nullptr),
+              "ppo_adam_pack_gather: next_b=%d", next_b);
+  TimingScope timing_scope(ctx);
+  TailArgs t{};
+  t.a = adam_pack_args(ctx, g_d, m_d, v_d, sched_d, neg_step_actor, neg_step_critic, bc2_sqrt,
+                       one_minus_beta1, beta2, one_minus_beta2, eps);
+  t.rows = next_rows_d;
+  t.rec = ctx->frec;
+  t.n_rec = ctx->frec_rows;
+  t.xb = ctx->fxb;
+  t.srow = ctx->fsrow;
+  t.b = next_b;
+  t.reduce = false;
+  ReduceArgs r{};
+  r.total = ctx->total_params;
+  const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
+  const TimRec rec{KC_ADAM, "step_tail_kernel", 0.0,
+                   28.0 * P + 2.0 * 2.0 * H * (t.a.din + 2.0 * H) +
+                       static_cast<double>(next_b) * (4.0 + 2.0 * kRecordBytes)};
+  return step_tail_launch(r, t, rec, as_stream(stream));
 }
 
 extern "C" int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
@@ -1944,6 +1982,7 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.xb = ctx->fxb;
   t.srow = ctx->fsrow;
   t.b = next_b;
+  t.reduce = true;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
                    4.0 * (q.G + 1.0) * P + 24.0 * P + 2.0 * 2.0 * H * (q.din + 2.0 * H) +

@@ -266,9 +266,10 @@ class Engine:
     def minibatch_grad_staged(self, rows, b: int, grad, loss, clip_lo: float, clip_hi: float,
                               entropy_coef: float, inv_b: float, inv_ba: float,
                               count: Optional[torch.Tensor] = None,
-                              weights_current: bool = False) -> None:
+                              weights_current: bool = False, rows_gathered: bool = False) -> None:
         """minibatch_grad on the staged records; weights_current=True skips the bf16 weight
-        refresh (valid right after adam_pack)."""
+        refresh (valid right after adam_pack), rows_gathered=True the row gather (the previous
+        adam_pack(next_rows=rows) did it)."""
         _need(rows, "rows", torch.int32, device=self.device)
         _need(grad, "grad", torch.float32, (self.n_params,), self.device)
         _need(loss, "loss", torch.float32, device=self.device)
@@ -276,7 +277,8 @@ class Engine:
             raise RuntimeError("loss must hold 2 floats")
         check(self.lib.ppo_minibatch_grad_staged(
             self._ctx, ptr(rows), int(b), ptr(count), clip_lo, clip_hi, entropy_coef, inv_b,
-            inv_ba, ptr(grad), ptr(loss), 1 if weights_current else 0, _stream(self.device)))
+            inv_ba, ptr(grad), ptr(loss), (1 if weights_current else 0) | (2 if rows_gathered else 0),
+            _stream(self.device)))
 
     def update_step_staged(self, rows, b: int, grad, loss, m, v, clip_lo: float, clip_hi: float,
                            entropy_coef: float, inv_b: float, inv_ba: float,
@@ -311,15 +313,24 @@ class Engine:
     def adam_pack(self, g, m, v, sched: Optional[torch.Tensor] = None, neg_step_actor: float = 0.0,
                   neg_step_critic: float = 0.0, bc2_sqrt: float = 1.0,
                   one_minus_beta1: float = 0.1, beta2: float = 0.999,
-                  one_minus_beta2: float = 0.001, eps: float = 1e-8) -> None:
+                  one_minus_beta2: float = 0.001, eps: float = 1e-8,
+                  next_rows: Optional[torch.Tensor] = None) -> None:
         """ppo_adam on the bound parameters (ppo_adam_sched when sched is given) that also
-        refreshes the fused kernels' bf16 weight images."""
+        refreshes the fused kernels' bf16 weight images; with next_rows, also gathers the next
+        minibatch's rows from the staged records (ppo_adam_pack_gather)."""
         for name, t in (("g", g), ("m", m), ("v", v)):
             _need(t, name, torch.float32, (self.n_params,), self.device)
         if sched is not None:
             _need(sched, "sched", torch.float32, None, self.device)
             if sched.numel() < 3:
                 raise RuntimeError("sched must hold 3 floats")
+        if next_rows is not None:
+            _need(next_rows, "next_rows", torch.int32, device=self.device)
+            check(self.lib.ppo_adam_pack_gather(
+                self._ctx, ptr(g), ptr(m), ptr(v), ptr(sched), neg_step_actor, neg_step_critic,
+                bc2_sqrt, one_minus_beta1, beta2, one_minus_beta2, eps, ptr(next_rows),
+                next_rows.numel(), _stream(self.device)))
+            return
         check(self.lib.ppo_adam_pack(self._ctx, ptr(g), ptr(m), ptr(v), ptr(sched),
                                      neg_step_actor, neg_step_critic, bc2_sqrt, one_minus_beta1,
                                      beta2, one_minus_beta2, eps, _stream(self.device)))

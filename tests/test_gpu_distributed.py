@@ -81,3 +81,59 @@ def test_exact_dp_two_ranks_match_single_process(gpu):
     assert float(diff.max()) <= 2 * 1e-4 * EPOCHS * (N_GLOBAL * T // B), float(diff.max())
     close = diff <= 1e-5 * p_single.abs() + 1e-7
     assert float(close.float().mean()) >= 0.97
+
+
+def _local_worker(rank, world, port, q):
+    """Weak-scaling ("local") data parallel on the fused bf16 path: each rank its own env shard
+    and Philox shuffles; per step the fused gradient, the all-reduce, Adam + images + next
+    gather.  Returns the parameters after two iterations and the kernels that ran."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    dev = torch.device("cuda", 0)
+    n, t, b = 64, 16, 256
+    s = make_synthetic_streams(n, t, 17, seed=31 + rank, p_terminate=0.05, device=dev)
+    run = make_run(num_envs=n, horizon=t, hidden=(256, 256), batch_size=b, epochs=2,
+                   rng="philox", seed=rank, dp_mode="local", precision="bf16")
+    torch.manual_seed(0)
+    agent = PPOEngineAgent(run, device=dev)
+    algo = PPOEngine(SyntheticVecEnvHelper(s, run, device=dev), agent, log=lambda m: None)
+    agent.engine.timing(True, capacity=4096)
+    for _ in range(2):
+        algo.iterate(verbose=False)
+    torch.cuda.synchronize()
+    kernels = sorted(agent.engine.timing_kernels())
+    agent.engine.timing(False)
+    q.put((rank, agent.packed_params().cpu(), kernels, algo.last_losses))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_local_dp_two_ranks_fused_replicas_agree(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r, params, kernels, losses = q.get(timeout=300)
+        got[r] = (params, kernels, losses)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # replicas bit-identical (same all-reduced gradient, same Adam), and they moved
+    assert torch.equal(got[0][0], got[1][0])
+    assert all(abs(x) < 1e6 for x in got[0][2])
+    kernels = got[0][1]
+    assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
+    assert "step_tail_kernel" in kernels, kernels           # Adam + images + next gather
+    assert "reduce_slabs_kernel" in kernels, kernels         # grad folded before the all-reduce
