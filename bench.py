@@ -147,10 +147,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+    # rehearsal knobs (not the measured configuration): PPO_BENCH_BACKEND=gloo and
+    # PPO_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the data-parallel path
+    if os.environ.get("PPO_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("PPO_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
     from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
