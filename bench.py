@@ -59,6 +59,10 @@ def parse():
     p.add_argument("--no-timing", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--timing-iters", type=int, default=2,
                    help="eager iterations after the timed region that carry per-kernel events")
+    p.add_argument("--env", choices=("device", "host"), default="device",
+                   help="device: synthetic dynamics on the GPU (the measured default); host: the "
+                        "same dynamics in a host worker pool with pinned async copies (PCIe-inclusive)")
+    p.add_argument("--env-workers", type=int, default=8, help="host pool worker processes")
     p.add_argument("--no-graphs", action="store_true",
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -176,7 +180,11 @@ def main():
     torch.manual_seed(0)  # identical initial parameters on every rank
     agent = PPOEngineAgent(run, device=dev)
     streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
-    helper = SyntheticVecEnvHelper(streams, run, device=dev)
+    if args.env == "host":
+        from mujoco_reinforcement_learning_amd.environments import HostPhysicsVecEnvHelper
+        helper = HostPhysicsVecEnvHelper(streams, run, device=dev, workers=args.env_workers)
+    else:
+        helper = SyntheticVecEnvHelper(streams, run, device=dev)
     algo = PPOEngine(helper, agent, log=lambda m: None)
 
     for _ in range(args.warmup):
@@ -223,6 +231,9 @@ def main():
                                     f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
                        "epochs": args.epochs, "rng": args.rng, "hipgraphs": not args.no_graphs,
+                       "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
+                               else f"host pool ({args.env_workers} worker processes, page-locked "
+                                    "shared memory, hipMemcpyAsync on a side stream)"),
                        "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
     if kernels:
         traffic = load_traffic(args.traffic)
@@ -241,6 +252,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args, hidden)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if hasattr(helper, "close"):
+        helper.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -245,6 +245,15 @@ int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d, const 
                   float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
                   void *stream);
 
+/* ---- host physics pool transfers (no reference counterpart: the
+ * reference steps MuJoCo in-process, running_gym_sequential_vectorized.py:21-59) ------------------
+ * Page-lock a host region (the pool's shared-memory obs / reward / terminated / action arrays) so
+ * ppo_memcpy_async moves it by DMA without a staging copy; kind 1 = host->device, 2 =
+ * device->host, asynchronous on `stream`. */
+int ppo_host_register(void *host, int64_t bytes);
+int ppo_host_unregister(void *host);
+int ppo_memcpy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
+
 /* ---- measurement: per-kernel-class timing (no reference counterpart; replaces @timeit,
  * error_handling_utils.py:5-17, with device-side timing) -----------------------------------------
  * enable=1 (re)starts recording a HIP event pair around every launch the ctx issues, on the

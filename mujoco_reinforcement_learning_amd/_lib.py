@@ -81,6 +81,9 @@ _SIGNATURES = {
                                 c_int, c_void_p, c_int, c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_ctx_fused_active": (c_int, [c_void_p]),
+    "ppo_host_register": (c_int, [c_void_p, c_int64]),
+    "ppo_host_unregister": (c_int, [c_void_p]),
+    "ppo_memcpy_async": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "ppo_stage_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_void_p]),
     "ppo_minibatch_grad_staged": (c_int, [c_void_p, c_void_p, c_int, c_void_p, ctypes.c_float,

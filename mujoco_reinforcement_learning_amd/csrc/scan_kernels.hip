@@ -624,6 +624,30 @@ extern "C" int ppo_synthetic_env_step(const float *base_obs_d, const float *base
   return 0;
 }
 
+// ---- host physics pool transfers (north_star: pinned hipMemcpyAsync obs->GPU / action->CPU) ----
+extern "C" int ppo_host_register(void *host, int64_t bytes) {
+  PPO_REQUIRE(host && bytes > 0, "ppo_host_register: bad args");
+  PPO_HIP_TRY(hipHostRegister(host, static_cast<size_t>(bytes), hipHostRegisterDefault));
+  return 0;
+}
+
+extern "C" int ppo_host_unregister(void *host) {
+  PPO_REQUIRE(host, "ppo_host_unregister: null");
+  PPO_HIP_TRY(hipHostUnregister(host));
+  return 0;
+}
+
+// kind 1: host -> device, 2: device -> host; asynchronous on `stream` (host side pinned or
+// registered for a true DMA)
+extern "C" int ppo_memcpy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream) {
+  PPO_REQUIRE(dst && src && bytes >= 0 && (kind == 1 || kind == 2), "ppo_memcpy_async: bad args");
+  if (bytes == 0) return 0;
+  PPO_HIP_TRY(hipMemcpyAsync(dst, src, static_cast<size_t>(bytes),
+                             kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                             as_stream(stream)));
+  return 0;
+}
+
 extern "C" int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, int64_t n,
                                  void *stream) {
   PPO_REQUIRE(out_d && n >= 0, "ppo_philox_normal: bad args");

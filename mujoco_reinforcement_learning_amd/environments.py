@@ -159,3 +159,86 @@ class SyntheticVecEnvHelper:
         else:
             ts.observation[environment_index, :, :-1] = ts.observation[environment_index, :,
                                                                        1:].clone()
+
+
+class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
+    """EnvironmentHelper whose physics runs on host cores (host_pool.HostPhysicsPool, P worker
+    processes over env slices in shared memory), with the transfers the north_star names:
+    actions device->host and observations / rewards / terminations host->device as
+    hipMemcpyAsync on a side stream between page-locked shared memory and the device.  Same
+    dynamics and values as :class:`SyntheticVecEnvHelper` (tested bit-for-bit); not
+    hipGraph-capturable (host work every step)."""
+
+    graph_safe = False
+
+    def __init__(self, streams: Optional[dict] = None, run: Optional[Run] = None,
+                 device: Optional[torch.device] = None, seed: int = 0, p_terminate: float = 0.0,
+                 workers: int = 4):
+        self._workers = workers
+        self.pool = None
+        super().__init__(streams, run, device, seed, p_terminate)
+
+    def initialize(self):
+        from .host_pool import HostPhysicsPool
+        super().initialize()  # device-side window / timestep buffers + device copies of streams
+        lib = E._lib.load()
+        if self.pool is not None:
+            self.close()
+        a = self.run.network_config.output_shape
+        self.pool = HostPhysicsPool(self.base_obs.cpu().numpy(), self.base_reward.cpu().numpy(),
+                                    self.base_terminated.cpu().numpy(), a, self._workers)
+        self._registered = []
+        for key in ("action", "obs", "reward", "term"):
+            arr = self.pool.v[key]
+            E.check(lib.ppo_host_register(arr.ctypes.data, arr.nbytes))
+            self._registered.append(arr.ctypes.data)
+        self._side = torch.cuda.Stream(device=self.device)
+        self._lib = lib
+
+    def close(self):
+        if self.pool is None:
+            return
+        torch.cuda.synchronize(self.device)
+        for p in getattr(self, "_registered", []):
+            self._lib.ppo_host_unregister(p)
+        self._registered = []
+        self.pool.close()
+        self.pool = None
+
+    def _physics(self, action: torch.Tensor, reward_out: torch.Tensor,
+                 terminated_out: torch.Tensor) -> None:
+        t = self.t
+        if t >= self.horizon:
+            raise RuntimeError("host VecEnv: horizon exhausted; call reset_environment()")
+        v, lib, side = self.pool.v, self._lib, self._side
+        cur = torch.cuda.current_stream(self.device)
+        act = action.contiguous()
+        side.wait_stream(cur)  # the policy that produced the actions
+        s = side.cuda_stream
+        E.check(lib.ppo_memcpy_async(v["action"].ctypes.data, act.data_ptr(), v["action"].nbytes,
+                                     2, s))
+        side.synchronize()  # the workers need the actions on the host
+        self.pool.step(t)
+        E.check(lib.ppo_memcpy_async(self._obs_next.data_ptr(), v["obs"].ctypes.data,
+                                     v["obs"].nbytes, 1, s))
+        E.check(lib.ppo_memcpy_async(reward_out.data_ptr(), v["reward"].ctypes.data,
+                                     v["reward"].nbytes, 1, s))
+        E.check(lib.ppo_memcpy_async(terminated_out.data_ptr(), v["term"].ctypes.data,
+                                     v["term"].nbytes, 1, s))
+        cur.wait_stream(side)  # later kernels see the uploaded step
+        act.record_stream(side)
+        self.timestep.reward = reward_out
+        self.timestep.terminated = terminated_out
+        self.t = t + 1
+
+    def step(self, action: torch.Tensor, reward_out: Optional[torch.Tensor] = None,
+             terminated_out: Optional[torch.Tensor] = None):
+        reward = reward_out if reward_out is not None else self.timestep.reward
+        term = terminated_out if terminated_out is not None else self.timestep.terminated
+        self._physics(action, reward, term)
+        E.obs_window_push(self.timestep.observation, self._obs_next, reset=term)
+
+    def step_raw(self, action: torch.Tensor, reward_out: torch.Tensor,
+                 terminated_out: torch.Tensor) -> torch.Tensor:
+        self._physics(action, reward_out, terminated_out)
+        return self._obs_next

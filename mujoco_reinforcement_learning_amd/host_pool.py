@@ -1,0 +1,163 @@
+"""Host physics pool (BASELINE north_star: "MuJoCo physics itself stays on
+the host cores as a vectorized subprocess pool with pinned hipMemcpyAsync obs->GPU / action->CPU
+overlapped on a side stream").
+
+The reference steps its VecEnv in-process (``running_gym_sequential_vectorized.py:21-59``:
+``gymnasium.make_vec`` + a per-env Python window loop).  Here P worker processes each own a
+contiguous slice of the N envs.  All per-step arrays live in POSIX shared memory that the GPU side
+page-locks (``ppo_host_register``):
+- actions (N, A) f32, written by a device->host DMA;
+- next observations (N, O) f64, rewards (N,) f64 and terminations (N,) u8, read back by
+  host->device DMAs.
+
+One step is then: DMA actions down, release the workers (a generation word in shared memory),
+every worker advances its slice and publishes its done word, DMA the results up.  Hand-offs spin
+on those words (yielding the core), so a step costs microseconds of synchronisation rather than a
+semaphore round trip.  Workers import numpy only and never touch the GPU.
+
+Physics: gymnasium / mujoco are not installed in this image, so the workers run the engine's
+synthetic dynamics (``environments.py`` docstring; bit-identical to
+``synthetic_env_step_kernel``):
+
+    obs'      = base_obs[t+1] + 0.1 * a[:, o % A]      (f64)
+    reward    = base_reward[t] - 0.01 * sum_a a^2      (f64, summed in order)
+    terminated = base_terminated[t]
+
+``step_slice`` is the one function a real MuJoCo pool replaces: it would call ``env.step`` on the
+worker's gymnasium envs.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import time
+from multiprocessing import shared_memory
+from typing import Dict, Tuple
+
+import numpy as np
+
+# ctrl words: step index, stop flag, step generation (bumped by the host to release a step)
+_CTRL_T, _CTRL_STOP, _CTRL_GEN = 0, 1, 2
+
+
+def _attach(specs: Dict[str, Tuple[str, tuple, str]]):
+    shms, views = [], {}
+    for key, (name, shape, dtype) in specs.items():
+        shm = shared_memory.SharedMemory(name=name)
+        shms.append(shm)
+        views[key] = np.ndarray(shape, dtype=np.dtype(dtype), buffer=shm.buf)
+    return shms, views
+
+
+def step_slice(v: Dict[str, np.ndarray], t: int, lo: int, hi: int) -> None:
+    """Advance envs [lo, hi) by one step (the synthetic dynamics above)."""
+    a = v["action"][lo:hi].astype(np.float64)
+    n_act = a.shape[1]
+    o = v["obs"].shape[1]
+    v["obs"][lo:hi] = v["base_obs"][t + 1, lo:hi].astype(np.float64) + 0.1 * a[:, np.arange(o) % n_act]
+    ctrl = np.zeros(hi - lo)
+    for j in range(n_act):  # in order, as the kernel's loop
+        ctrl = ctrl + a[:, j] * a[:, j]
+    v["reward"][lo:hi] = v["base_reward"][t, lo:hi].astype(np.float64) - 0.01 * ctrl
+    v["term"][lo:hi] = v["base_term"][t, lo:hi]
+
+
+def _wait_change(word: np.ndarray, idx: int, old: int, stop: np.ndarray = None) -> int:
+    """Spin (yielding the core) until word[idx] != old; a step hand-off costs microseconds
+    instead of a semaphore round trip."""
+    while True:
+        cur = int(word[idx])
+        if cur != old or (stop is not None and stop[_CTRL_STOP]):
+            return cur
+        time.sleep(0)
+
+
+def _worker(wid: int, lo: int, hi: int, specs) -> None:
+    shms, v = _attach(specs)
+    ctrl, done = v["ctrl"], v["done"]
+    gen = 0
+    try:
+        while True:
+            gen = _wait_change(ctrl, _CTRL_GEN, gen, stop=ctrl)
+            if ctrl[_CTRL_STOP]:
+                break
+            step_slice(v, int(ctrl[_CTRL_T]), lo, hi)
+            done[wid] = gen  # publish after the slice's outputs are written
+    finally:
+        for s in shms:
+            s.close()
+
+
+class HostPhysicsPool:
+    """P worker processes stepping env slices in shared memory (see the module docstring)."""
+
+    def __init__(self, base_obs: np.ndarray, base_reward: np.ndarray, base_term: np.ndarray,
+                 act_dim: int, workers: int = 4):
+        t1, n, o = base_obs.shape
+        self.num_envs, self.obs_dim, self.act_dim = n, o, act_dim
+        self.workers = max(1, min(int(workers), n))
+        arrays = {
+            "base_obs": (base_obs.shape, "float32"),
+            "base_reward": (base_reward.shape, "float32"),
+            "base_term": (base_term.shape, "uint8"),
+            "action": ((n, act_dim), "float32"),
+            "obs": ((n, o), "float64"),
+            "reward": ((n,), "float64"),
+            "term": ((n,), "uint8"),
+            "ctrl": ((3,), "int64"),
+            "done": ((max(1, min(int(workers), n)),), "int64"),
+        }
+        self._shms, self.specs, self.v = [], {}, {}
+        for key, (shape, dtype) in arrays.items():
+            nbytes = max(1, int(np.prod(shape)) * np.dtype(dtype).itemsize)
+            shm = shared_memory.SharedMemory(create=True, size=nbytes)
+            self._shms.append(shm)
+            self.specs[key] = (shm.name, shape, dtype)
+            self.v[key] = np.ndarray(shape, dtype=np.dtype(dtype), buffer=shm.buf)
+        self.v["base_obs"][...] = base_obs
+        self.v["base_reward"][...] = base_reward
+        self.v["base_term"][...] = base_term.astype(np.uint8)
+        self.v["ctrl"][...] = 0
+        self.v["done"][...] = 0
+        self._gen = 0
+        ctx = mp.get_context("spawn")  # never fork a process that may have initialised HIP
+        bounds = np.linspace(0, n, self.workers + 1).astype(int)
+        self._procs = [ctx.Process(target=_worker, daemon=True,
+                                   args=(i, int(bounds[i]), int(bounds[i + 1]), self.specs))
+                       for i in range(self.workers)]
+        for p in self._procs:
+            p.start()
+        self._closed = False
+
+    def step(self, t: int) -> None:
+        """Advance all envs from step t (workers read v['action'], write obs / reward / term)."""
+        self._gen += 1
+        ctrl, done = self.v["ctrl"], self.v["done"]
+        ctrl[_CTRL_T] = t
+        ctrl[_CTRL_GEN] = self._gen  # release (after the step index and the actions)
+        deadline, spins = time.monotonic() + 60.0, 0
+        while int(done.min()) != self._gen:
+            spins += 1
+            if spins % 4096 == 0 and (time.monotonic() > deadline or
+                                      not all(p.is_alive() for p in self._procs)):
+                raise RuntimeError("host physics pool: a worker died or stalled")
+            time.sleep(0)
+
+    def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        self.v["ctrl"][_CTRL_STOP] = 1
+        for p in self._procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.terminate()
+        self.v = {}
+        for s in self._shms:
+            s.close()
+            s.unlink()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

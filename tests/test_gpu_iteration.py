@@ -195,3 +195,42 @@ def test_checkpoint_roundtrip(gpu, tmp_path):
     assert torch.equal(agent.packed(agent.flat_m), m_saved)
     sd = torch.load(tmp_path / "networks" / "3" / "networks.pth", weights_only=True)
     assert "actor.actor.first_layers.0.weight" in sd and "critic.network.last_layer.bias" in sd
+
+
+@pytest.mark.parametrize("prec,hidden", [("f32", (64, 64)), ("bf16", (256, 256))])
+def test_host_physics_pool_matches_device_env(gpu, prec, hidden):
+    """HostPhysicsVecEnvHelper (P=2 worker processes, page-locked shared memory, hipMemcpyAsync
+    on a side stream) drives two PPO iterations to the same rollout buffers, losses and
+    parameters, bit for bit, as the device-resident synthetic env on the same streams."""
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (HostPhysicsVecEnvHelper,
+                                                                SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    n, t, b = 96, 16, 512
+    streams = make_synthetic_streams(n, t, 17, seed=9, p_terminate=0.05)
+    res = []
+    for cls in (SyntheticVecEnvHelper, HostPhysicsVecEnvHelper):
+        run = make_run(num_envs=n, horizon=t, hidden=hidden, batch_size=b, epochs=2, rng="philox",
+                       seed=2, precision=prec)
+        torch.manual_seed(2)
+        agent = PPOEngineAgent(run, device=gpu)
+        kw = {"workers": 2} if cls is HostPhysicsVecEnvHelper else {}
+        helper = cls(streams, run, device=gpu, **kw)
+        algo = PPOEngine(helper, agent, log=lambda m: None)
+        snaps = []
+        for _ in range(2):
+            algo.iterate(verbose=False)
+            torch.cuda.synchronize()
+            buf = algo.buffer
+            snaps.append([x.cpu().clone() for x in (buf.states, buf.actions, buf.reward,
+                                                   buf.terminated, buf.values, buf.advantage,
+                                                   agent.packed_params())])
+        if cls is HostPhysicsVecEnvHelper:
+            helper.close()
+        res.append(snaps)
+    names = ("states", "actions", "reward", "terminated", "values", "advantage", "params")
+    for it, (d, h) in enumerate(zip(*res)):
+        for name, x, y in zip(names, d, h):
+            assert torch.equal(x, y), f"iteration {it}: {name} differs (host pool vs device env)"
