@@ -79,6 +79,10 @@ def load_traffic(path):
         return json.load(f).get("bytes_per_launch", {})
 
 
+# gymnasium observation / action sizes of the BASELINE configs (SURVEY.md s8 notation)
+_ENV_NAMES = {(17, 6): "HalfCheetah-v4", (27, 8): "Ant-v4", (376, 17): "Humanoid-v4"}
+
+
 def roofline(name, c, traffic, force_hbm=False):
     """Roofline of one kernel instantiation from its live event records.  The bound is the roof
     the kernel's own algorithmic work hits first: MFMA (FLOPs / dense peak of its dtype) or HBM
@@ -225,7 +229,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",
-            "config": {"workload": (f"HalfCheetah-v4 shapes: {n} envs/GPU x {t} steps, obs "
+            "config": {"workload": (f"{_ENV_NAMES.get((args.obs_dim, args.act_dim), 'custom')} "
+                                    f"shapes: {n} envs/GPU x {t} steps, obs "
                                     f"{args.obs_dim}, act {args.act_dim}, actor+critic "
                                     f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
                                     f"epochs x {n * t // args.batch} minibatches of {args.batch}"),

@@ -277,6 +277,53 @@ __global__ void obs_normalize_kernel(const double *__restrict__ window, float *_
   }
 }
 
+// Wide observations (O > 32, e.g. Humanoid-v4 O=376 with its six slices): one wave per (env, slot)
+// instead of one thread.  Each slice statistic is a lane-strided partial sum followed by a
+// fixed xor-tree across the wave (deterministic run to run); the f64 result differs from the
+// sequential loop only in summation order, i.e. it rounds to the same f32 state up to rare
+// ties (the 1-ulp bar of test_obs_window_and_normalize).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void obs_normalize_wide_kernel(
+    const double *__restrict__ window, float *__restrict__ state, int n, int o, int w,
+    SliceTable tab, int normalize) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (i >= static_cast<int64_t>(n) * w) return;  // wave-uniform
+  const int env = static_cast<int>(i / w);
+  const int slot = static_cast<int>(i % w);
+  const double *src = window + static_cast<int64_t>(env) * o * w + slot;  // feature f at f*w
+  float *dst = state + (static_cast<int64_t>(env) * w + slot) * o;
+  if (!normalize) {
+    for (int f = lane; f < o; f += 64) dst[f] = static_cast<float>(src[static_cast<int64_t>(f) * w]);
+    return;
+  }
+  for (int s = 0; s < tab.count; ++s) {
+    const int lo = tab.edge[s], hi = tab.edge[s + 1];
+    const int cnt = hi - lo;
+    if (cnt <= 0) continue;
+    double sum = 0.0;
+    for (int f = lo + lane; f < hi; f += 64) sum += src[static_cast<int64_t>(f) * w];
+    const double mean = wave_sum(sum) / cnt;
+    double csum = 0.0;
+    for (int f = lo + lane; f < hi; f += 64) csum += src[static_cast<int64_t>(f) * w] - mean;
+    const double cmean = wave_sum(csum) / cnt;
+    double ss = 0.0;
+    for (int f = lo + lane; f < hi; f += 64) {
+      const double d = (src[static_cast<int64_t>(f) * w] - mean) - cmean;
+      ss += d * d;
+    }
+    double sd = sqrt(wave_sum(ss) / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
+    if (sd == 0.0) sd = 1.0;
+    for (int f = lo + lane; f < hi; f += 64)
+      dst[f] = static_cast<float>((src[static_cast<int64_t>(f) * w] - mean) / sd);
+  }
+}
+
 // ============================================================================================
 // Synthetic VecEnv step (harness; oracle/ppo_ref.py RefSyntheticEnv)
 // ============================================================================================
@@ -599,9 +646,14 @@ extern "C" int ppo_obs_normalize(const double *window_d, float *state_d, int n, 
   }
   const int64_t total = static_cast<int64_t>(n) * w;
   FreeTimingScope timing_scope;
-  launch_k(TimRec{KC_OBS, "obs_normalize_kernel", 0.0, 12.0 * total * o}, obs_normalize_kernel,
-           dim3(ceil_div(total, 128)), dim3(128), 0, as_stream(stream), window_d, state_d, n, o,
-           w, tab, normalize);
+  if (o > 32)
+    launch_k(TimRec{KC_OBS, "obs_normalize_wide_kernel", 0.0, 12.0 * total * o},
+             obs_normalize_wide_kernel, dim3(ceil_div(total * 64, 256)), dim3(256), 0,
+             as_stream(stream), window_d, state_d, n, o, w, tab, normalize);
+  else
+    launch_k(TimRec{KC_OBS, "obs_normalize_kernel", 0.0, 12.0 * total * o}, obs_normalize_kernel,
+             dim3(ceil_div(total, 128)), dim3(128), 0, as_stream(stream), window_d, state_d, n, o,
+             w, tab, normalize);
   PPO_LAUNCHED();
   return 0;
 }

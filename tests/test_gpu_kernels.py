@@ -79,7 +79,7 @@ def test_normalize_rows(gpu, dtype):
 
 
 # ---------------------------------------------------------------------- observations (A1) + env
-@pytest.mark.parametrize("o,w", [(17, 1), (17, 3), (27, 2), (376, 1)])
+@pytest.mark.parametrize("o,w", [(17, 1), (17, 3), (27, 2), (376, 1), (376, 2)])
 def test_obs_window_and_normalize(gpu, o, w):
     E = _E()
     n = 50
