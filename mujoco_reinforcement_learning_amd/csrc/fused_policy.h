@@ -36,6 +36,7 @@ struct PolicyFusedArgs {
   const float *eps;
   uint64_t seed, offset;
   const uint64_t *offset_base;
+  uint64_t *stamps;              // diagnostics (ReLU only): (2, 128, 11) per-phase cycles, or null
   float *action, *logp, *value, *mean;
 };
 

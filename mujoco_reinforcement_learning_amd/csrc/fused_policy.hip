@@ -38,9 +38,16 @@ struct PolicyLds {
   static_assert(TOTAL <= 163840, "LDS budget");
 };
 
-template <int H, int ACT, int NH, bool ACTOR>
+template <int H, int ACT, int NH, bool ACTOR, bool STAMP = false>
 __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const FusedNet &N,
                                             char *lds) {
+  // STAMP (diagnostic build): wave 0 records s_memtime at each phase boundary
+  uint64_t tst[8];
+#define PSTAMP(k)                                      \
+  if constexpr (STAMP) {                               \
+    tst[k] = __builtin_amdgcn_s_memtime();             \
+  }
+  PSTAMP(0);
   using L = PolicyLds<H>;
   char *const ximg = lds + L::X;
   char *const a1img = lds + L::A1;
@@ -65,6 +72,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   if (tid < 8) hs[tid] = (tid < (ACTOR ? A : 1) && N.bh) ? N.bh[tid] : 0.f;
   if (ACTOR && tid >= 8 && tid < 16) hs[tid] = (tid - 8 < A) ? q.logstd[tid - 8] : 0.f;
 
+  PSTAMP(1);
   // the window / state writer: the actor's workgroups, or the critic's on a value-only call
   const bool writer = ACTOR || !q.do_actor;
   // ---- observe (A1): thread per env row, the A1 kernels' f64 loops ----
@@ -120,6 +128,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
+  PSTAMP(2);
   // states -> rollout buffer (writer workgroups; coalesced) and the bf16 X image
   if (writer) {
     for (int idx = tid; idx < R * O; idx += NT) {
@@ -133,6 +142,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
         pack2(xs[xr * kPolicyXsPitch + c2], xs[xr * kPolicyXsPitch + c2 + 1]);
   }
   __syncthreads();
+  PSTAMP(3);
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----
   bf16x8 ring[PD + 1];
@@ -167,6 +177,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
+  PSTAMP(4);
 
   // ---- L1 + head partial sums over the wave's 32 features (f32) ----
   {
@@ -176,6 +187,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, a1img, r, h, ring, a2);
+    PSTAMP(5);
     float zpart[2][NH];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -216,6 +228,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
+  PSTAMP(6);
 
   // ---- heads ----
   if constexpr (ACTOR) {
@@ -254,15 +267,26 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       q.value[env] = N.bh ? v + hs[0] : v;
     }
   }
+  PSTAMP(7);
+  if constexpr (STAMP) {
+    if (tid == 0 && blockIdx.x < 128) {
+      uint64_t *dst = q.stamps + (static_cast<int64_t>(blockIdx.y) * 128 + blockIdx.x) * 11;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) dst[k] = tst[k + 1] - tst[k];
+      dst[9] = tst[7] - tst[0];
+      dst[10] = tst[0];
+    }
+  }
+#undef PSTAMP
 }
 
-template <int H, int ACT, int NA>
+template <int H, int ACT, int NA, bool STAMP = false>
 __global__ __launch_bounds__(NT, 1) void policy_fused_kernel(PolicyFusedArgs q) {
   __shared__ __attribute__((aligned(16))) char lds[PolicyLds<H>::TOTAL];
   // y = 0 actor, y = 1 critic when both run; a single-net call launches one row of workgroups
   const bool actor = q.do_actor && blockIdx.y == 0;
-  if (actor) policy_body<H, ACT, NA, true>(q, q.net[0], lds);
-  else policy_body<H, ACT, 1, false>(q, q.net[1], lds);
+  if (actor) policy_body<H, ACT, NA, true, STAMP>(q, q.net[0], lds);
+  else policy_body<H, ACT, 1, false, STAMP>(q, q.net[1], lds);
 }
 
 int policy_fused_launch(const PolicyFusedArgs &q, const TimRec &rec, hipStream_t st) {
@@ -274,6 +298,12 @@ int policy_fused_launch(const PolicyFusedArgs &q, const TimRec &rec, hipStream_t
   const dim3 grid(ceil_div(q.n, R), (q.do_actor && q.do_critic) ? 2 : 1);
   auto go = [&](auto kernel) { launch_k(rec, kernel, grid, dim3(NT), 0, st, q); };
   const int na = q.act_dim <= 2 ? 2 : q.act_dim <= 4 ? 4 : q.act_dim <= 6 ? 6 : 8;
+  if (q.stamps) {  // diagnostic build: ReLU, padded head width 6 (HalfCheetah) only
+    PPO_REQUIRE(q.act == PPO_ACT_RELU && na == 6, "policy stamps: ReLU with A in (4, 6] only");
+    go(policy_fused_kernel<256, PPO_ACT_RELU, 6, true>);
+    PPO_LAUNCHED();
+    return 0;
+  }
   auto by_na = [&](auto act_tag) {
     constexpr int ACTV = decltype(act_tag)::value;
     if (na == 2) go(policy_fused_kernel<256, ACTV, 2>);

@@ -2044,6 +2044,8 @@ extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs
   q.seed = seed;
   q.offset = offset;
   q.offset_base = ctx->rng_counter;
+  q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
+  if (q.stamps) ctx->fstamp_g = 128;
   q.action = action_d;
   q.logp = logp_d;
   q.value = value_d;
