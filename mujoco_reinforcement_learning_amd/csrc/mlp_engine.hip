@@ -2058,7 +2058,7 @@ extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs
                      (eps_d ? 4.0 * A : 0.0) + (action_d ? 4.0 * A : 0.0) + (mean_d ? 4.0 * A : 0.0) +
                      (logp_d ? 4.0 : 0.0) + (value_d ? 4.0 : 0.0));
   const TimRec rec{KC_POLICY_HEAD,
-                   tim_active() ? intern_name("policy_fused_kernel<%d, %d, %d>", ctx->fused_hidden, q.act,
+                   tim_active() ? intern_name("policy_fused_kernel<%d, %d, %d, false>", ctx->fused_hidden, q.act,
                                              q.act_dim <= 2 ? 2 : q.act_dim <= 4 ? 4 : q.act_dim <= 6 ? 6 : 8)
                                 : nullptr,
                    fl, by};
