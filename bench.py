@@ -54,7 +54,7 @@ def parse():
                         "mode with the reference's f32 CPU trainer)")
     p.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     p.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    p.add_argument("--cpu-rollout-steps", type=int, default=32)
+    p.add_argument("--cpu-rollout-steps", type=int, default=128)
     p.add_argument("--cpu-epochs", type=int, default=1)
     p.add_argument("--no-timing", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--timing-iters", type=int, default=2,
@@ -63,6 +63,10 @@ def parse():
                    help="device: synthetic dynamics on the GPU (the measured default); host: the "
                         "same dynamics in a host worker pool with pinned async copies (PCIe-inclusive)")
     p.add_argument("--env-workers", type=int, default=8, help="host pool worker processes")
+    p.add_argument("--no-legs", action="store_true",
+                   help="skip the extra same-workload legs (f32 precision, host-pool env) that the "
+                        "default N=1 line carries next to `value`")
+    p.add_argument("--leg-steps", type=int, default=3, help="timed iterations per extra leg")
     p.add_argument("--no-graphs", action="store_true",
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -106,11 +110,22 @@ def roofline(name, c, traffic, force_hbm=False):
             "algorithmic_per_launch": (c["flops"] if mfma else c["bytes"]) / launches}
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, hidden):
     """Oracle on the host cores: rollout_steps of the T-step rollout, the full GAE, cpu_epochs of
     the E-epoch update; extrapolated linearly to one full iteration."""
     from oracle import ppo_ref as R
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = len(os.sched_getaffinity(0))  # every core this process may run on (SURVEY s8(d))
     torch.set_num_threads(threads)
     n, t = args.num_envs, args.horizon
     cfg = R.RefConfig(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
@@ -140,11 +155,76 @@ def cpu_baseline(args, hidden):
     t_epoch = (time.perf_counter() - t0) / args.cpu_epochs
     t_iter = t_roll + t_gae + t_epoch * args.epochs
     return {"value": n * t / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "torch": torch.__version__,
             "sample": (f"oracle/ppo_ref.py (torch {torch.__version__} CPU, {threads} threads): "
                        f"{k} of {t} rollout steps + full GAE + {args.cpu_epochs} of {args.epochs} "
                        f"epochs at N={n}, B={args.batch}, 2x{hidden[0]} MLP; extrapolated "
                        f"(rollout {t_roll:.2f}s, gae {t_gae:.3f}s, epoch {t_epoch:.2f}s/iter-scaled)"),
             "seconds_per_iteration": t_iter}
+
+
+def build(args, precision, env_kind, dev, rank):
+    """(run, agent, helper, algo) for one leg of the workload (BASELINE configs[1] shapes)."""
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    n, t = args.num_envs, args.horizon
+    run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
+                   hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
+                   seed=rank, precision=precision, rollout_graph=not args.no_graphs,
+                   train_graph=not args.no_graphs)
+    torch.manual_seed(0)  # identical initial parameters on every rank
+    agent = PPOEngineAgent(run, device=dev)
+    streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
+    if env_kind == "host":
+        from mujoco_reinforcement_learning_amd.environments import HostPhysicsVecEnvHelper
+        helper = HostPhysicsVecEnvHelper(streams, run, device=dev, workers=args.env_workers)
+    else:
+        helper = SyntheticVecEnvHelper(streams, run, device=dev)
+    algo = PPOEngine(helper, agent, log=lambda m: None)
+    return run, agent, helper, algo
+
+
+def time_iterations(algo, steps, warmup, world, dev) -> float:
+    """W untimed iterations, then K timed ones bracketed by barrier + synchronize; the max over
+    ranks of the wall time."""
+    for _ in range(warmup):
+        algo._iterate()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        algo._iterate()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt)
+    return elapsed
+
+
+def leg(args, precision, env_kind, dev) -> dict:
+    """One extra single-GPU leg of the same workload (not `value`): its env-steps/s."""
+    run, agent, helper, algo = build(args, precision, env_kind, dev, 0)
+    try:
+        elapsed = time_iterations(algo, args.leg_steps, 1, 1, dev)
+    finally:
+        if hasattr(helper, "close"):
+            helper.close()
+    n, t = args.num_envs, args.horizon
+    return {"value": n * t * args.leg_steps / elapsed, "unit": "env-steps/s",
+            "ms_per_step": 1000 * elapsed / args.leg_steps, "steps": args.leg_steps,
+            "warmup": 1, "precision": precision,
+            "env": ("device (synthetic dynamics on the GPU)" if env_kind == "device" else
+                    f"host pool ({args.env_workers} worker processes, page-locked shared memory, "
+                    "hipMemcpyAsync on a side stream: obs H2D + action D2H every step)")}
 
 
 def main():
@@ -168,45 +248,10 @@ def main():
         else:
             torch.distributed.init_process_group(backend)
 
-    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
-    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
-    from mujoco_reinforcement_learning_amd import engine as E
-    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
-                                                                make_synthetic_streams)
-    from mujoco_reinforcement_learning_amd.runconfig import make_run
-
     hidden = tuple(int(h) for h in args.hidden.split(","))
     n, t = args.num_envs, args.horizon
-    run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
-                   hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
-                   seed=rank, precision=args.precision, rollout_graph=not args.no_graphs,
-                   train_graph=not args.no_graphs)
-    torch.manual_seed(0)  # identical initial parameters on every rank
-    agent = PPOEngineAgent(run, device=dev)
-    streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
-    if args.env == "host":
-        from mujoco_reinforcement_learning_amd.environments import HostPhysicsVecEnvHelper
-        helper = HostPhysicsVecEnvHelper(streams, run, device=dev, workers=args.env_workers)
-    else:
-        helper = SyntheticVecEnvHelper(streams, run, device=dev)
-    algo = PPOEngine(helper, agent, log=lambda m: None)
-
-    for _ in range(args.warmup):
-        algo._iterate()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        algo._iterate()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt)
+    run, agent, helper, algo = build(args, args.precision, args.env, dev, rank)
+    elapsed = time_iterations(algo, args.steps, args.warmup, world, dev)
     classes, kernels = {}, {}
     if not args.no_timing:
         # Per-kernel durations: HIP event pairs on each dispatch packet, over --timing-iters
@@ -253,6 +298,15 @@ def main():
                                               if v["launches"]}
         line["kernels_ms_per_step"] = {k: round(v["ms"] / ti, 4) for k, v in
                                        sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
+    if world == 1 and not args.no_legs:
+        del algo, agent
+        torch.cuda.empty_cache()
+        if args.precision != "f32":
+            # the reference's precision on the same workload (f32 parity mode)
+            line["f32_leg"] = leg(args, "f32", args.env, dev)
+        if args.env != "host":
+            # s8(d)'s t_iter includes the per-step obs H2D and action D2H: the host-pool env
+            line["pcie_inclusive_leg"] = leg(args, args.precision, "host", dev)
     if rank == 0 and world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, hidden)
     if rank == 0:

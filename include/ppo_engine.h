@@ -79,7 +79,7 @@ int ppo_param_offsets(const ppo_ctx *ctx, int64_t *offsets, int max_tensors);
 int ppo_bind_params(ppo_ctx *ctx, float *params_d);
 
 /* ---- A1: observation window + per-sample standardisation -------------------------------------
- * replaces EnvironmentHelper.step's window shift (running_gym_sequential_vectorized.py:120-125,
+ * replaces EnvironmentHelper.step's window shift (running_gym_sequential_vectorized.py:53-58,
  * helper.py:51-57) and get_state/normalize_state/_normalize (:61-92).
  * window_d: (N, O, W) f64, the reference's timestep.observation.  obs_d: (N, O) new observation
  * (f64 if obs_is_f64 else f32).  reset_d (nullable): u8 per env; 1 -> all W slots := obs
@@ -104,7 +104,7 @@ int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_
                     void *stream);
 /* Fused observe + act (A1-A4 in one launch in precision bf16 with the fused shapes; otherwise the
  * A1 kernels followed by ppo_policy_step): replaces EnvironmentHelper.step's window push
- * (running_gym_sequential_vectorized.py:120-125), get_state (:61-92) and PPOAgent.act /
+ * (running_gym_sequential_vectorized.py:53-58), get_state (:61-92) and PPOAgent.act /
  * get_state_value (ppo.py:22-26, ppo_agent.py:24-43) for one rollout step.
  * window_d (N, O, W) f64 is pushed with obs_d (N, O) f64 when obs_d != NULL (reset_d / all_reset as
  * ppo_obs_window_push), standardised as ppo_obs_normalize into state_d (N, W*O) f32, then the
@@ -287,6 +287,19 @@ int ppo_synthetic_env_step(const float *base_obs_d, const float *base_reward_d,
                            double *obs_out_d, double *reward_out_d, uint8_t *term_out_d,
                            void *stream);
 int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, int64_t n, void *stream);
+/* One step of the single evaluation env of Algorithm.test (base_algorithm.py:21-48) on the same
+ * synthetic streams (env 0, base arrays (T+1, N, O) / (T, N) / (T, N)), with the reference's
+ * host branch (:33-37) taken on the device: *step_d = k (device int32, zeroed by the test reset);
+ * terminated -> window (O, W) f64 := base_obs[0, 0] in every slot (reset_environment(test),
+ * helper.py:59-64) and k := 0; else shift + append base_obs[(k+1)%(T+1), 0] + 0.1 a[o % A]
+ * (helper.py:51-57, :36-37) and k := k+1.  *reward_sum_d += base_reward[k%T, 0] - 0.01 sum a^2
+ * (f64, the sequential sum(rewards) of :38,48); *term_out_d = terminated.  action_d: (A,) f32,
+ * the flattened test-phase mean (agent.py:35-38). */
+int ppo_synthetic_test_step(const float *base_obs_d, const float *base_reward_d,
+                            const uint8_t *base_term_d, int t_len, int n_envs,
+                            const float *action_d, int o, int a, int w, double *window_d,
+                            int32_t *step_d, double *reward_sum_d, uint8_t *term_out_d,
+                            void *stream);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,9 @@ _SIGNATURES = {
     "ppo_synthetic_env_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_philox_normal": (c_int, [c_uint64, c_uint64, c_void_p, c_int64, c_void_p]),
+    "ppo_synthetic_test_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                        c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
     "ppo_ctx_set_rng_counter": (c_int, [c_void_p, c_void_p]),
     "ppo_ctx_set_precision": (c_int, [c_void_p, c_int]),
     "ppo_ctx_timing": (c_int, [c_void_p, c_int, c_int]),

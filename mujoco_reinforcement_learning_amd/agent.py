@@ -18,6 +18,7 @@ from .features import Run
 from .models import EngineActor, EngineCritic, move_to_flat
 
 _ACT_NAMES = {nn.ReLU: "relu", nn.Tanh: "tanh", nn.ELU: "elu"}
+REFERENCE_CRITIC_HIDDEN = (128, 128)  # models/critic.py:14
 
 
 class FlatAdam:
@@ -138,7 +139,8 @@ class PPOEngineAgent:
         if act_cls not in _ACT_NAMES:
             raise ValueError(f"activation {act_cls} not supported by the engine (ReLU/Tanh/ELU)")
         hidden = list(nc.linear_hidden_shapes)[:nc.num_linear_layers]
-        critic_hidden = run.engine_config.critic_hidden_shapes or hidden
+        # models/critic.py:10-15 hard-codes [128, 128]; engine_config may widen it
+        critic_hidden = list(run.engine_config.critic_hidden_shapes or REFERENCE_CRITIC_HIDDEN)
         in_dim = nc.input_shape * ec.window_length
         self.networks = nn.ModuleDict()
         # PPOAgent.initialize_networks builds the actor first, then the critic (RNG order)

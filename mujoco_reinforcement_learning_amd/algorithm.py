@@ -73,9 +73,21 @@ class PPOEngine:
                 lo, hi = self.dp.my_shard(n)
                 eps = torch.randn(self.dp.global_envs(n), a)[lo:hi]
             else:
-                eps = torch.randn(n, a)
+                eps = torch.randn(n, a, generator=self._local_gen())
             return eps.to(self.agent.device, non_blocking=True), 0
         return None, None
+
+    def _local_gen(self):
+        """Generator for the torch-RNG draws: the global CPU generator (the reference's stream)
+        except in local data-parallel mode, where every rank starts from the same seeded
+        parameters and would otherwise draw identical noise and row orders on every env shard;
+        there each rank forks its own generator keyed by (seed, rank)."""
+        if not (self.dp.active and self.dp.mode == "local"):
+            return None
+        if getattr(self, "_rank_gen", None) is None:
+            self._rank_gen = torch.Generator().manual_seed(
+                self._seed() * 1_000_003 + 7919 * (self.dp.rank + 1))
+        return self._rank_gen
 
     # ---- ppo.py:13-60 ----------------------------------------------------------------------
     def _graph_ok(self) -> bool:
@@ -221,7 +233,13 @@ class PPOEngine:
         sched = agent.adam_schedule(steps)
         if sched is None:
             return None
-        key = (b, epochs, batches)
+        beta1, beta2 = agent.optimizers["actor"].param_groups[0]["betas"]
+        eps = agent.optimizers["actor"].param_groups[0]["eps"]
+        ppo = self.run.ppo_config
+        # every scalar the captured graph bakes in (the step sizes live in the device schedule)
+        key = (b, epochs, batches, float(clip_lo), float(clip_hi), float(ppo.entropy_eps),
+               float(inv_b), float(inv_ba), float(beta1), float(beta2), float(eps), eng.fused,
+               eng.precision)
         if getattr(self, "_tg_key", None) != key:
             self._tg_key = key
             self._tg_rows = torch.empty(epochs, batches * b, dtype=torch.int32, device=dev)
@@ -232,9 +250,6 @@ class PPOEngine:
             E.feistel_rows(self._seed() + 7919 * self.dp.rank, self.iteration * epochs + epoch, 0,
                            batches * b, n, t_len, self._tg_rows[epoch])
         self._tg_sched.copy_(sched, non_blocking=True)
-        beta1, beta2 = agent.optimizers["actor"].param_groups[0]["betas"]
-        eps = agent.optimizers["actor"].param_groups[0]["eps"]
-        ppo = self.run.ppo_config
 
         staged = eng.fused
         if staged:
@@ -337,7 +352,9 @@ class PPOEngine:
         current = False  # bf16 weight images refreshed by the last optimizer step
         for epoch in range(epochs):
             if self._rng() == "torch":
-                perm = torch.randperm((n_glob if exact else n) * t_len).to(dev, non_blocking=True)
+                gen = None if exact else self._local_gen()
+                perm = torch.randperm((n_glob if exact else n) * t_len,
+                                      generator=gen).to(dev, non_blocking=True)
             for i in range(batches_per_epoch):
                 count = None
                 if exact:
@@ -346,7 +363,7 @@ class PPOEngine:
                                    shard=self.dp.my_shard(n), count=self._count)
                     count = self._count
                 elif self._rng() == "torch":
-                    torch.randn(b, a)  # ppo.py:110
+                    torch.randn(b, a, generator=gen)  # ppo.py:110
                     E.perm_to_rows(perm, i * b, b, n, t_len, self._rows)
                 else:
                     E.feistel_rows(self._seed() + 7919 * self.dp.rank,
@@ -376,6 +393,48 @@ class PPOEngine:
         actor_loss = float(epoch_means[:, 0].mean())
         critic_loss = float(epoch_means[:, 1].mean())
         self.last_losses = (actor_loss, critic_loss)
+
+    # ---- base_algorithm.py:21-48: deterministic evaluation rollout ----------------------------
+    @torch.no_grad()
+    def test(self, visualize: bool = False, steps: int = 1000) -> float:
+        """Algorithm.test: ``steps`` single-env steps with the mean action
+        (agent.act(test_phase=True), flattened to (A,) as agent.py:35-38), reset on termination,
+        window shift otherwise; returns sum(rewards) / len(rewards).
+
+        Device-resident helpers (``test_step``) take the termination branch on the device and
+        keep the f64 reward sum there, so the loop never synchronises the host until the final
+        read; other helpers get the reference's host protocol (test_environment.step + branch).
+        ``visualize`` is accepted for signature compatibility; rendering is out of scope."""
+        helper, agent = self.environment_helper, self.agent
+        agent.networks.eval()
+        helper.reset_environment(test_phase=True)
+        next_state = helper.get_state(test_phase=True)
+        if hasattr(helper, "test_step"):
+            reward_sum = torch.zeros(1, dtype=torch.float64, device=agent.device)
+            for _ in range(steps):
+                current_state = next_state  # get_state returns a fresh tensor (torch.clone, :29)
+                action, _ = agent.act(current_state, return_dist=True, test_phase=True)
+                helper.test_step(action.reshape(-1), reward_sum)
+                next_state = helper.get_state(test_phase=True)
+            mean_reward = float(reward_sum) / steps
+        else:
+            rewards = []
+            ts = helper.test_timestep
+            for _ in range(steps):
+                current_state = torch.clone(next_state)
+                action, _ = agent.act(current_state, return_dist=True, test_phase=True)
+                last_obs, reward, ts.terminated, ts.truncated, _ = helper.test_environment.step(
+                    action.reshape(-1).cpu().numpy())
+                if ts.terminated:
+                    helper.reset_environment(test_phase=True)
+                else:
+                    helper.shift_observations(test_phase=True, environment_index=-1)
+                    ts.observation[:, -1] = torch.as_tensor(last_obs)
+                rewards.append(reward)
+                next_state = helper.get_state(test_phase=True)
+            mean_reward = sum(rewards) / len(rewards)
+        agent.networks.train()
+        return mean_reward
 
     # ---- ppo.py:156-159, base_algorithm.py:53-58 ----------------------------------------------
     def _iterate(self):

@@ -1,6 +1,6 @@
 // Fused rollout policy step for precision mode bf16 (SURVEY.md s8(a) A1-A4 in one launch):
 // observation-window push + per-sample standardisation (running_gym_sequential_vectorized.py:
-// 61-92, 120-125), actor and critic forward (network_block_creator.py:74-86, linear/actor.py:
+// 53-58, 61-92), actor and critic forward (network_block_creator.py:74-86, linear/actor.py:
 // 25-30, critic.py:22-25), Normal sampling and log-prob (ppo_agent.py:27-43, ppo.py:22-26).
 //
 // grid = (ceil(N / 64), nets): blockIdx.y is the net (0 actor, 1 critic), one workgroup = 64

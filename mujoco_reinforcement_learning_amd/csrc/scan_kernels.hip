@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64) void normalize_rows_kernel(T *__restrict__ x, i
 }
 
 // ============================================================================================
-// Observation window (helper.py:51-64, running_gym_sequential_vectorized.py:120-125)
+// Observation window (helper.py:51-64, running_gym_sequential_vectorized.py:53-58)
 // ============================================================================================
 template <typename OT>
 __global__ void obs_window_push_kernel(double *__restrict__ window, const OT *__restrict__ obs,
@@ -348,6 +348,48 @@ __global__ void synthetic_env_step_kernel(const float *__restrict__ base_obs,
     }
     reward_out[env] = static_cast<double>(base_reward[env]) - 0.01 * ctrl;
     term_out[env] = base_term[env];
+  }
+}
+
+// One step of the single test environment inside Algorithm.test (base_algorithm.py:21-48), with
+// the host branch of :33-37 taken on the device: the step counter k lives in device memory, so
+// the 1000-step evaluation loop never synchronises the host.  One block; thread f handles
+// feature f.  Dynamics = env 0 of the synthetic streams at k (RefSyntheticEnv.test_step):
+//   obs' = base_obs[(k+1) % (T+1), 0] + 0.1 a[f % A],  r = base_reward[k % T, 0] - 0.01 sum a^2,
+//   terminated = base_term[k % T, 0];  terminated -> reset_environment(test): every window slot
+//   := base_obs[0, 0] and k := 0 (helper.py:59-64); else shift + append (helper.py:51-57) and
+//   k := k + 1.  rewards.append(r) (:38) is a sequential f64 running sum.
+__global__ __launch_bounds__(256) void synthetic_test_step_kernel(
+    const float *__restrict__ base_obs, const float *__restrict__ base_reward,
+    const uint8_t *__restrict__ base_term, int t_len, int n_envs, const float *__restrict__ action,
+    int o, int a, int w, double *__restrict__ window, int32_t *__restrict__ step,
+    double *__restrict__ reward_sum, uint8_t *__restrict__ term_out) {
+  const int k = *step;
+  const int kt = k % t_len;
+  const bool term = base_term[static_cast<int64_t>(kt) * n_envs] != 0;
+  const float *nxt = base_obs + static_cast<int64_t>((k + 1) % (t_len + 1)) * n_envs * o;
+  for (int f = threadIdx.x; f < o; f += blockDim.x) {
+    double *row = window + static_cast<int64_t>(f) * w;
+    if (term) {
+      const double x0 = static_cast<double>(base_obs[f]);
+      for (int s = 0; s < w; ++s) row[s] = x0;
+    } else {
+      const double x = static_cast<double>(nxt[f]) + 0.1 * static_cast<double>(action[f % a]);
+      for (int s = 0; s + 1 < w; ++s) row[s] = row[s + 1];
+      row[w - 1] = x;
+    }
+  }
+  __syncthreads();  // every thread has read *step
+  if (threadIdx.x == 0) {
+    double ctrl = 0.0;
+    for (int j = 0; j < a; ++j) {
+      const double aj = static_cast<double>(action[j]);
+      ctrl = ctrl + aj * aj;
+    }
+    const double r = static_cast<double>(base_reward[static_cast<int64_t>(kt) * n_envs]) - 0.01 * ctrl;
+    *reward_sum = *reward_sum + r;
+    *term_out = term ? 1 : 0;
+    *step = term ? 0 : k + 1;
   }
 }
 
@@ -672,6 +714,24 @@ extern "C" int ppo_synthetic_env_step(const float *base_obs_d, const float *base
            synthetic_env_step_kernel, dim3(ceil_div(total, 256)), dim3(256), 0,
            as_stream(stream), base_obs_d, base_reward_d, base_term_d, action_d, n, o, a,
            obs_out_d, reward_out_d, term_out_d);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_synthetic_test_step(const float *base_obs_d, const float *base_reward_d,
+                                       const uint8_t *base_term_d, int t_len, int n_envs,
+                                       const float *action_d, int o, int a, int w,
+                                       double *window_d, int32_t *step_d, double *reward_sum_d,
+                                       uint8_t *term_out_d, void *stream) {
+  PPO_REQUIRE(base_obs_d && base_reward_d && base_term_d && action_d && window_d && step_d &&
+                  reward_sum_d && term_out_d && t_len > 0 && n_envs > 0 && o > 0 && a > 0 &&
+                  w > 0,
+              "ppo_synthetic_test_step: bad args");
+  FreeTimingScope timing_scope;
+  launch_k(TimRec{KC_ENV, "synthetic_test_step_kernel", 0.0, 4.0 * o + 8.0 * o * (2 * w - 1)},
+           synthetic_test_step_kernel, dim3(1), dim3(256), 0, as_stream(stream), base_obs_d,
+           base_reward_d, base_term_d, t_len, n_envs, action_d, o, a, w, window_d, step_d,
+           reward_sum_d, term_out_d);
   PPO_LAUNCHED();
   return 0;
 }

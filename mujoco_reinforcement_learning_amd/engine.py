@@ -449,6 +449,30 @@ def synthetic_env_step(base_obs, base_reward, base_term, action, obs_out, reward
                                      _stream(dev)))
 
 
+def synthetic_test_step(base_obs, base_reward, base_term, action, window, step, reward_sum,
+                        term_out) -> None:
+    """One step of the evaluation env (ppo_synthetic_test_step): env 0 of the synthetic streams,
+    window (O, W) f64 updated in place, the device step counter / reward sum / terminated flag
+    advanced without a host synchronisation."""
+    lib = _lib.load()
+    t1, n, o = base_obs.shape
+    dev = base_obs.device
+    _need(base_obs, "base_obs", torch.float32)
+    _need(base_reward, "base_reward", torch.float32, (t1 - 1, n), dev)
+    _need(base_term, "base_term", None, (t1 - 1, n), dev)
+    _need(action, "action", torch.float32, device=dev)
+    _need(window, "window", torch.float64, device=dev)
+    if window.numel() % o or window.shape[-2] != o:
+        raise RuntimeError(f"window has shape {tuple(window.shape)}, expected (..., O={o}, W)")
+    _need(step, "step", torch.int32, (1,), dev)
+    _need(reward_sum, "reward_sum", torch.float64, (1,), dev)
+    _need(term_out, "term_out", None, (1,), dev)
+    check(lib.ppo_synthetic_test_step(ptr(base_obs), ptr(base_reward), ptr(base_term), t1 - 1, n,
+                                      ptr(action), o, action.numel(), window.shape[-1],
+                                      ptr(window), ptr(step), ptr(reward_sum), ptr(term_out),
+                                      _stream(dev)))
+
+
 def philox_normal(seed: int, offset: int, out: torch.Tensor) -> None:
     lib = _lib.load()
     _need(out, "out", torch.float32)

@@ -89,6 +89,7 @@ class SyntheticVecEnvHelper:
         self.environment = SimpleNamespace(num_envs=n)
         self.test_environment = SimpleNamespace(num_envs=1)
         self._obs_next = torch.empty(n, o, **f64)
+        self._test_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.t = 0
 
     # ---- EnvironmentHelper API -------------------------------------------------------------
@@ -99,12 +100,14 @@ class SyntheticVecEnvHelper:
         self.images = []
 
     def reset_environment(self, test_phase: bool):
-        """helper.py:59-64 + running_gym_sequential_vectorized.py:161-167."""
+        """helper.py:59-67 + running_gym_sequential_vectorized.py:94-100.  The test env (env 0 of
+        the streams) restarts at stream step 0 with every window slot = base_obs[0, 0]."""
         if test_phase:
             E.obs_window_push(self.test_timestep.observation, self.base_obs[0, :1].contiguous(),
                               all_reset=True)
             self.test_timestep.terminated.zero_()
             self.test_timestep.truncated.zero_()
+            self._test_step.zero_()
             return
         self.t = 0
         E.obs_window_push(self.timestep.observation, self.base_obs[0], all_reset=True)
@@ -113,7 +116,8 @@ class SyntheticVecEnvHelper:
 
     def step(self, action: torch.Tensor, reward_out: Optional[torch.Tensor] = None,
              terminated_out: Optional[torch.Tensor] = None):
-        """Training-phase step of all N envs (running_gym_sequential_vectorized.py:107-126).
+        """Training-phase step of all N envs (running_gym_sequential_vectorized.py:40-59, the window
+        update of :53-58 / helper.py:51-57).
         ``reward_out`` / ``terminated_out`` let the engine land the outputs straight in its
         rollout buffer."""
         t = self.t
@@ -144,13 +148,24 @@ class SyntheticVecEnvHelper:
         return self._obs_next
 
     def get_state(self, test_phase: bool = False, out: Optional[torch.Tensor] = None):
-        """(N, W, O) ``Run.dtype`` state (running_gym_sequential_vectorized.py:150-159)."""
+        """(N, W, O) ``Run.dtype`` state (running_gym_sequential_vectorized.py:83-92)."""
         ts = self.test_timestep if test_phase else self.timestep
         n, o, w = ts.observation.shape
         if out is None:
             out = torch.empty(n, w, o, dtype=torch.float32, device=self.device)
         E.obs_normalize(ts.observation, out, normalize=self.run.normalize_observations)
         return out.view(n, w, o)
+
+    def test_step(self, action: torch.Tensor, reward_sum: torch.Tensor) -> None:
+        """One step of the evaluation env inside Algorithm.test (base_algorithm.py:30-39):
+        test_environment.step(action.reshape(-1)), then reset_environment(test) on termination or
+        shift + append otherwise, and rewards.append -- as one device launch
+        (ppo_synthetic_test_step), the termination branch taken on the device.  ``reward_sum``
+        (1,) f64 accumulates the rewards in order."""
+        ts = self.test_timestep
+        E.synthetic_test_step(self.base_obs, self.base_reward, self.base_terminated,
+                              action.reshape(-1).contiguous(), ts.observation[0], self._test_step,
+                              reward_sum, ts.terminated)
 
     def shift_observations(self, test_phase: bool, environment_index: int):
         ts = self.test_timestep if test_phase else self.timestep

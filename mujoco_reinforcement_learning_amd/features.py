@@ -114,6 +114,9 @@ class SACConfig:
     automatic_entropy_tuning: bool
 
 
+ENGINE_CONFIG_FILE = "engine_configuration.json"
+
+
 @dataclass
 class EngineConfig:
     """Engine-only knobs (not in the reference; defaults reproduce the reference behaviour).
@@ -121,8 +124,10 @@ class EngineConfig:
     rng: "torch" draws sampling noise and minibatch permutations from the torch global CPU
          generator in the reference order (bit-for-bit the same draws as ppo.py); "philox" uses
          counter-based Philox normals and a keyed Feistel permutation on the GPU (no host RNG).
-    critic_hidden_shapes: hidden widths of the MLP critic; None = the actor's
-         ``linear_hidden_shapes`` (the reference critic.py hard-codes [128, 128]).
+    critic_hidden_shapes: hidden widths of the MLP critic; None = the reference critic's
+         hard-coded [128, 128] (models/critic.py:10-15), so a drop-in run builds the same critic
+         and its networks.pth / optimizer_critic.pth load into the reference's modules.  The
+         BASELINE configs ("actor+critic 2x256") set it explicitly (runconfig.make_run).
     seed: key of the philox streams.
     dp_mode: "local" (weak scaling: per-rank shuffles, loss / (B*world)) or "exact" (global
          reference permutation sharded across ranks, loss / B) -- distributed.py.
@@ -182,13 +187,19 @@ class Run(metaclass=Singleton):
         Singleton._instances.pop(Run, None)
 
     def save(self):
+        """features.py:134-143: configurations.json in the reference's exact schema (its
+        get_configurations restores Run positionally, so an extra key would break a reference
+        resume); the engine-only knobs go to engine_configuration.json beside it."""
         cfg = {"run": asdict(self)}
+        engine = cfg["run"].pop("engine_config")
         cfg["run"]["dtype"] = str(cfg["run"]["dtype"]).split(".")[-1]
         cfg["run"]["network_config"]["activation_class"] = (
             self.network_config.activation_class.__name__)
         os.makedirs(self.experiment_path, exist_ok=True)
         with open(f"{self.experiment_path}/configurations.json", "w") as fh:
             fh.write(json.dumps(cfg, indent=4))
+        with open(f"{self.experiment_path}/{ENGINE_CONFIG_FILE}", "w") as fh:
+            fh.write(json.dumps(engine, indent=4))
 
     @staticmethod
     def get_configurations(experiment_path: str) -> "Run":
@@ -207,6 +218,11 @@ class Run(metaclass=Singleton):
             NetworkConfig(*cfg.pop("network_config").values()),
             DynamicConfig(*cfg.pop("dynamic_config").values()),
         ]
-        engine = EngineConfig(**cfg.pop("engine_config", {}))
+        engine_kw = cfg.pop("engine_config", None)
+        side = f"{experiment_path}/{ENGINE_CONFIG_FILE}"
+        if engine_kw is None and os.path.exists(side):
+            with open(side) as fh:
+                engine_kw = json.load(fh)
+        engine = EngineConfig(**(engine_kw or {}))  # a reference run dir: engine defaults
         Run.reset_instance()
         return Run(*parts, *cfg.values(), engine_config=engine)

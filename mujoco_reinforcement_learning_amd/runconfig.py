@@ -24,7 +24,15 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
              experiment_path: str = "/tmp/ppo_engine_run",
              replace: bool = True) -> Run:
     """Defaults: the headline HalfCheetah config (BASELINE.json configs[1]) with main.py's PPO
-    hyper-parameters (lr 1e-4, gamma 0.99, lambda 0.98, clip 0.1, entropy 1e-4, E=10)."""
+    hyper-parameters (lr 1e-4, gamma 0.99, lambda 0.98, clip 0.1, entropy 1e-4, E=10).
+
+    critic_hidden: None -> the actor's widths (the BASELINE configs name one MLP shape for actor
+    and critic); pass "reference" for the reference critic's hard-coded [128, 128]
+    (models/critic.py:14, main.py's network)."""
+    if critic_hidden is None:
+        critic_hidden = hidden
+    elif critic_hidden == "reference":
+        critic_hidden = (128, 128)
     if replace:
         Run.reset_instance()
     return Run(RewardConfig(),
@@ -50,8 +58,8 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
                normalize_observations=normalize_observations, sequence_wise_normalization=False,
                dtype=torch.float32, render_size=[200, 200],
                engine_config=EngineConfig(rng=rng,
-                                          critic_hidden_shapes=list(critic_hidden)
-                                          if critic_hidden else None, seed=seed,
+                                          critic_hidden_shapes=[int(h) for h in critic_hidden],
+                                          seed=seed,
                                           dp_mode=dp_mode, rollout_graph=rollout_graph,
                                           train_graph=train_graph,
                                           precision=precision))

@@ -221,7 +221,7 @@ class RefSyntheticEnv:
     synthetic dynamics whose next observation depends on the action, keeping the T rollout steps
     sequential:  obs' = base_obs[t+1] + 0.1 * a[:, o % A];  r = base_reward[t] - 0.01 * sum_a a^2
     (f64, sequential in a);  terminated = base_terminated[t].  The observation window follows
-    EnvironmentHelper semantics (helper.py:51-67, running_gym_sequential_vectorized.py:107-126).
+    EnvironmentHelper semantics (helper.py:51-67, running_gym_sequential_vectorized.py:40-59).
     """
 
     def __init__(self, base_obs: torch.Tensor, base_reward: torch.Tensor,
@@ -257,7 +257,7 @@ class RefSyntheticEnv:
         self.reward = self.base_reward[t].double() - 0.01 * ctrl
         self.terminated = self.base_terminated[t].clone()
         self.truncated = torch.zeros(n, dtype=torch.bool)
-        # running_gym_sequential_vectorized.py:120-125
+        # running_gym_sequential_vectorized.py:53-58
         term = self.terminated
         shifted = torch.cat([self.window[:, :, 1:], nxt[..., None]], dim=2)
         full = nxt[..., None].repeat(1, 1, self.W)
@@ -266,6 +266,37 @@ class RefSyntheticEnv:
 
     def get_state(self, normalize: bool):
         return get_state(self.window, normalize)
+
+    # ---- the single evaluation env of Algorithm.test (base_algorithm.py:21-48): env 0 of the
+    # streams, restarted at stream step 0 by every test reset --------------------------------
+    def test_reset(self):
+        """helper.py:59-67 with test_phase=True: window (1, O, W) := the reset observation."""
+        self.test_t = 0
+        self.test_window = self.base_obs[0, :1].double()[..., None].repeat(1, 1, self.W)
+
+    def test_reset_window(self):
+        """reset_environment(test_phase=True) after a termination (base_algorithm.py:33-34)."""
+        self.test_reset()
+
+    def test_env_step(self, action: torch.Tensor):
+        """test_environment.step(action (A,)) -> (observation, reward, terminated, truncated,
+        info) with the synthetic dynamics at stream step k."""
+        k = self.test_t
+        t_len = self.base_reward.shape[0]
+        a = action.double()
+        o = self.base_obs.shape[2]
+        obs = self.base_obs[(k + 1) % (t_len + 1), 0].double() + 0.1 * a[torch.arange(o) % self.A]
+        ctrl = 0.0
+        for j in range(self.A):
+            ctrl = ctrl + float(a[j]) * float(a[j])
+        reward = float(self.base_reward[k % t_len, 0]) - 0.01 * ctrl
+        terminated = bool(self.base_terminated[k % t_len, 0])
+        self.test_t = k + 1
+        return obs, reward, terminated, False, {}
+
+    def test_get_state(self, normalize: bool):
+        """running_gym_sequential_vectorized.py:83-92 with test_phase=True."""
+        return get_state(self.test_window, normalize)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -418,6 +449,29 @@ def iterate(env: RefSyntheticEnv, agent: RefAgent, current_episode: int = 0):
     calculate_advantages(memory, agent.cfg)
     losses = train(agent, memory, current_episode)
     return memory, losses
+
+
+@torch.no_grad()
+def test(env: RefSyntheticEnv, agent: RefAgent, steps: int = 1000) -> float:
+    """base_algorithm.py:21-48 (Algorithm.test, visualize=False): deterministic mean-action
+    rollout of the single test env, reset on termination, window shift + append otherwise."""
+    cfg = agent.cfg
+    rewards = []
+    env.test_reset()
+    next_state = env.test_get_state(cfg.normalize_observations)
+    for _ in range(steps):
+        current_state = torch.clone(next_state)
+        action, _ = agent.act(current_state, return_dist=True, test_phase=True)
+        last_observation, reward, terminated, _, _ = env.test_env_step(action.reshape(-1))
+        if terminated:
+            env.test_reset_window()
+        else:
+            # helper.py:51-57 (test_phase) then observation[:, -1] = last_observation
+            env.test_window[..., :-1] = env.test_window[..., 1:].clone()
+            env.test_window[0, :, -1] = last_observation
+        rewards.append(reward)
+        next_state = env.test_get_state(cfg.normalize_observations)
+    return sum(rewards) / len(rewards)
 
 
 def flat_params(agent: RefAgent) -> torch.Tensor:

@@ -7,11 +7,19 @@ Run here (the container that has /root/reference), never on the GPU box:
 It imports ``models.linear.actor.Actor`` and ``models.network_block_creator.create_network`` from
 /root/reference/src (both import cleanly with torch only -- SURVEY.md s8(c)), builds them under
 fixed ``torch.manual_seed`` values in the PPOAgent order (actor, then critic:
-ppo_agent.py:12-14), and records every parameter plus the forward outputs on a fixed input.  The
-critic is the reference ``NetworkBlock`` with ``output_shape=1`` and the window flattened (the
-coherent MLP critic of SURVEY.md s0 / s8(b)).  Only data (inputs and expected outputs) is written:
-no reference source travels.
+ppo_agent.py:12-14), and records, per case:
+  meta        [seed, obs, window, act, n_actor_hidden, n_critic_hidden, *actor, *critic]
+  activation  the activation name ("relu" / "tanh" / "elu")
+  x           a fixed (32, W, O) input
+  mean / std / value   the reference forward outputs on x
+  sha256/<state_dict key>   digest of every parameter's bytes (the init pin)
+  <state_dict key>          the parameter itself, for the small nets only (< 200 k values)
+The critic is the reference ``NetworkBlock`` with ``output_shape=1`` and the window flattened (the
+coherent MLP critic of SURVEY.md s0 / s8(b)); its widths are the reference critic's hard-coded
+[128, 128] (models/critic.py:14) for main.py's network, the actor's widths for the BASELINE
+configs.  Only data (inputs, expected outputs, digests) is written: no reference source travels.
 """
+import hashlib
 import os
 import sys
 
@@ -20,13 +28,20 @@ import torch
 
 REF_SRC = "/root/reference/src"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_mlp.npz")
+FULL_PARAMS_LIMIT = 200_000
 
 CASES = [
-    # name, seed, obs, window, act, hidden, activation
-    ("relu_2x64", 0, 17, 1, 6, [64, 64], "ReLU"),
-    ("tanh_2x64_w2", 1, 17, 2, 6, [64, 64], "Tanh"),
-    ("elu_2x32_ant", 2, 27, 1, 8, [32, 32], "ELU"),
-    ("relu_2x256", 3, 17, 1, 6, [256, 256], "ReLU"),
+    # name, seed, obs, window, act, actor hidden, critic hidden, activation
+    ("relu_2x64", 0, 17, 1, 6, [64, 64], [64, 64], "ReLU"),
+    ("tanh_2x64_w2", 1, 17, 2, 6, [64, 64], [64, 64], "Tanh"),
+    ("elu_2x32_ant", 2, 27, 1, 8, [32, 32], [32, 32], "ELU"),
+    ("relu_2x256", 3, 17, 1, 6, [256, 256], [256, 256], "ReLU"),
+    # BASELINE configs[2] Ant-v4 and configs[3] Humanoid-v4 shapes
+    ("ant_relu_2x256", 6, 27, 1, 8, [256, 256], [256, 256], "ReLU"),
+    ("humanoid_relu_3x512", 4, 376, 1, 17, [512, 512, 512], [512, 512, 512], "ReLU"),
+    # the reference's own network (main.py:63-75): O=348, W=5, [256,256,128,128], A=17, ReLU,
+    # critic [128, 128] (models/critic.py:14)
+    ("main_py_net", 5, 348, 5, 17, [256, 256, 128, 128], [128, 128], "ReLU"),
 ]
 
 
@@ -55,12 +70,12 @@ def main():
     from models.network_block_creator import create_network
 
     out = {}
-    for name, seed, obs, window, act, hidden, activation in CASES:
+    for name, seed, obs, window, act, hidden, critic_hidden, activation in CASES:
         run = _make_run(obs, window, act, hidden, activation)
         torch.manual_seed(seed)
         actor = Actor()
         critic_cfg = {"final_activation": None, "activation": run.network_config.activation_class,
-                      "hidden_layer_count": len(hidden), "shapes": list(hidden)}
+                      "hidden_layer_count": len(critic_hidden), "shapes": list(critic_hidden)}
         critic = create_network(critic_cfg, input_shape=obs * window, output_shape=1,
                                 normalize_at_the_end=False, use_bias=True)
         gen = torch.Generator().manual_seed(1000 + seed)
@@ -72,11 +87,17 @@ def main():
         out[f"{name}/mean"] = mean.numpy()
         out[f"{name}/std"] = std.numpy()
         out[f"{name}/value"] = value.numpy()
-        for k, v in actor.state_dict().items():
-            out[f"{name}/actor.{k}"] = v.numpy()
-        for k, v in critic.state_dict().items():
-            out[f"{name}/critic.network.{k}"] = v.numpy()
-        out[f"{name}/meta"] = np.array([seed, obs, window, act, *hidden], dtype=np.int64)
+        out[f"{name}/activation"] = np.array(activation.lower())
+        sd = {f"actor.{k}": v for k, v in actor.state_dict().items()}
+        sd.update({f"critic.network.{k}": v for k, v in critic.state_dict().items()})
+        small = sum(v.numel() for v in sd.values()) < FULL_PARAMS_LIMIT
+        for k, v in sd.items():
+            arr = v.detach().contiguous().numpy()
+            out[f"{name}/sha256/{k}"] = np.array(hashlib.sha256(arr.tobytes()).hexdigest())
+            if small:
+                out[f"{name}/{k}"] = arr
+        out[f"{name}/meta"] = np.array([seed, obs, window, act, len(hidden), len(critic_hidden),
+                                        *hidden, *critic_hidden], dtype=np.int64)
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, sum(v.nbytes for v in out.values()), "bytes raw")
 

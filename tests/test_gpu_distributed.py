@@ -13,6 +13,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from parity_util import assert_params_match, capture_engine_grads
+
 pytestmark = pytest.mark.gpu
 
 N_GLOBAL, T, B, EPOCHS = 16, 16, 64, 2
@@ -23,7 +25,7 @@ def _streams():
     return make_synthetic_streams(N_GLOBAL, T, 17, seed=21, p_terminate=0.05)
 
 
-def _run(n_envs, shard, dp_mode, dev):
+def _run(n_envs, shard, dp_mode, dev, capture=False):
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
     from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
     from mujoco_reinforcement_learning_amd.environments import SyntheticVecEnvHelper
@@ -39,7 +41,10 @@ def _run(n_envs, shard, dp_mode, dev):
     torch.manual_seed(1234)
     mem = algo.rollout()
     algo.calculate_advantages(mem)
+    grads = capture_engine_grads(algo) if capture else None
     algo.train(mem)
+    if capture:
+        return agent.packed_params().cpu(), mem["advantage"].cpu(), grads, agent
     return agent.packed_params().cpu(), mem["advantage"].cpu()
 
 
@@ -55,7 +60,8 @@ def _worker(rank, world, port, q):
 
 
 def test_exact_dp_two_ranks_match_single_process(gpu):
-    p_single, adv_single = _run(N_GLOBAL, (0, N_GLOBAL), "local", gpu)
+    p_single, adv_single, g_single, agent = _run(N_GLOBAL, (0, N_GLOBAL), "local", gpu,
+                                                 capture=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     s = socket.socket()
@@ -77,10 +83,9 @@ def test_exact_dp_two_ranks_match_single_process(gpu):
     # rollout/GAE per shard: rank r's advantages are the single run's env rows [r*8, (r+1)*8)
     torch.testing.assert_close(torch.cat([got[0][1], got[1][1]]), adv_single, rtol=1e-5,
                                atol=1e-5)
-    diff = (got[0][0] - p_single).abs()
-    assert float(diff.max()) <= 2 * 1e-4 * EPOCHS * (N_GLOBAL * T // B), float(diff.max())
-    close = diff <= 1e-5 * p_single.abs() + 1e-7
-    assert float(close.float().mean()) >= 0.97
+    # the single process is the reference here: rtol 1e-5 except the counted Adam sign-flip-prone
+    # set (gradient below 1e-3 of its tensor's max at some step; tests/parity_util.py)
+    assert_params_match(got[0][0], p_single, g_single, agent, 1e-4, label="exact DP x2")
 
 
 def _local_worker(rank, world, port, q):

@@ -1,0 +1,79 @@
+#!/bin/bash
+# One GPU call on the gpurun box, parameterised by STEPS (space-separated, run in order, the call
+# stops at the first failing step).  Every GPU step has its own time limit.
+#   tests     pytest -m gpu (K="expr" narrows it with -k)
+#   smoke     __graft_entry__.smoke()
+#   bench     the default bench line (bf16) -> gpurun_out/bench_$TAG.json (BENCH_ARGS appended)
+#   f32       bench --precision f32 -> gpurun_out/bench_${TAG}_f32.json
+#   host      bench --env host (PCIe-inclusive) -> gpurun_out/bench_${TAG}_host.json
+#   trace     rocprofv3 --kernel-trace --stats over the bench + timing agreement
+#   traffic   FETCH_SIZE / WRITE_SIZE PMC passes over the bench -> traffic per launch
+#   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
+#   phases    fused-update phase stamps (tools/fused_phases.py)
+#   micro     tools/micro_fused.py timing of the fused update kernel alone
+# usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-r02}
+STEPS=${STEPS:-"tests smoke bench"}
+fail() { echo "STEP $1 FAILED"; [ -n "$2" ] && tail -40 "$2"; exit 1; }
+
+for S in $STEPS; do
+  echo "=== $S ($(date +%T))"
+  case $S in
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        ${K:+-k "$K"} -s > gpurun_out/gpu_tests_${TAG}.log 2>&1 || fail tests gpurun_out/gpu_tests_${TAG}.log
+      grep -E "passed|failed" gpurun_out/gpu_tests_${TAG}.log | tail -2 ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 \
+        || fail smoke gpurun_out/smoke_${TAG}.log
+      tail -2 gpurun_out/smoke_${TAG}.log ;;
+    bench)
+      timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
+        || fail bench gpurun_out/bench_${TAG}.err
+      cat gpurun_out/bench_${TAG}.json ;;
+    f32)
+      timeout -k 10 400 python bench.py --precision f32 --no-cpu-baseline > gpurun_out/bench_${TAG}_f32.json \
+        2> gpurun_out/bench_${TAG}_f32.err || fail f32 gpurun_out/bench_${TAG}_f32.err
+      cat gpurun_out/bench_${TAG}_f32.json ;;
+    host)
+      timeout -k 10 400 python bench.py --env host --no-cpu-baseline > gpurun_out/bench_${TAG}_host.json \
+        2> gpurun_out/bench_${TAG}_host.err || fail host gpurun_out/bench_${TAG}_host.err
+      cat gpurun_out/bench_${TAG}_host.json ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_${TAG}_trace -o bench --output-format csv \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-legs > gpurun_out/rp_${TAG}_bench.json \
+        2> gpurun_out/rp_${TAG}_trace.log || fail trace gpurun_out/rp_${TAG}_trace.log
+      python tools/rocprof_agree.py gpurun_out/rp_${TAG}_bench.json \
+        $(find gpurun_out/rp_${TAG}_trace -name "*kernel_stats.csv") gpurun_out/agree_${TAG}.json ;;
+    traffic)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/rp_${TAG}_fetch -o fetch --output-format csv \
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs \
+        > gpurun_out/rp_${TAG}_fetch.log 2>&1 || fail fetch gpurun_out/rp_${TAG}_fetch.log
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/rp_${TAG}_write -o write --output-format csv \
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs \
+        > gpurun_out/rp_${TAG}_write.log 2>&1 || fail write gpurun_out/rp_${TAG}_write.log
+      python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_fetch -name "*counter_collection.csv") \
+        $(find gpurun_out/rp_${TAG}_write -name "*counter_collection.csv") gpurun_out/traffic_${TAG}.json ;;
+    pmc)
+      i=0
+      for P in ${PASSES:-"SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_INSTS_VALU,SQ_INSTS_LDS SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc ${P//,/ } -d gpurun_out/pmc_${TAG}/p$i -o pmc --output-format csv \
+          -- python3 tools/micro_fused.py 10 > gpurun_out/pmc_${TAG}_p$i.log 2>&1 || fail pmc$i gpurun_out/pmc_${TAG}_p$i.log
+      done
+      python3 tools/pmc_summary.py gpurun_out/pmc_${TAG} fused_update > gpurun_out/pmc_${TAG}.txt
+      cat gpurun_out/pmc_${TAG}.txt ;;
+    phases)
+      timeout -k 10 200 python tools/fused_phases.py > gpurun_out/phases_${TAG}.txt 2>&1 || fail phases gpurun_out/phases_${TAG}.txt
+      cat gpurun_out/phases_${TAG}.txt ;;
+    micro)
+      timeout -k 10 200 python tools/micro_fused.py 20 > gpurun_out/micro_${TAG}.txt 2>&1 || fail micro gpurun_out/micro_${TAG}.txt
+      cat gpurun_out/micro_${TAG}.txt ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+done
+echo "ALL STEPS OK"
