@@ -152,9 +152,58 @@ class PPOEngine:
                                 normalize=norm, value=buf.values[t_len])
         return buf
 
+    def _rollout_pipelined(self, base_off: int) -> RolloutBuffer:
+        """Rollout over a host-physics helper split into halves (HostPhysicsVecEnvHelper,
+        overlap=True): per step and half, the half's observe + act (ppo_observe_act on its rows,
+        Philox offsets / eps rows of the full step, so the values equal the unsplit rollout), its
+        action D2H on its side stream, its workers' physics and its H2D uploads.  The host
+        releases each half as soon as its actions land, so one half's physics runs while the GPU
+        computes the other half's policy step (running_gym_sequential_vectorized.py:40-59 is the
+        serial reference loop)."""
+        helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
+        n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        helper.reset()
+        helper.reset_environment(test_phase=False)
+        eng.pack_weights()
+        window = helper.timestep.observation
+        norm = bool(self.run.normalize_observations)
+        seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
+        halves = helper.halves
+
+        def act(t, obs_rows=None, reset_rows=None, eps=None, g=0, last=False):
+            lo, hi = halves[g]
+            rows = slice(lo, hi)
+            if last:
+                eng.observe_act(window[rows], buf.states[t][rows], obs=obs_rows, reset=reset_rows,
+                                normalize=norm, value=buf.values[t][rows])
+                return
+            eng.observe_act(window[rows], buf.states[t][rows], obs=obs_rows, reset=reset_rows,
+                            all_reset=False, normalize=norm,
+                            eps=None if eps is None else eps[rows], seed=seed,
+                            offset=base_off + t * n * a + lo * a, action=buf.actions[t][rows],
+                            logp=buf.logp[t][rows], value=buf.values[t][rows])
+            helper.begin_half(g, buf.actions[t][rows])
+
+        eps, _ = self._eps(n, a)
+        for g in range(len(halves)):
+            act(0, eps=eps, g=g)
+        for t in range(t_len):
+            for g in range(len(halves)):
+                helper.release_half(g, t)
+            if t + 1 < t_len:
+                eps, _ = self._eps(n, a)
+            for g, (lo, hi) in enumerate(halves):
+                obs = helper.finish_half(g, buf.reward[t][lo:hi], buf.terminated[t][lo:hi])
+                act(t + 1, obs, buf.terminated[t][lo:hi], eps, g, last=t + 1 == t_len)
+            helper.end_step(buf.reward[t], buf.terminated[t])
+        return buf
+
     def _rollout_steps(self, base_off: int) -> RolloutBuffer:
         helper, eng, buf = self.environment_helper, self.agent.engine, self.buffer
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
+        if len(getattr(helper, "halves", ())) > 1 and \
+                getattr(self.run.engine_config, "fused_rollout", True):
+            return self._rollout_pipelined(base_off)
         if hasattr(helper, "step_raw") and getattr(self.run.engine_config, "fused_rollout", True):
             return self._rollout_fused(base_off)
         helper.reset()

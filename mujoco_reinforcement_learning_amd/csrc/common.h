@@ -54,6 +54,17 @@ __device__ __forceinline__ float act_backward(float grad, float y, int act) {
   return (y <= 0.f) ? grad * (y + 1.f) : grad;
 }
 
+// bf16 round trip (round-to-nearest-even, the hardware v_cvt_pk_bf16_f32): the operand rounding of
+// precision mode PPO_PREC_BF16 in the kernels that multiply on the VALU (bf16 x bf16 is exact in
+// f32, so an f32 FMA of rounded operands is the product an MFMA would form).
+__device__ __forceinline__ float bf16_round(float x) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  const f2_t f = {x, 0.f};
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, b2_t));
+  return __uint_as_float(u << 16);
+}
+
 // ---- wave64 reductions (butterfly: every lane ends with the same, order-fixed sum) ------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

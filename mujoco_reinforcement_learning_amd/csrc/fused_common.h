@@ -83,6 +83,64 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// ---- 16x16x32 bf16 MFMA (the head products) ------------------------------------------------
+// A[16 x 32]: lane l holds A[l & 15][8 (l >> 4) + j]; B[32 x 16]: B[8 (l >> 4) + j][l & 15];
+// D[16 x 16]: lane l holds D[4 (l >> 4) + i][l & 15], i = 0..3 (cdna_hip_programming.md s3).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16x16x32 operand whose k runs over image ROWS k0..k0+31 and whose m/n runs over image COLUMNS
+// col0..col0+15: lane (c = lane & 15, g = lane >> 4) gets rows k0 + 8g .. +7 of column col0 + c.
+// Same ds_read_b64_tr_b16 block pattern as tr_frag: a 32-lane half's two blocks sit 8 rows apart
+// in the same 16 columns (conflict-free on the XOR-swizzled image).
+__device__ __forceinline__ bf16x8 tr_frag16(const char *img, int pitch, int k0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * g + q;
+  const int c = (col0 >> 3) + (p >> 1);
+  return tr_pair(img + img_off(row, c, pitch) + 8 * (p & 1),
+                 img + img_off(row + 4, c, pitch) + 8 * (p & 1));
+}
+
+// bf16 head-weight image: 16 rows (heads; rows >= the net's head width are zero) of H bf16 plus
+// 8 bf16 of padding, so the 16 lanes of a 16x16x32 B-operand read hit 16 distinct bank groups.
+template <int H>
+struct HeadImg {
+  static constexpr int PITCH = 2 * H + 16;  // bytes
+  static constexpr int BYTES = 16 * PITCH;
+};
+
+// dz images of one 64-row chunk (bf16, the head-backward MFMA operands): row-major [64][16]
+// (d2 = dz . Wh, B operand: 8 heads of one row) and head-major [16][64 + 8] (head dW, A operand:
+// 8 rows of one head).
+constexpr int kDzRowBytes = 32;
+constexpr int kDzTPitch = 2 * (kFusedRows + 8);
+
+// Stage the net's head weights as the bf16 image (one pass over the block) and return this lane's
+// d2-MFMA A fragment W_h^T: lane (c = lane & 31, h = lane >> 5) of wave w holds
+// W_h[8h + j][32w + c], j = 0..7 (call after a barrier that follows the staging).
+template <int H>
+__device__ __forceinline__ void stage_head_image(char *img, const float *wh, int nh_real, int tid,
+                                                 int nt) {
+  for (int i = tid; i < 16 * (H / 2); i += nt) {
+    const int a = i / (H / 2), f = 2 * (i % (H / 2));
+    const float x0 = a < nh_real ? wh[a * H + f] : 0.f;
+    const float x1 = a < nh_real ? wh[a * H + f + 1] : 0.f;
+    *reinterpret_cast<uint32_t *>(img + a * HeadImg<H>::PITCH + 2 * f) = pack2(x0, x1);
+  }
+}
+template <int H>
+__device__ __forceinline__ bf16x8 head_t_frag(const char *img, int w, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = *reinterpret_cast<const short *>(img + (8 * h + j) * HeadImg<H>::PITCH + 2 * (32 * w + c));
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // Fixed-order reduce-scatter of 16 per-lane values over the 32 lanes of a wave half: after the
 // xor-16/8/4/2 halvings and a final xor-1 add, lane m holds the full sum of value
 // q(m) = 8*b4(m) + 4*b3(m) + 2*b2(m) + b1(m) (bit k of m: bk), duplicated on lanes m, m^1.
@@ -133,20 +191,36 @@ __device__ __forceinline__ int rs16_feature(int lane) {
 __device__ __forceinline__ int reg_feature(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
 // acc[t] += W[32w + r][:] . img[32t + r][:] over k = 0..H-1 for row tiles t = 0, 1.  A operand
-// = 16-B rows of the L2-resident bf16 weight image (wrow -> row 32w + r, column 8h), B operand
-// = 16-B row reads of the LDS activation image.  Weight fragments run through a ring of PD + 1
-// registers: the load for k-step s + PD is issued before the MFMAs of step s (the first PD by
-// wring_prime, a phase earlier), so L2 latency hides behind 2*PD MFMAs per wave; the B reads of
-// step s + 1 overlap step s; sched_barrier pins one k-step per scheduling region so the
-// compiler cannot hoist the whole pass's loads (register blow-up).
+// = the L2-resident bf16 weight image in FRAGMENT-MAJOR order (w_frag below: the 64 lanes' 16-B
+// fragments of one (k-step, wave) are one contiguous 1 KB block, so a ring load is 8 full cache
+// lines instead of 32 partial row pieces), B operand = 16-B row reads of the LDS activation image.
+// Weight fragments run through a ring of PD + 1 registers: the load for k-step s + PD is issued
+// before the MFMAs of step s (the first PD by wring_prime, a phase earlier), so L2 latency hides
+// behind 2*PD MFMAs per wave; the B reads of step s + 1 overlap step s; sched_barrier pins one
+// k-step per scheduling region so the compiler cannot hoist the whole pass's loads (register
+// blow-up).
 constexpr int PD = 3;  // prefetch distance (k-steps); ring period PD + 1 = 4
+
+// Fragment-major H x H image: element (o, i) -- output feature o, input column i -- of the
+// 32x32x16 A operand for (k-step s = i / 16, wave w = o / 32, lane h*32 + r) lives at
+// ((s * (H/32) + w) * 64 + h * 32 + r) * 8 + (i & 7), h = (i / 8) & 1, r = o & 31.
+__device__ __forceinline__ int64_t w_frag(int o, int i, int H) {
+  return (static_cast<int64_t>((i >> 4) * (H >> 5) + (o >> 5)) * 64 + ((i >> 3) & 1) * 32 + (o & 31)) * 8 +
+         (i & 7);
+}
+// The wave's fragment of k-step 0 (lane = h * 32 + r); k-step s is s * 16 * H elements further.
 template <int H>
-__device__ __forceinline__ void wring_prime(const __bf16 *wrow, bf16x8 (&ring)[PD + 1]) {
+__device__ __forceinline__ const __bf16 *w_frag_base(const __bf16 *img, int w, int lane) {
+  return img + (static_cast<int64_t>(w) * 64 + lane) * 8;
+}
+
+template <int H>
+__device__ __forceinline__ void wring_prime(const __bf16 *wfrag, bf16x8 (&ring)[PD + 1]) {
 #pragma unroll
-  for (int s = 0; s < PD; ++s) ring[s] = *reinterpret_cast<const bf16x8 *>(wrow + 16 * s);
+  for (int s = 0; s < PD; ++s) ring[s] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * s);
 }
 template <int H>
-__device__ __forceinline__ void mlp_pass(const __bf16 *wrow, const char *img, int r, int h,
+__device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, int r, int h,
                                          bf16x8 (&ring)[PD + 1], f32x16 (&acc)[2]) {
   constexpr int KS = H / 16;
   static_assert(KS % (PD + 1) == 0, "ring period must divide the k-steps");
@@ -162,7 +236,7 @@ __device__ __forceinline__ void mlp_pass(const __bf16 *wrow, const char *img, in
       // would make the in-flight count differ between loop iterations, and the vmcnt waits of
       // the rolled loop assume a uniform count
       ring[(u + PD) % (PD + 1)] =
-          *reinterpret_cast<const bf16x8 *>(wrow + 16 * min(s + PD, KS - 1));
+          *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * min(s + PD, KS - 1));
       const char *p = rowp + 16 * ((2 * s + h) ^ swz);
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);

@@ -29,9 +29,9 @@ struct PolicyLds {
   static constexpr int PITCH = 2 * H;
   static constexpr int X = 0;                                   // bf16 [64][32]
   static constexpr int A1 = X + R * 64;                         // bf16 [64][H]
-  static constexpr int ZP = A1 + R * PITCH;                     // f32 [8 waves][64][8]
-  static constexpr int WH = ZP + NW * R * 8 * 4;                // f32 head [8][H]
-  static constexpr int BIAS = WH + 8 * H * 4;                   // f32 b0[H], b1[H]
+  static constexpr int A2 = A1 + R * PITCH;                     // bf16 [64][H]
+  static constexpr int WH = A2 + R * PITCH;                     // bf16 head image [16][H + 8]
+  static constexpr int BIAS = WH + HeadImg<H>::BYTES;           // f32 b0[H], b1[H]
   static constexpr int HS = BIAS + 2 * H * 4;                   // f32 head bias[8], logstd[8]
   static constexpr int XS = HS + 16 * 4;                        // f32 [64][33] standardised states
   static constexpr int TOTAL = XS + R * kPolicyXsPitch * 4;
@@ -51,8 +51,8 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   using L = PolicyLds<H>;
   char *const ximg = lds + L::X;
   char *const a1img = lds + L::A1;
-  float *const zp = reinterpret_cast<float *>(lds + L::ZP);
-  float *const whs = reinterpret_cast<float *>(lds + L::WH);
+  char *const a2img = lds + L::A2;
+  char *const whb = lds + L::WH;
   float *const bias = reinterpret_cast<float *>(lds + L::BIAS);
   float *const hs = reinterpret_cast<float *>(lds + L::HS);
   float *const xs = reinterpret_cast<float *>(lds + L::XS);
@@ -63,8 +63,8 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   const int A = q.act_dim;
   const int O = q.obs_dim;
 
-  // ---- stage head / bias parameters (f32) ----
-  for (int i = tid; i < NH * H; i += NT) whs[i] = (ACTOR && i / H >= A) ? 0.f : N.wh[i];
+  // ---- stage head (bf16 image) / bias parameters ----
+  stage_head_image<H>(whb, N.wh, ACTOR ? A : 1, tid, NT);
   for (int i = tid; i < 2 * H; i += NT) {
     const float *b = i < H ? N.b0 : N.b1;
     bias[i] = b ? b[i % H] : 0.f;
@@ -146,7 +146,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----
   bf16x8 ring[PD + 1];
-  wring_prime<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, ring);
+  wring_prime<H>(w_frag_base<H>(N.w1b, w, lane), ring);
   {
     f32x16 acc[2];
 #pragma unroll
@@ -179,92 +179,77 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   __syncthreads();
   PSTAMP(4);
 
-  // ---- L1 + head partial sums over the wave's 32 features (f32) ----
+  // ---- L1: a2 = act(W1 a1 + b1) -> A2 image (bf16: the head's operand) ----
   {
     f32x16 a2[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
-    mlp_pass<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, a1img, r, h, ring, a2);
+    mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
     PSTAMP(5);
-    float zpart[2][NH];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int a = 0; a < NH; ++a) zpart[t][a] = 0.f;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * w + 8 * g + 4 * h;
       const float4 bv = *reinterpret_cast<const float4 *>(bias + H + f0);
-      float4 y[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        y[t] = make_float4(act_forward(a2[t][4 * g] + bv.x, ACT), act_forward(a2[t][4 * g + 1] + bv.y, ACT),
-                           act_forward(a2[t][4 * g + 2] + bv.z, ACT), act_forward(a2[t][4 * g + 3] + bv.w, ACT));
-#pragma unroll
-      for (int a = 0; a < NH; ++a) {
-        const float4 wv = *reinterpret_cast<const float4 *>(whs + a * H + f0);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          float p = zpart[t][a];
-          p = fmaf(y[t].x, wv.x, p);
-          p = fmaf(y[t].y, wv.y, p);
-          p = fmaf(y[t].z, wv.z, p);
-          p = fmaf(y[t].w, wv.w, p);
-          zpart[t][a] = p;
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int a = 0; a < NH; ++a) zpart[t][a] += __shfl_xor(zpart[t][a], 32, 64);
-      if (h == 0) {
-        float *dst = zp + (w * R + 32 * t + r) * 8;
-#pragma unroll
-        for (int a = 0; a < NH; ++a) dst[a] = zpart[t][a];
-      }
+        *reinterpret_cast<uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
+            make_uint2(pack2(act_forward(a2[t][4 * g] + bv.x, ACT), act_forward(a2[t][4 * g + 1] + bv.y, ACT)),
+                       pack2(act_forward(a2[t][4 * g + 2] + bv.z, ACT), act_forward(a2[t][4 * g + 3] + bv.w, ACT)));
     }
   }
   __syncthreads();
   PSTAMP(6);
 
-  // ---- heads ----
-  if constexpr (ACTOR) {
-    const int lrow = tid >> 3, a = tid & 7, env = row0 + lrow;  // 512 threads = 64 rows x 8
-    float lp = 0.f;
-    if (a < A && env < q.n) {
-      float zz = 0.f;
+  // ---- heads: z = a2 . W_h^T on the 16x16x32 MFMA (the update kernel's bf16 products); waves w
+  //      and w + 4 form the same 16-row tile and split its rows: lane -> head n = lane & 15, rows
+  //      16 (w & 3) + 4 (lane >> 4) + 2 (w >> 2) + {0, 1} ----
+  {
+    const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
+    f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int v = 0; v < NW; ++v) zz += zp[(v * R + lrow) * 8 + a];
-      if (N.bh) zz += hs[a];
-      const float mu = q.omv * tanhf(zz);
-      const float sd = expf(hs[8 + a]);
-      const int64_t idx = static_cast<int64_t>(env) * A + a;
-      const float e = q.eps ? q.eps[idx]
-                            : philox_normal_at(q.seed, q.offset + (q.offset_base ? *q.offset_base : 0) + idx);
-      const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
-      if (q.action) q.action[idx] = x;
-      if (q.mean) q.mean[idx] = mu;
-      const float d = x - mu;
+    for (int s = 0; s < H / 32; ++s)
+      zacc = mfma16(lds_b128(a2img + img_off(16 * tile + n, 4 * s + qg, L::PITCH)),
+                    lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
+    asm volatile("s_nop 15" : "+v"(zacc));
+    const float zr[2] = {half ? zacc[2] : zacc[0], half ? zacc[3] : zacc[1]};
+    if constexpr (ACTOR) {
+      const bool act_lane = n < A;
+      const float sd = act_lane ? expf(hs[8 + n]) : 1.f;
+      const float lsd = act_lane ? logf(sd) : 0.f;
       const float var = sd * sd;
-      lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
-    }
-    float s = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
 #pragma unroll
-    for (int aa = 0; aa < NH; ++aa) {
-      const float t = __shfl(lp, (lane & ~7) + aa, 64);
-      if (aa < A) s += t;
-    }
-    if (a == 0 && env < q.n && q.logp) q.logp[env] = s;
-  } else {
-    const int env = row0 + tid;
-    if (tid < R && env < q.n && q.value) {
-      float v = 0.f;
+      for (int i = 0; i < 2; ++i) {
+        const int env = row0 + 16 * tile + 4 * qg + 2 * half + i;
+        float lp = 0.f;
+        if (act_lane && env < q.n) {
+          float zz = zr[i];
+          if (N.bh) zz += hs[n];
+          const float mu = q.omv * tanhf(zz);
+          const int64_t idx = static_cast<int64_t>(env) * A + n;
+          const float e = q.eps ? q.eps[idx]
+                                : philox_normal_at(q.seed, q.offset + (q.offset_base ? *q.offset_base : 0) + idx);
+          const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
+          if (q.action) q.action[idx] = x;
+          if (q.mean) q.mean[idx] = mu;
+          const float d = x - mu;
+          lp = ((-(d * d)) / (2.f * var) - lsd) - kLogSqrt2Pi;
+        }
+        float s = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
 #pragma unroll
-      for (int u = 0; u < NW; ++u) v += zp[(u * R + tid) * 8];
-      q.value[env] = N.bh ? v + hs[0] : v;
+        for (int aa = 0; aa < NH; ++aa) {
+          const float t = __shfl(lp, (lane & ~15) + aa, 64);
+          if (aa < A) s += t;
+        }
+        if (n == 0 && env < q.n && q.logp) q.logp[env] = s;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int env = row0 + 16 * tile + 4 * qg + 2 * half + i;
+        if (n == 0 && env < q.n && q.value) q.value[env] = N.bh ? zr[i] + hs[0] : zr[i];
+      }
     }
   }
   PSTAMP(7);

@@ -36,6 +36,8 @@ namespace ppo {
 
 using namespace fu;
 
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(pack2(x, 0.f) & 0xffffu); }
+
 // ============================================================================================
 // Prep: gather the minibatch rows once per minibatch into contiguous bf16 / f32 staging, and
 // refresh the bf16 weight images (row-major and transposed W1) from the f32 masters.
@@ -110,8 +112,8 @@ __global__ __launch_bounds__(256) void fused_prep_kernel(FusedArgs q, int row_bl
     const int64_t t = i - static_cast<int64_t>(H) * kFusedKX;
     const int o = static_cast<int>(t / H), c = static_cast<int>(t % H);
     const __bf16 v = __builtin_bit_cast(__bf16, static_cast<uint16_t>(pack2(N.w1[t], 0.f) & 0xffffu));
-    w1b[t] = v;
-    w1bt[static_cast<int64_t>(c) * H + o] = v;
+    w1b[w_frag(o, c, H)] = v;   // fragment-major images (fused_common.h w_frag)
+    w1bt[w_frag(c, o, H)] = v;
   }
 }
 
@@ -153,8 +155,6 @@ __global__ __launch_bounds__(256) void fused_records_kernel(uint4 *__restrict__ 
 // the transposed image through an LDS transpose, so both image writes are coalesced.
 // ============================================================================================
 constexpr int kPackTile = 32;
-
-__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(pack2(x, 0.f) & 0xffffu); }
 
 __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a, int gen_blocks) {
   const float ns_a = a.sched ? a.sched[0] : a.neg_a;
@@ -204,14 +204,14 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a, int gen_
     a.m[i] = m;
     a.v[i] = v;
     const uint16_t hb = bf16_bits(p);
-    w1b[t] = hb;
+    w1b[w_frag(to * kPackTile + lo, tc * kPackTile + lc, H)] = hb;
     tile[lo][lc] = hb;
   }
   __syncthreads();
 #pragma unroll 4
   for (int k = 0; k < kPackTile * kPackTile / 256; ++k) {
     const int idx = k * 256 + tid, lc = idx / kPackTile, lo = idx % kPackTile;
-    w1bt[static_cast<int64_t>(tc * kPackTile + lc) * H + to * kPackTile + lo] = tile[lo][lc];
+    w1bt[w_frag(tc * kPackTile + lc, to * kPackTile + lo, H)] = tile[lo][lc];
   }
 }
 
@@ -264,10 +264,11 @@ __global__ __launch_bounds__(256) void step_tail_kernel(ReduceArgs r, TailArgs t
     const int64_t e1 = i - a.off_w1[z];
     if (e1 >= 0 && e1 < static_cast<int64_t>(H) * H) {  // 4 columns of one W1 row (H % 4 == 0)
       const int o = static_cast<int>(e1 / H), c = static_cast<int>(e1 % H);
-      *reinterpret_cast<uint2 *>(a.w1b[z] + e1) = make_uint2(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]));
+      // 4 consecutive columns stay inside one 8-element fragment run (c % 4 == 0)
+      *reinterpret_cast<uint2 *>(a.w1b[z] + w_frag(o, c, H)) = make_uint2(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]));
       uint16_t *wt = reinterpret_cast<uint16_t *>(a.w1bt[z]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wt[static_cast<int64_t>(c + e) * H + o] = bf16_bits(pv[e]);
+      for (int e = 0; e < 4; ++e) wt[w_frag(c + e, o, H)] = bf16_bits(pv[e]);
     }
     const int64_t e0 = i - a.off_w0[z];
 #pragma unroll
@@ -283,49 +284,68 @@ __global__ __launch_bounds__(256) void step_tail_kernel(ReduceArgs r, TailArgs t
 // ============================================================================================
 // The fused update kernel
 // ============================================================================================
-template <int H>
+template <int H, bool F32A2>
 struct Lds {
-  static constexpr int PITCH = 2 * H;          // A1 / D2 / D1 row pitch (bytes), multiple of 256
-  static constexpr int A2P = 4 * H + 16;       // A2F row pitch (bytes): +16 B -> conflict-free b128 stores
-  static constexpr int WH = 0;                                  // f32 head weights [8][H]
-  static constexpr int BIAS = WH + kFusedMaxAct * H * 4;        // f32 b0[H], b1[H]
+  static constexpr int PITCH = 2 * H;          // A1 / D2 / A2 / D1 bf16 row pitch (bytes), multiple of 256
+  static constexpr int A2P = 4 * H + 16;       // A2F f32 row pitch (bytes): +16 B -> conflict-free b128 stores
+  static constexpr int WHB = 0;                                 // bf16 head image [16][H + 8]
+  static constexpr int BIAS = WHB + HeadImg<H>::BYTES;          // f32 b0[H], b1[H]
   static constexpr int X = BIAS + 2 * H * 4;                    // bf16 [64][32]
   static constexpr int A1 = X + R * 64;                         // bf16 [64][H]
-  static constexpr int D2 = A1 + R * PITCH;                     // bf16 [64][H]; head partials alias
-  static constexpr int A2F = D2 + R * PITCH;                    // f32 [64][H]; D1 bf16 image aliases
-  static constexpr int DZ = A2F + R * A2P;                      // f32 [64][12]
-  static constexpr int RED = DZ + R * DZP * 4;                  // f32 [64][8] row-thread partials
-  static constexpr int HS = RED + R * 8 * 4;                    // f32 head bias[8], logstd[8]
-  static constexpr int TOTAL = HS + 16 * 4;
+  static constexpr int D2 = A1 + R * PITCH;                     // bf16 [64][H]
+  // a2 after the layer-1 epilogue: the bf16 image (ReLU: act' needs only the sign it keeps) or
+  // the f32 values (tanh / ELU: act'(a2) on the f32 a2, the head operands rounded on the fly);
+  // the D1 image (bf16) takes the region over after phase 5
+  static constexpr int A2 = D2 + R * PITCH;
+  static constexpr int A2BYTES = F32A2 ? R * A2P : R * PITCH;
+  static constexpr int DZ = A2 + A2BYTES;                       // bf16 dz [64][16]
+  static constexpr int DZT = DZ + R * kDzRowBytes;              // bf16 dz^T [16][64 + 8]
+  static constexpr int HS = DZT + 16 * kDzTPitch;               // f32 head bias, logstd, log std, var [16] each
+  static constexpr int SROW = HS + 64 * 4;                      // f32 [64][16] the chunk's row scalars
+  static constexpr int RED = SROW;                              // epilogue: f32 [8 waves][16 heads][4]
+  static constexpr int TOTAL = SROW + R * kFusedSP * 4;
   static_assert(TOTAL <= 163840, "LDS budget");
-  static_assert(NW * R * 8 * 4 <= R * PITCH, "head partials must fit in the D2 image");
-  static_assert(R * PITCH <= R * A2P, "D1 image must fit in the A2F region");
+  static_assert(R * PITCH <= A2BYTES, "D1 image must fit in the a2 region");
 };
+
+
+// 8 f32 (two float4) -> the bf16x8 MFMA operand (RNE), for the f32-a2 (tanh / ELU) instantiations
+__device__ __forceinline__ bf16x8 pack8(float4 u, float4 v) {
+  const uint4 p = make_uint4(pack2(u.x, u.y), pack2(u.z, u.w), pack2(v.x, v.y), pack2(v.z, v.w));
+  return __builtin_bit_cast(bf16x8, p);
+}
+
+// VALU reads of a 16x16x32 result right after the (unrolled) MFMA chain: pinned wait states as
+// mfma_drain does for the 32x32x16 accumulators
+__device__ __forceinline__ void mfma16_drain(f32x4 &acc) { asm volatile("s_nop 15" : "+v"(acc)); }
 
 // STAMP (diagnostic build, ppo_ctx_phase_stamps): wave 0 sums s_memtime deltas per phase segment
 // over the chunks and writes them per workgroup; the product kernel has STAMP = false.
 constexpr int kStampSlots = 11;
 
 // One net's workgroup: 8 waves; wave w owns feature tile w (features 32w..32w+31) in every
-// feature-tiled phase, dW1 tiles (o-tiles 2(w&3)+{0,1}) x (i-tiles 4(w>>2)+{0..3}) and dW0 tile
-// w.  NH = head width (actor: act_dim padded to 2/4/6/8 with zero head rows, critic: 1),
-// compile-time so every per-action loop is branch-free.
+// feature-tiled phase, dW1 tiles (o-tiles 2(w&3)+{0,1}) x (i-tiles 4(w>>2)+{0..3}), dW0 tile w and
+// the head-dW tiles of its features.  NH = head width padded to 2/4/6/8 (actor) or 1 (critic),
+// compile-time so the per-action loops are branch-free.  Every fc product -- the three hidden
+// GEMMs and the head -- is a bf16-operand MFMA with f32 accumulation (oracle.use_bf16_gemms).
 template <int H, int ACT, int NH, bool ACTOR, bool STAMP>
 __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N, char *lds,
                                            uint64_t *stamps) {
   static_assert(H == 32 * NW, "wave w owns feature tile w");
-  using L = Lds<H>;
+  constexpr bool F32A2 = ACT != PPO_ACT_RELU;
+  using L = Lds<H, F32A2>;
   constexpr int z = ACTOR ? 0 : 1;
   char *const ximg = lds + L::X;
   char *const a1img = lds + L::A1;
   char *const d2img = lds + L::D2;
-  char *const d1img = lds + L::A2F;
-  float *const whs = reinterpret_cast<float *>(lds + L::WH);
+  char *const a2img = lds + L::A2;
+  char *const d1img = lds + L::A2;  // after phase 5
+  char *const whb = lds + L::WHB;
+  char *const dzimg = lds + L::DZ;
+  char *const dztimg = lds + L::DZT;
   const float *const b0s = reinterpret_cast<const float *>(lds + L::BIAS);
   const float *const b1s = b0s + H;
-  float *const dzs = reinterpret_cast<float *>(lds + L::DZ);
-  float *const zp = reinterpret_cast<float *>(lds + L::D2);  // [NW][R][8] head partials
-  const float *const a2f = reinterpret_cast<const float *>(lds + L::A2F);
+  const float *const a2f = reinterpret_cast<const float *>(lds + L::A2);
 
   const int tid0 = threadIdx.x, w = tid0 >> 6;
   int tid = tid0, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -338,27 +358,30 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   lane = tid & 63;                \
   r = lane & 31;                  \
   h = lane >> 5
-  const int A = q.act_dim;        // real actor width (NH >= A; rows A..NH-1 of whs are zero)
+  const int A = q.act_dim;        // real actor width (NH >= A; head rows A..15 are zero)
   const int G = q.G;
   const int nchunks = (q.b + R - 1) / R;
   const int count = q.rows_n ? *q.rows_n : q.b;
 
-  for (int i = tid; i < NH * H; i += NT) {
-    const int a = i / H;
-    whs[i] = (ACTOR && a >= A) ? 0.f : N.wh[i];
-  }
+  stage_head_image<H>(whb, N.wh, ACTOR ? A : 1, tid, NT);
   for (int i = tid; i < 2 * H; i += NT) {
     const float *b = i < H ? N.b0 : N.b1;
     (reinterpret_cast<float *>(lds + L::BIAS))[i] = b ? b[i % H] : 0.f;
   }
-  if (tid < 16) {
-    const int a = tid & 7;
+  if (tid < 32) {
+    const int a = tid & 15;
     const bool ok = a < (ACTOR ? A : 1);
     (reinterpret_cast<float *>(lds + L::HS))[tid] =
-        tid < 8 ? ((ok && N.bh) ? N.bh[a] : 0.f) : ((ACTOR && ok) ? q.logstd[a] : 0.f);
+        tid < 16 ? ((ok && N.bh) ? N.bh[a] : 0.f) : ((ACTOR && ok) ? q.logstd[a] : 0.f);
+  }
+  if (tid < 16) {  // per-head Normal constants: log(std), var = std^2, std = exp(logstd)
+    const bool ok = ACTOR && tid < A;
+    const float sd = ok ? expf(q.logstd[tid]) : 1.f;
+    (reinterpret_cast<float *>(lds + L::HS))[32 + tid] = ok ? logf(sd) : 0.f;
+    (reinterpret_cast<float *>(lds + L::HS))[48 + tid] = sd * sd;
   }
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
-  const float *const hlogstd = hbias + 8;
+  __syncthreads();
 
   // ---- persistent accumulators ----
   f32x16 gw1[2][4];   // dW1 tiles: o-tiles 2*(w&3)+{0,1}, i-tiles 4*(w>>2)+{0..3}
@@ -371,23 +394,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       for (int e = 0; e < 16; ++e) gw1[a][b][e] = 0.f;
 #pragma unroll
   for (int e = 0; e < 16; ++e) gw0[e] = 0.f;
-  float gb1 = 0.f, gb0 = 0.f;                 // rs16-scattered bias grads (feature rs16_feature)
-  float gwh[NH];                              // head dW: feature fh = tid % H, rows group tid / H
+  f32x4 ghw[2];       // head dW: heads 4*(lane>>4)+i, features 32w + 16u + (lane & 15)
 #pragma unroll
-  for (int a = 0; a < NH; ++a) gwh[a] = 0.f;
-  float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;  // row-thread (lrow, la) partials
-
-  // loss-phase thread -> (row lrow, action la); head-dW thread -> (feature fh, row group rg).
-  // Re-derived from the opaque lane id inside each phase (see OPAQUE_LANE).
-  int lrow = tid0 >> 3, la = tid0 & 7;
-  constexpr int RG = NT / H;
-  int fh = tid0 % H, rg = tid0 / H;
-#define OPAQUE_ROWS()  \
-  OPAQUE_LANE();       \
-  lrow = tid >> 3;     \
-  la = tid & 7;        \
-  fh = tid % H;        \
-  rg = tid / H
+  for (int u = 0; u < 2; ++u) ghw[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gb1 = 0.f, gb0 = 0.f;                 // rs16-scattered bias grads (feature rs16_feature)
+  float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;  // head (lane & 15) partials
 
   // X staging: thread -> 8 B (row tid>>3, unit tid&7) of the chunk's bf16 states
   auto load_x = [&](int c) -> uint2 {
@@ -413,12 +424,14 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 
   bf16x8 ring[PD + 1];
   for (; chunk < nchunks; chunk += G) {
-    // ---- phase 0: X image; row scalars for the loss phase; W0 fragments ----
-    OPAQUE_ROWS();
+    // ---- phase 0: X image; W0 fragments; the chunk's row scalars (actions, old log-prob,
+    //      advantage, value target: 64 x 64 B) issued for the head phase, staged at phase 1's end
+    OPAQUE_LANE();
     *reinterpret_cast<uint2 *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xpre;
-    const int jrow = chunk * R + lrow;
-    const bool valid = jrow < count;
-    float s_act = 0.f, s_old = 0.f, s_adv = 0.f, s_vt = 0.f;
+    const int srow_j = chunk * R + (tid >> 3);
+    const uint2 srow_v = srow_j < q.b
+        ? *reinterpret_cast<const uint2 *>(q.srow + static_cast<int64_t>(srow_j) * kFusedSP + 2 * (tid & 7))
+        : make_uint2(0u, 0u);
     bf16x8 w0f[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -428,7 +441,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 
     // ---- phase 1: a1 = act(W0 x + b0) -> A1 image ----
     OPAQUE_LANE();
-    wring_prime<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, ring);  // for phase 2
+    wring_prime<H>(w_frag_base<H>(N.w1b, w, lane), ring);  // for phase 2
     {
       f32x16 acc[2];
 #pragma unroll
@@ -455,224 +468,190 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         }
       }
     }
+    *reinterpret_cast<uint2 *>(lds + L::SROW + tid * 8) = srow_v;
     __syncthreads();
     STAMP_AT(1);
 
     // ---- phase 2: a2 = W1 a1 (f32 accumulators) ----
     OPAQUE_LANE();
-    // the loss phase's row scalars: issued here, in flight behind this barrier-free MFMA pass
-    if (jrow < q.b) {
-      const float *sp = q.srow + static_cast<int64_t>(jrow) * kFusedSP;
-      if constexpr (ACTOR) {
-        if (la < A) s_act = sp[la];
-        s_old = sp[A];
-        s_adv = sp[A + 1];
-      } else {
-        s_vt = sp[A + 2];
-      }
-    }
-    {
-      f32x16 a2[2];
+    f32x16 a2[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
-      mlp_pass<H>(N.w1b + static_cast<int64_t>(32 * w + r) * H + 8 * h, a1img, r, h, ring, a2);
-      STAMP_AT(2);
+      for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
+    mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
+    STAMP_AT(2);
 
-      // ---- phase 3: bias + act -> A2F (f32); head partial sums over the wave's 32 features ----
-      OPAQUE_LANE();
+    // ---- phase 3: bias + act -> a2 region; the head phase's row scalars issued here ----
+    OPAQUE_LANE();
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int f0 = 32 * w + 8 * g + 4 * h;
-        const float4 bv = *reinterpret_cast<const float4 *>(b1s + f0);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          *reinterpret_cast<float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0) =
-              make_float4(act_forward(a2[t][4 * g] + bv.x, ACT),
-                          act_forward(a2[t][4 * g + 1] + bv.y, ACT),
-                          act_forward(a2[t][4 * g + 2] + bv.z, ACT),
-                          act_forward(a2[t][4 * g + 3] + bv.w, ACT));
-      }
-    }
-    {
-      // a2 is dead from here on; the partial sums re-read this lane's own f32 values
-      float zpart[2][NH];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int a = 0; a < NH; ++a) zpart[t][a] = 0.f;
-#pragma unroll 1
-      for (int g = 0; g < 4; ++g) {
-        const int f0 = 32 * w + 8 * g + 4 * h;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const float4 y = *reinterpret_cast<const float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0);
-#pragma unroll
-          for (int a = 0; a < NH; ++a) {
-            const float4 wv = *reinterpret_cast<const float4 *>(whs + a * H + f0);
-            float p = zpart[t][a];
-            p = fmaf(y.x, wv.x, p);
-            p = fmaf(y.y, wv.y, p);
-            p = fmaf(y.z, wv.z, p);
-            p = fmaf(y.w, wv.w, p);
-            zpart[t][a] = p;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one feature group per region (no load hoisting)
-      }
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * w + 8 * g + 4 * h;
+      const float4 bv = *reinterpret_cast<const float4 *>(b1s + f0);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int a = 0; a < NH; ++a) zpart[t][a] += __shfl_xor(zpart[t][a], 32, 64);
-        if (h == 0) {
-          float *dst = zp + (w * R + 32 * t + r) * 8;
-          if constexpr (NH == 1) {
-            dst[0] = zpart[t][0];
-          } else {
-#pragma unroll
-            for (int a = 0; a < NH; a += 2)
-              *reinterpret_cast<float2 *>(dst + a) = make_float2(zpart[t][a], zpart[t][a + 1]);
-          }
-        }
+        const float y0 = act_forward(a2[t][4 * g] + bv.x, ACT);
+        const float y1 = act_forward(a2[t][4 * g + 1] + bv.y, ACT);
+        const float y2 = act_forward(a2[t][4 * g + 2] + bv.z, ACT);
+        const float y3 = act_forward(a2[t][4 * g + 3] + bv.w, ACT);
+        if constexpr (F32A2)
+          *reinterpret_cast<float4 *>(a2img + (32 * t + r) * L::A2P + 4 * f0) = make_float4(y0, y1, y2, y3);
+        else
+          *reinterpret_cast<uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
+              make_uint2(pack2(y0, y1), pack2(y2, y3));
       }
     }
     __syncthreads();
     STAMP_AT(3);
 
-    // ---- phase 4: per-row loss head (thread = (row, action)), torch formulas as
-    //      update_head_q4_kernel ----
-    OPAQUE_ROWS();
+    // ---- phase 4: head z = a2 . W_h^T on the 16x16x32 MFMA, then the per-(row, action) loss
+    //      head in registers -> dz images.  Waves w and w + 4 form the same 16-row z tile
+    //      (8 MFMAs each) and split its rows: lane -> head n = lane & 15, rows
+    //      16 (w & 3) + 4 (lane >> 4) + 2 (w >> 2) + {0, 1} ----
+    OPAQUE_LANE();
     {
-      float dzv = 0.f;
-      if constexpr (ACTOR) {
-        float y = 0.f, d = 0.f, var = 1.f, lp = 0.f;
-        const bool act_lane = la < A;
-        if (act_lane) {
-          float zz = 0.f;
+      const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
+      const float *const srl = reinterpret_cast<const float *>(lds + L::SROW);
+      f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int v = 0; v < NW; ++v) zz += zp[(v * R + lrow) * 8 + la];
-          if (N.bh) zz += hbias[la];
-          y = tanhf(zz);
-          const float mu = q.omv * y;
-          const float sd = expf(hlogstd[la]);
-          const float x = valid ? s_act : mu;
-          d = x - mu;
-          var = sd * sd;
-          lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+      for (int s = 0; s < H / 32; ++s) {
+        bf16x8 av;
+        if constexpr (F32A2) {
+          const float *p = a2f + (16 * tile + n) * (L::A2P / 4) + 32 * s + 8 * qg;
+          av = pack8(*reinterpret_cast<const float4 *>(p), *reinterpret_cast<const float4 *>(p + 4));
+        } else {
+          av = lds_b128(a2img + img_off(16 * tile + n, 4 * s + qg, L::PITCH));
         }
-        float logp = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
+        zacc = mfma16(av, lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
+      }
+      mfma16_drain(zacc);
+      const float zr[2] = {half ? zacc[2] : zacc[0], half ? zacc[3] : zacc[1]};
+      const float h_lsd = hbias[32 + n], h_var = hbias[48 + n];
+      float dz[2];
 #pragma unroll
-        for (int a = 0; a < NH; ++a) {
-          const float t = __shfl(lp, (lane & ~7) + a, 64);
-          if (a < A) logp += t;
-        }
-        const float old_lp = valid ? s_old : logp;
-        const float adv = valid ? s_adv : 0.f;
-        const float ratio = expf(logp - old_lp);
-        const float s1 = ratio * adv;
-        const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
-        const float s2 = cl * adv;
-        const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
-        const float gg = -q.inv_b;
-        const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
-        const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
-        const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
-        const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
-        const float dlogp = valid ? dratio * ratio : 0.f;
-        if (act_lane) {
-          const float dmu = dlogp * (d / var);
-          dzv = (dmu * q.omv) * (1.f - y * y);
-          if (valid) {
-            g_ls += dlogp * ((d * d) / var - 1.f) - q.ent_coef * q.inv_ba;
-            g_bh += dzv;
+      for (int i = 0; i < 2; ++i) {
+        const int lr = 16 * tile + 4 * qg + 2 * half + i;
+        const bool valid = chunk * R + lr < count;
+        const float *sp = srl + lr * kFusedSP;
+        dz[i] = 0.f;
+        if constexpr (ACTOR) {
+          const bool act_lane = n < A;
+          float y = 0.f, d = 0.f, lp = 0.f;
+          if (act_lane) {
+            float zz = zr[i];
+            if (N.bh) zz += hbias[n];
+            y = tanhf(zz);
+            const float mu = q.omv * y;
+            const float x = valid ? sp[n] : mu;
+            d = x - mu;
+            lp = ((-(d * d)) / (2.f * h_var) - h_lsd) - kLogSqrt2Pi;
+          }
+          float logp = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
+#pragma unroll
+          for (int a = 0; a < NH; ++a) {
+            const float t = __shfl(lp, (lane & ~15) + a, 64);
+            if (a < A) logp += t;
+          }
+          const float old_lp = valid ? sp[A] : logp;
+          const float adv = valid ? sp[A + 1] : 0.f;
+          const float ratio = expf(logp - old_lp);
+          const float s1 = ratio * adv;
+          const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+          const float s2 = cl * adv;
+          const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+          const float gg = -q.inv_b;
+          const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+          const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+          const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+          const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+          const float dlogp = valid ? dratio * ratio : 0.f;
+          if (act_lane) {
+            const float dmu = dlogp * (d / h_var);
+            dz[i] = (dmu * q.omv) * (1.f - y * y);
+            if (valid) {
+              g_ls += dlogp * ((d * d) / h_var - 1.f) - q.ent_coef * q.inv_ba;
+              g_bh += dz[i];
+            }
+          }
+          if (valid && n == 0) g_loss += mn;
+        } else {
+          if (n == 0) {
+            float v = zr[i];
+            if (N.bh) v += hbias[0];
+            const float vt = valid ? sp[A + 2] : v;
+            const float diff = v - vt;
+            const float ad = fabsf(diff);
+            if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+            dz[i] = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+            g_bh += dz[i];
           }
         }
-        if (valid && la == 0) g_loss += mn;
-      } else {
-        if (la == 0) {
-          float v = 0.f;
-#pragma unroll
-          for (int u = 0; u < NW; ++u) v += zp[(u * R + lrow) * 8];
-          if (N.bh) v += hbias[0];
-          const float vt = valid ? s_vt : v;
-          const float diff = v - vt;
-          const float ad = fabsf(diff);
-          if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
-          dzv = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
-          g_bh += dzv;
-        }
       }
-      dzs[lrow * DZP + la] = dzv;
+      // bf16 dz images (the head-backward operands; zero for padded heads and invalid rows)
+      const int lr0 = 16 * tile + 4 * qg + 2 * half;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        *reinterpret_cast<uint16_t *>(dzimg + (lr0 + i) * kDzRowBytes + 2 * n) = bf16_bits(dz[i]);
+      *reinterpret_cast<uint32_t *>(dztimg + n * kDzTPitch + 2 * lr0) = pack2(dz[0], dz[1]);
     }
     __syncthreads();
     STAMP_AT(4);
 
-    // ---- phase 5a: d2 = (dz . Wh) * act'(a2) (f32) -> bias grad, bf16 -> D2 image ----
+    // ---- phase 5: d2 = (dz . W_h) * act'(a2) on MFMA -> bias grad, D2 image; head dW ----
     OPAQUE_LANE();
     {
+      const bf16x8 wht = head_t_frag<H>(whb, w, lane);  // A operand: W_h^T of the wave's features
       float bsum[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        float dz[NH];
-        if constexpr (NH == 1) {
-          dz[0] = dzs[(32 * t + r) * DZP];
-        } else {
+      for (int t = 0; t < 2; ++t) {  // one row tile at a time (one live accumulator)
+        f32x16 acc[1];
 #pragma unroll
-          for (int a = 0; a < NH; a += 2) {
-            const float2 v = *reinterpret_cast<const float2 *>(dzs + (32 * t + r) * DZP + a);
-            dz[a] = v.x;
-            dz[a + 1] = v.y;
-          }
-        }
+        for (int e = 0; e < 16; ++e) acc[0][e] = 0.f;
+        acc[0] = mfma(wht, lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h), acc[0]);
+        mfma_drain(acc);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int f0 = 32 * w + 8 * g + 4 * h;
-          float sx = 0.f, sy = 0.f, sz = 0.f, sw = 0.f;
-#pragma unroll
-          for (int a = 0; a < NH; ++a) {
-            const float4 wv = *reinterpret_cast<const float4 *>(whs + a * H + f0);
-            sx = fmaf(dz[a], wv.x, sx);
-            sy = fmaf(dz[a], wv.y, sy);
-            sz = fmaf(dz[a], wv.z, sz);
-            sw = fmaf(dz[a], wv.w, sw);
+          float ya, yb, yc, yd;
+          if constexpr (F32A2) {
+            const float4 yv = *reinterpret_cast<const float4 *>(a2img + (32 * t + r) * L::A2P + 4 * (32 * w + 8 * g + 4 * h));
+            ya = yv.x, yb = yv.y, yc = yv.z, yd = yv.w;
+          } else {
+            const uint2 yv = *reinterpret_cast<const uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h);
+            ya = bf_lo(yv.x), yb = bf_hi(yv.x), yc = bf_lo(yv.y), yd = bf_hi(yv.y);
           }
-          const float4 yv = *reinterpret_cast<const float4 *>(lds + L::A2F + (32 * t + r) * L::A2P + 4 * f0);
-          const float d0 = act_backward(sx, yv.x, ACT);
-          const float d1 = act_backward(sy, yv.y, ACT);
-          const float d2 = act_backward(sz, yv.z, ACT);
-          const float d3 = act_backward(sw, yv.w, ACT);
+          const float d0 = act_backward(acc[0][4 * g], ya, ACT);
+          const float d1 = act_backward(acc[0][4 * g + 1], yb, ACT);
+          const float d2 = act_backward(acc[0][4 * g + 2], yc, ACT);
+          const float d3 = act_backward(acc[0][4 * g + 3], yd, ACT);
           bsum[4 * g] += d0;
           bsum[4 * g + 1] += d1;
           bsum[4 * g + 2] += d2;
           bsum[4 * g + 3] += d3;
           *reinterpret_cast<uint2 *>(d2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
               make_uint2(pack2(d0, d1), pack2(d2, d3));
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
       gb1 += rs16(bsum, lane);
     }
-    // ---- phase 5b: head dW += dz^T a2 (f32; thread = feature, row group) ----
-    OPAQUE_ROWS();
-    {
-      constexpr int RPG = R / RG;
-#pragma unroll 2
-      for (int rr = 0; rr < RPG; ++rr) {
-        const int row = rg * RPG + rr;
-        const float av = a2f[row * (L::A2P / 4) + fh];
-        if constexpr (NH == 1) {
-          gwh[0] = fmaf(dzs[row * DZP], av, gwh[0]);
-        } else {
+    // head dW += dz^T a2 over the chunk's 64 rows: wave w's two 16-feature tiles
 #pragma unroll
-          for (int a = 0; a < NH; a += 2) {
-            const float2 dv = *reinterpret_cast<const float2 *>(dzs + row * DZP + a);
-            gwh[a] = fmaf(dv.x, av, gwh[a]);
-            gwh[a + 1] = fmaf(dv.y, av, gwh[a + 1]);
-          }
+    for (int ks = 0; ks < R / 32; ++ks) {
+      const bf16x8 af = lds_b128(dztimg + (lane & 15) * kDzTPitch + 2 * (32 * ks + 8 * (lane >> 4)));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        bf16x8 bv;
+        if constexpr (F32A2) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = a2f[(32 * ks + 8 * (lane >> 4) + j) * (L::A2P / 4) + 32 * w + 16 * u + (lane & 15)];
+          bv = pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+        } else {
+          bv = tr_frag16(a2img, L::PITCH, 32 * ks, 32 * w + 16 * u, lane);
         }
+        ghw[u] = mfma16(af, bv, ghw[u]);
       }
     }
     __syncthreads();
@@ -683,7 +662,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     // reads and spills).  The dgrad weight ring is primed first so its L2 latency hides behind
     // this LDS-only phase.
     OPAQUE_LANE();
-    wring_prime<H>(N.w1bt + static_cast<int64_t>(32 * w + r) * H + 8 * h, ring);
+    wring_prime<H>(w_frag_base<H>(N.w1bt, w, lane), ring);
     xpre = load_x(chunk + G);  // next chunk's states: in flight until the next phase 0
 #pragma unroll 1
     for (int ks = 0; ks < R / 16; ++ks) {
@@ -699,7 +678,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     }
     STAMP_AT(6);
 
-    // ---- phase 6b: d1 = (W1^T d2) * act'(a1) -> D1 image (the A2F region is free) ----
+    // ---- phase 6b: d1 = (W1^T d2) * act'(a1) -> D1 image (the a2 region is free) ----
     OPAQUE_LANE();
     {
       f32x16 acc[2];
@@ -707,7 +686,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-      mlp_pass<H>(N.w1bt + static_cast<int64_t>(32 * w + r) * H + 8 * h, d2img, r, h, ring, acc);
+      mlp_pass<H>(w_frag_base<H>(N.w1bt, w, lane), d2img, r, h, ring, acc);
       STAMP_AT(7);
       OPAQUE_LANE();
       // act'(a1): ReLU needs only the sign, which the bf16 image keeps exactly; tanh / ELU
@@ -769,7 +748,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     STAMP_AT(9);
   }
 #undef STAMP_AT
-#undef OPAQUE_ROWS
 #undef OPAQUE_LANE
 
   // ================= epilogue: one partial-gradient slab per workgroup =================
@@ -777,10 +755,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   lane = tid & 63;
   r = lane & 31;
   h = lane >> 5;
-  lrow = tid >> 3;
-  la = tid & 7;
-  fh = tid % H;
-  rg = tid / H;
   if constexpr (STAMP) {
     if (tid0 == 0) {
       uint64_t *dst = stamps + (static_cast<int64_t>(z) * gridDim.x + blockIdx.x) * kStampSlots;
@@ -810,45 +784,54 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     if (N.b1) slab[N.off_b1 + f] = gb1;
     if (N.b0) slab[N.off_b0 + f] = gb0;
   }
-  // head dW: combine the RG row groups in order through LDS (the A2F region is free now)
-  float *red = reinterpret_cast<float *>(lds + L::A2F);  // [RG][8][H]
-#pragma unroll
-  for (int a = 0; a < NH; ++a) red[(rg * kFusedMaxAct + a) * H + fh] = gwh[a];
-  float *rrow = reinterpret_cast<float *>(lds + L::RED);   // [64 rows][8]
-  float *lrow_sh = reinterpret_cast<float *>(lds + L::DZ);  // [64 rows][8] (dz image is free)
-  rrow[lrow * 8 + la] = g_bh;
-  lrow_sh[lrow * 8 + la] = g_ls;
-  __syncthreads();
+  // head dW (a, f) row-major [A_net][H]
   const int na = ACTOR ? A : 1;
-  for (int i = tid; i < na * H; i += NT) {
-    const int a = i / H, f = i % H;
-    float s = 0.f;
-    for (int g = 0; g < RG; ++g) s += red[(g * kFusedMaxAct + a) * H + f];
-    slab[N.off_wh + i] = s;
-  }
-  if (tid < na && N.bh) {
-    float s = 0.f;
-    for (int row = 0; row < R; ++row) s += rrow[row * 8 + tid];
-    slab[N.off_bh + tid] = s;
-  }
-  if (ACTOR && tid >= 64 && tid < 64 + A) {
-    float s = 0.f;
-    for (int row = 0; row < R; ++row) s += lrow_sh[row * 8 + tid - 64];
-    slab[q.off_logstd + tid - 64] = s;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = 4 * (lane >> 4) + i;
+      if (a < na) slab[N.off_wh + static_cast<int64_t>(a) * H + 32 * w + 16 * u + (lane & 15)] = ghw[u][i];
+    }
+  // head bias / log-std / loss partials: per lane (head lane & 15) -> the 4 lane groups of a
+  // wave in a fixed xor order -> waves 0..7 in order through LDS
+  float *red = reinterpret_cast<float *>(lds + L::RED);  // [8][16][4]
+  {
+    g_bh += __shfl_xor(g_bh, 16, 64);
+    g_bh += __shfl_xor(g_bh, 32, 64);
+    g_ls += __shfl_xor(g_ls, 16, 64);
+    g_ls += __shfl_xor(g_ls, 32, 64);
+    g_loss += __shfl_xor(g_loss, 16, 64);
+    g_loss += __shfl_xor(g_loss, 32, 64);
+    if (lane < 16) {
+      float *dst = red + (w * 16 + lane) * 4;
+      dst[0] = g_bh;
+      dst[1] = g_ls;
+      dst[2] = g_loss;
+    }
   }
   __syncthreads();
-  rrow[lrow * 8 + la] = g_loss;
-  __syncthreads();
+  if (tid < na) {
+    float sb = 0.f, sl = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      sb += red[(v * 16 + tid) * 4];
+      sl += red[(v * 16 + tid) * 4 + 1];
+    }
+    if (N.bh) slab[N.off_bh + tid] = sb;
+    if (ACTOR) slab[q.off_logstd + tid] = sl;
+  }
   if (tid == 0) {
     float s = 0.f;
-    for (int row = 0; row < R; ++row) s += rrow[row * 8];
+#pragma unroll
+    for (int v = 0; v < NW; ++v) s += red[(v * 16) * 4 + 2];
     q.loss_part[2 * blockIdx.x + z] = s;
   }
 }
 
 template <int H, int ACT, int NA, bool STAMP>
 __global__ __launch_bounds__(NT, 1) void fused_update_kernel(FusedArgs q, uint64_t *stamps) {
-  __shared__ __attribute__((aligned(16))) char lds[Lds<H>::TOTAL];
+  __shared__ __attribute__((aligned(16))) char lds[Lds<H, ACT != PPO_ACT_RELU>::TOTAL];
   if (blockIdx.y == 0) fused_body<H, ACT, NA, true, STAMP>(q, q.net[0], lds, stamps);
   else fused_body<H, ACT, 1, false, STAMP>(q, q.net[1], lds, stamps);
 }

@@ -559,6 +559,7 @@ struct PolicyHeadArgs {
   uint64_t seed, offset;
   const uint64_t *offset_base;    // device counter added to offset (ppo_ctx_set_rng_counter)
   float *action, *logp, *value, *mean;
+  int bf16;                       // precision bf16: head operands rounded to bf16 (f32 accumulate)
 };
 
 // One wave per env row.  logp follows Normal.log_prob term by term:
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs q) {
 #pragma unroll
     for (int j = 0; j < HPL; ++j) {
       const int k = lane + 64 * j;
-      h[j] = (k < q.da) ? hr[k] : 0.f;
+      h[j] = (k < q.da) ? (q.bf16 ? bf16_round(hr[k]) : hr[k]) : 0.f;
     }
     float my_z = 0.f;
     for (int a = 0; a < q.act_dim; ++a) {
@@ -583,7 +584,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs q) {
 #pragma unroll
       for (int j = 0; j < HPL; ++j) {
         const int k = lane + 64 * j;
-        if (k < q.da) part = fmaf(h[j], w[k], part);
+        if (k < q.da) part = fmaf(h[j], q.bf16 ? bf16_round(w[k]) : w[k], part);
       }
       const float z = wave_sum(part);
       if (lane == a) my_z = z;
@@ -617,7 +618,8 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs q) {
 #pragma unroll
     for (int j = 0; j < HPL; ++j) {
       const int k = lane + 64 * j;
-      if (k < q.dc) part = fmaf(hr[k], q.wc[k], part);
+      if (k < q.dc)
+        part = q.bf16 ? fmaf(bf16_round(hr[k]), bf16_round(q.wc[k]), part) : fmaf(hr[k], q.wc[k], part);
     }
     const float v = wave_sum(part);
     if (lane == 0) q.value[row] = q.bc ? v + q.bc[0] : v;
@@ -644,7 +646,14 @@ struct UpdateHeadArgs {
   // critic b at off_bc
   float *hw_part;
   int hw_stride, off_ba, off_wc, off_bc;
+  int bf16;                      // precision bf16: every head product on bf16-rounded operands
 };
+
+// operand rounding of precision mode bf16 (identity in f32 mode)
+__device__ __forceinline__ float rb(float x, int bf16) { return bf16 ? bf16_round(x) : x; }
+__device__ __forceinline__ float4 rb4(float4 v, int bf16) {
+  return bf16 ? make_float4(bf16_round(v.x), bf16_round(v.y), bf16_round(v.z), bf16_round(v.w)) : v;
+}
 
 // Fast head: 4 lanes per row, 16 rows per wave pass, D = 16*NJ columns (actor and critic last
 // hidden widths equal).  Lane (row r = lane>>2, quarter qd = lane&3) holds float4 chunks
@@ -672,8 +681,8 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
   float *dzs = lps + 4 * 16 * kMaxAct;  // [4 waves][16 rows][kMaxAct] d(pre-tanh)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane >> 2, qd = lane & 3;
-  for (int i = tid; i < A * D; i += 256) wsh[i] = q.wa[i];
-  for (int i = tid; i < D; i += 256) wsh[A * D + i] = q.wc[i];
+  for (int i = tid; i < A * D; i += 256) wsh[i] = rb(q.wa[i], q.bf16);
+  for (int i = tid; i < D; i += 256) wsh[A * D + i] = rb(q.wc[i], q.bf16);
   __syncthreads();
   const int count = q.rows_n ? *q.rows_n : q.rows_max;
   const int r0 = static_cast<int>((static_cast<int64_t>(blockIdx.x) * count) / q.splits);
@@ -714,10 +723,11 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
 #pragma unroll
           for (int t = 0; t < NJ; ++t) {
             const float4 wv = w[4 * t + qd];
-            p = fmaf(h[t].x, wv.x, p);
-            p = fmaf(h[t].y, wv.y, p);
-            p = fmaf(h[t].z, wv.z, p);
-            p = fmaf(h[t].w, wv.w, p);
+            const float4 hb = rb4(h[t], q.bf16);
+            p = fmaf(hb.x, wv.x, p);
+            p = fmaf(hb.y, wv.y, p);
+            p = fmaf(hb.z, wv.z, p);
+            p = fmaf(hb.w, wv.w, p);
           }
           p += __shfl_xor(p, 1, 64);
           p += __shfl_xor(p, 2, 64);
@@ -779,7 +789,7 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
     for (int t = 0; t < NJ; ++t) {
       float4 s = make_float4(0, 0, 0, 0);
       for (int a = 0; a < A; ++a) {
-        const float dz = dz_row[a];
+        const float dz = rb(dz_row[a], q.bf16);
         const float4 wv = reinterpret_cast<const float4 *>(wsh + a * D)[4 * t + qd];
         s.x = fmaf(dz, wv.x, s.x);
         s.y = fmaf(dz, wv.y, s.y);
@@ -799,10 +809,11 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
 #pragma unroll
     for (int t = 0; t < NJ; ++t) {
       const float4 wv = wc[4 * t + qd];
-      p = fmaf(h[t].x, wv.x, p);
-      p = fmaf(h[t].y, wv.y, p);
-      p = fmaf(h[t].z, wv.z, p);
-      p = fmaf(h[t].w, wv.w, p);
+      const float4 hb = rb4(h[t], q.bf16);
+      p = fmaf(hb.x, wv.x, p);
+      p = fmaf(hb.y, wv.y, p);
+      p = fmaf(hb.z, wv.z, p);
+      p = fmaf(hb.w, wv.w, p);
     }
     p += __shfl_xor(p, 1, 64);
     p += __shfl_xor(p, 2, 64);
@@ -814,13 +825,14 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
     const float dv = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
     if (valid && qd == 0) q.dzc[j] = dv;
     float4 *gcrow = reinterpret_cast<float4 *>(q.gc + static_cast<int64_t>(j) * D);
+    const float dvb = rb(dv, q.bf16);
 #pragma unroll
     for (int t = 0; t < NJ; ++t) {
       const float4 wv = wc[4 * t + qd];
       if (valid)
         gcrow[4 * t + qd] =
-            make_float4(act_backward(dv * wv.x, h[t].x, q.act), act_backward(dv * wv.y, h[t].y, q.act),
-                        act_backward(dv * wv.z, h[t].z, q.act), act_backward(dv * wv.w, h[t].w, q.act));
+            make_float4(act_backward(dvb * wv.x, h[t].x, q.act), act_backward(dvb * wv.y, h[t].y, q.act),
+                        act_backward(dvb * wv.z, h[t].z, q.act), act_backward(dvb * wv.w, h[t].w, q.act));
     }
     if constexpr (FW) {
       // head dW += dz^T H over this pass's 16 rows (dz rows of invalid j are exactly 0 and are
@@ -836,22 +848,23 @@ __global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
         for (int u = 0; u < CH; ++u) {
           const int c = lane + 64 * u;
           if (c < 4 * NJ) {
-            const float4 ha4 = reinterpret_cast<const float4 *>(q.ha + jj * D)[c];
-            const float4 hc4 = reinterpret_cast<const float4 *>(q.hc + jj * D)[c];
+            const float4 ha4 = rb4(reinterpret_cast<const float4 *>(q.ha + jj * D)[c], q.bf16);
+            const float4 hc4 = rb4(reinterpret_cast<const float4 *>(q.hc + jj * D)[c], q.bf16);
 #pragma unroll
             for (int a = 0; a < AF; ++a) {
               if (a < A) {
-                const float dz = dzr[a];
+                const float dz = rb(dzr[a], q.bf16);
                 wa_acc[u][a].x = fmaf(dz, ha4.x, wa_acc[u][a].x);
                 wa_acc[u][a].y = fmaf(dz, ha4.y, wa_acc[u][a].y);
                 wa_acc[u][a].z = fmaf(dz, ha4.z, wa_acc[u][a].z);
                 wa_acc[u][a].w = fmaf(dz, ha4.w, wa_acc[u][a].w);
               }
             }
-            wc_acc[u].x = fmaf(dvr, hc4.x, wc_acc[u].x);
-            wc_acc[u].y = fmaf(dvr, hc4.y, wc_acc[u].y);
-            wc_acc[u].z = fmaf(dvr, hc4.z, wc_acc[u].z);
-            wc_acc[u].w = fmaf(dvr, hc4.w, wc_acc[u].w);
+            const float dvrb = rb(dvr, q.bf16);
+            wc_acc[u].x = fmaf(dvrb, hc4.x, wc_acc[u].x);
+            wc_acc[u].y = fmaf(dvrb, hc4.y, wc_acc[u].y);
+            wc_acc[u].z = fmaf(dvrb, hc4.z, wc_acc[u].z);
+            wc_acc[u].w = fmaf(dvrb, hc4.w, wc_acc[u].w);
           }
         }
         if (lane < A) b_acc += dzr[lane];
@@ -961,7 +974,7 @@ __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
 #pragma unroll
       for (int t = 0; t < HPL; ++t) {
         const int k = lane + 64 * t;
-        if (k < q.da) part = fmaf(h[t], w[k], part);
+        if (k < q.da) part = fmaf(rb(h[t], q.bf16), rb(w[k], q.bf16), part);
       }
       const float z = wave_sum(part);
       if (lane == a) my_z = z;
@@ -1006,7 +1019,8 @@ __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
       const int k = lane + 64 * t;
       if (k < q.da) {
         float s = 0.f;
-        for (int a = 0; a < A; ++a) s = fmaf(__shfl(dz, a, 64), q.wa[static_cast<int64_t>(a) * q.da + k], s);
+        for (int a = 0; a < A; ++a)
+          s = fmaf(rb(__shfl(dz, a, 64), q.bf16), rb(q.wa[static_cast<int64_t>(a) * q.da + k], q.bf16), s);
         gr[k] = act_backward(s, h[t], q.act);
       }
     }
@@ -1021,7 +1035,7 @@ __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
 #pragma unroll
     for (int t = 0; t < HPL; ++t) {
       const int k = lane + 64 * t;
-      if (k < q.dc) part = fmaf(h[t], q.wc[k], part);
+      if (k < q.dc) part = fmaf(rb(h[t], q.bf16), rb(q.wc[k], q.bf16), part);
     }
     float v = wave_sum(part);
     if (q.bc) v = v + q.bc[0];
@@ -1034,7 +1048,7 @@ __global__ __launch_bounds__(256) void update_head_kernel(UpdateHeadArgs q) {
 #pragma unroll
     for (int t = 0; t < HPL; ++t) {
       const int k = lane + 64 * t;
-      if (k < q.dc) gc[k] = act_backward(dv * q.wc[k], h[t], q.act);
+      if (k < q.dc) gc[k] = act_backward(rb(dv, q.bf16) * rb(q.wc[k], q.bf16), h[t], q.act);
     }
   }
   // fixed-order block reduction: waves 0..3
@@ -1801,6 +1815,7 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
   q.logp = logp_d;
   q.value = value_d;
   q.mean = mean_d;
+  q.bf16 = ctx->prec == PPO_PREC_BF16;
   const int hpl = hpl_for(std::max(q.da, q.dc));
   const int grid = ceil_div(n, 4);
   const int na = q.act_dim;
@@ -2138,6 +2153,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   u.off_ba = ctx->hw_off_ba;
   u.off_wc = ctx->hw_off_wc;
   u.off_bc = ctx->hw_off_bc;
+  u.bf16 = ctx->prec == PPO_PREC_BF16;
   // algorithmic FLOPs: head forward + dH_L (+ head dW when fused); bytes per row: read H_L
   // (actor, critic), action, 4 scalars + row index; write dH_L (actor, critic) and dz (A + 1)
   const TimRec rec{KC_UPDATE_HEAD,

@@ -180,16 +180,23 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
     """EnvironmentHelper whose physics runs on host cores (host_pool.HostPhysicsPool, P worker
     processes over env slices in shared memory), with the transfers the north_star names:
     actions device->host and observations / rewards / terminations host->device as
-    hipMemcpyAsync on a side stream between page-locked shared memory and the device.  Same
+    hipMemcpyAsync on side streams between page-locked shared memory and the device.  Same
     dynamics and values as :class:`SyntheticVecEnvHelper` (tested bit-for-bit); not
-    hipGraph-capturable (host work every step)."""
+    hipGraph-capturable (host work every step).
+
+    overlap=True splits the envs into two halves with their own worker groups and side streams,
+    and exposes the pipelined protocol PPOEngine's rollout drives (begin_half / release_half /
+    finish_half): while one half steps its physics on the host, the GPU runs the other half's
+    observe + act and both halves' DMAs, instead of serialising policy -> D2H -> physics -> H2D
+    for all envs every step."""
 
     graph_safe = False
 
     def __init__(self, streams: Optional[dict] = None, run: Optional[Run] = None,
                  device: Optional[torch.device] = None, seed: int = 0, p_terminate: float = 0.0,
-                 workers: int = 4):
+                 workers: int = 4, overlap: bool = True):
         self._workers = workers
+        self._overlap = overlap
         self.pool = None
         super().__init__(streams, run, device, seed, p_terminate)
 
@@ -200,14 +207,21 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
         if self.pool is not None:
             self.close()
         a = self.run.network_config.output_shape
+        n = self.base_obs.shape[1]
+        groups = 2 if (self._overlap and n >= 2 and self._workers >= 2) else 1
         self.pool = HostPhysicsPool(self.base_obs.cpu().numpy(), self.base_reward.cpu().numpy(),
-                                    self.base_terminated.cpu().numpy(), a, self._workers)
+                                    self.base_terminated.cpu().numpy(), a, self._workers,
+                                    groups=groups)
+        gb = self.pool.group_bounds
+        self.halves = [(gb[g], gb[g + 1]) for g in range(self.pool.groups)]
         self._registered = []
         for key in ("action", "obs", "reward", "term"):
             arr = self.pool.v[key]
             E.check(lib.ppo_host_register(arr.ctypes.data, arr.nbytes))
             self._registered.append(arr.ctypes.data)
-        self._side = torch.cuda.Stream(device=self.device)
+        self._sides = [torch.cuda.Stream(device=self.device) for _ in self.halves]
+        self._side = self._sides[0]
+        self._ev_d2h = [torch.cuda.Event() for _ in self.halves]
         self._lib = lib
 
     def close(self):
@@ -220,31 +234,65 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
         self.pool.close()
         self.pool = None
 
-    def _physics(self, action: torch.Tensor, reward_out: torch.Tensor,
-                 terminated_out: torch.Tensor) -> None:
-        t = self.t
-        if t >= self.horizon:
-            raise RuntimeError("host VecEnv: horizon exhausted; call reset_environment()")
-        v, lib, side = self.pool.v, self._lib, self._side
-        cur = torch.cuda.current_stream(self.device)
-        act = action.contiguous()
-        side.wait_stream(cur)  # the policy that produced the actions
-        s = side.cuda_stream
-        E.check(lib.ppo_memcpy_async(v["action"].ctypes.data, act.data_ptr(), v["action"].nbytes,
-                                     2, s))
-        side.synchronize()  # the workers need the actions on the host
-        self.pool.step(t)
-        E.check(lib.ppo_memcpy_async(self._obs_next.data_ptr(), v["obs"].ctypes.data,
-                                     v["obs"].nbytes, 1, s))
-        E.check(lib.ppo_memcpy_async(reward_out.data_ptr(), v["reward"].ctypes.data,
-                                     v["reward"].nbytes, 1, s))
-        E.check(lib.ppo_memcpy_async(terminated_out.data_ptr(), v["term"].ctypes.data,
-                                     v["term"].nbytes, 1, s))
-        cur.wait_stream(side)  # later kernels see the uploaded step
+    # ---- pipelined protocol (one half = one worker group + one side stream) -------------------
+    def begin_half(self, g: int, action_rows: torch.Tensor) -> None:
+        """Queue the D2H copy of half g's actions on its side stream, ordered after the work
+        already enqueued on the current stream (call right after that half's observe + act)."""
+        lo, hi = self.halves[g]
+        v, side = self.pool.v, self._sides[g]
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        act = action_rows.contiguous()
+        nbytes = (hi - lo) * v["action"].shape[1] * 4
+        E.check(self._lib.ppo_memcpy_async(v["action"][lo:hi].ctypes.data, act.data_ptr(), nbytes,
+                                           2, side.cuda_stream))
         act.record_stream(side)
+        self._ev_d2h[g].record(side)
+
+    def release_half(self, g: int, t: int) -> None:
+        """Host: wait for half g's actions to land, then start its workers on step t."""
+        if self.t >= self.horizon:
+            raise RuntimeError("host VecEnv: horizon exhausted; call reset_environment()")
+        self._ev_d2h[g].synchronize()
+        self.pool.release(g, t)
+
+    def finish_half(self, g: int, reward_rows: torch.Tensor,
+                    term_rows: torch.Tensor) -> torch.Tensor:
+        """Wait for half g's workers, queue its H2D copies on its side stream and make the
+        current stream wait for them; returns the half's (n_half, O) f64 observation rows."""
+        lo, hi = self.halves[g]
+        v, lib, side = self.pool.v, self._lib, self._sides[g]
+        self.pool.wait(g)
+        s = side.cuda_stream
+        o = v["obs"].shape[1]
+        obs_rows = self._obs_next[lo:hi]
+        E.check(lib.ppo_memcpy_async(obs_rows.data_ptr(), v["obs"][lo:hi].ctypes.data,
+                                     (hi - lo) * o * 8, 1, s))
+        E.check(lib.ppo_memcpy_async(reward_rows.data_ptr(), v["reward"][lo:hi].ctypes.data,
+                                     (hi - lo) * 8, 1, s))
+        E.check(lib.ppo_memcpy_async(term_rows.data_ptr(), v["term"][lo:hi].ctypes.data,
+                                     (hi - lo), 1, s))
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        return obs_rows
+
+    def end_step(self, reward_out: torch.Tensor, terminated_out: torch.Tensor) -> None:
+        """Bookkeeping once every half has finished step t."""
         self.timestep.reward = reward_out
         self.timestep.terminated = terminated_out
-        self.t = t + 1
+        self.t += 1
+
+    # ---- the unpipelined EnvironmentHelper.step protocol ---------------------------------------
+    def _physics(self, action: torch.Tensor, reward_out: torch.Tensor,
+                 terminated_out: torch.Tensor) -> None:
+        if self.t >= self.horizon:
+            raise RuntimeError("host VecEnv: horizon exhausted; call reset_environment()")
+        t = self.t
+        for g, (lo, hi) in enumerate(self.halves):
+            self.begin_half(g, action[lo:hi])
+        for g in range(len(self.halves)):
+            self.release_half(g, t)
+        for g, (lo, hi) in enumerate(self.halves):
+            self.finish_half(g, reward_out[lo:hi], terminated_out[lo:hi])
+        self.end_step(reward_out, terminated_out)
 
     def step(self, action: torch.Tensor, reward_out: Optional[torch.Tensor] = None,
              terminated_out: Optional[torch.Tensor] = None):

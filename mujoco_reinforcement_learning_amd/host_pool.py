@@ -10,10 +10,14 @@ page-locks (``ppo_host_register``):
 - next observations (N, O) f64, rewards (N,) f64 and terminations (N,) u8, read back by
   host->device DMAs.
 
-One step is then: DMA actions down, release the workers (a generation word in shared memory),
-every worker advances its slice and publishes its done word, DMA the results up.  Hand-offs spin
-on those words (yielding the core), so a step costs microseconds of synchronisation rather than a
-semaphore round trip.  Workers import numpy only and never touch the GPU.
+The workers form ``groups`` independent groups over contiguous env ranges (one control word each),
+so the caller can pipeline: while group 0 steps its envs on the host, the GPU runs group 1's
+policy and DMAs, and the other way round (environments.HostPhysicsVecEnvHelper, overlap mode).
+One group step is: DMA the group's actions down, release its workers (a generation word in shared
+memory), every worker advances its slice and publishes its done word, DMA the results up.
+Hand-offs spin on those words (yielding the core), so a step costs microseconds of
+synchronisation rather than a semaphore round trip.  Workers import numpy only and never touch
+the GPU.
 
 Physics: gymnasium / mujoco are not installed in this image, so the workers run the engine's
 synthetic dynamics (``environments.py`` docstring; bit-identical to
@@ -35,7 +39,7 @@ from typing import Dict, Tuple
 
 import numpy as np
 
-# ctrl words: step index, stop flag, step generation (bumped by the host to release a step)
+# ctrl words per group: step index, stop flag, step generation (bumped by the host to release it)
 _CTRL_T, _CTRL_STOP, _CTRL_GEN = 0, 1, 2
 
 
@@ -71,9 +75,9 @@ def _wait_change(word: np.ndarray, idx: int, old: int, stop: np.ndarray = None) 
         time.sleep(0)
 
 
-def _worker(wid: int, lo: int, hi: int, specs) -> None:
+def _worker(wid: int, grp: int, lo: int, hi: int, specs) -> None:
     shms, v = _attach(specs)
-    ctrl, done = v["ctrl"], v["done"]
+    ctrl, done = v["ctrl"][grp], v["done"]
     gen = 0
     try:
         while True:
@@ -91,10 +95,12 @@ class HostPhysicsPool:
     """P worker processes stepping env slices in shared memory (see the module docstring)."""
 
     def __init__(self, base_obs: np.ndarray, base_reward: np.ndarray, base_term: np.ndarray,
-                 act_dim: int, workers: int = 4):
+                 act_dim: int, workers: int = 4, groups: int = 1):
         t1, n, o = base_obs.shape
         self.num_envs, self.obs_dim, self.act_dim = n, o, act_dim
-        self.workers = max(1, min(int(workers), n))
+        self.groups = max(1, min(int(groups), n))
+        self.workers = max(self.groups, min(int(workers), n))
+        self.workers -= self.workers % self.groups  # equal worker count per group
         arrays = {
             "base_obs": (base_obs.shape, "float32"),
             "base_reward": (base_reward.shape, "float32"),
@@ -103,8 +109,8 @@ class HostPhysicsPool:
             "obs": ((n, o), "float64"),
             "reward": ((n,), "float64"),
             "term": ((n,), "uint8"),
-            "ctrl": ((3,), "int64"),
-            "done": ((max(1, min(int(workers), n)),), "int64"),
+            "ctrl": ((self.groups, 3), "int64"),
+            "done": ((self.workers,), "int64"),
         }
         self._shms, self.specs, self.v = [], {}, {}
         for key, (shape, dtype) in arrays.items():
@@ -118,35 +124,56 @@ class HostPhysicsPool:
         self.v["base_term"][...] = base_term.astype(np.uint8)
         self.v["ctrl"][...] = 0
         self.v["done"][...] = 0
-        self._gen = 0
+        self._gen = [0] * self.groups
         ctx = mp.get_context("spawn")  # never fork a process that may have initialised HIP
-        bounds = np.linspace(0, n, self.workers + 1).astype(int)
-        self._procs = [ctx.Process(target=_worker, daemon=True,
-                                   args=(i, int(bounds[i]), int(bounds[i + 1]), self.specs))
-                       for i in range(self.workers)]
+        self.group_bounds = [int(x) for x in np.linspace(0, n, self.groups + 1).astype(int)]
+        per = self.workers // self.groups
+        self._procs, self._group_workers = [], []
+        for g in range(self.groups):
+            lo, hi = self.group_bounds[g], self.group_bounds[g + 1]
+            wb = np.linspace(lo, hi, per + 1).astype(int)
+            ids = list(range(g * per, (g + 1) * per))
+            self._group_workers.append(ids)
+            for k, wid in enumerate(ids):
+                self._procs.append(ctx.Process(target=_worker, daemon=True,
+                                               args=(wid, g, int(wb[k]), int(wb[k + 1]),
+                                                     self.specs)))
         for p in self._procs:
             p.start()
         self._closed = False
 
-    def step(self, t: int) -> None:
-        """Advance all envs from step t (workers read v['action'], write obs / reward / term)."""
-        self._gen += 1
-        ctrl, done = self.v["ctrl"], self.v["done"]
+    def release(self, group: int, t: int) -> None:
+        """Start step t of the group's envs (its workers read v['action'] rows of the group)."""
+        self._gen[group] += 1
+        ctrl = self.v["ctrl"][group]
         ctrl[_CTRL_T] = t
-        ctrl[_CTRL_GEN] = self._gen  # release (after the step index and the actions)
+        ctrl[_CTRL_GEN] = self._gen[group]  # release (after the step index and the actions)
+
+    def wait(self, group: int) -> None:
+        """Block until the group's workers have published step results (obs / reward / term)."""
+        done, ids = self.v["done"], self._group_workers[group]
+        lo, hi = ids[0], ids[-1] + 1
+        gen = self._gen[group]
         deadline, spins = time.monotonic() + 60.0, 0
-        while int(done.min()) != self._gen:
+        while int(done[lo:hi].min()) != gen:
             spins += 1
             if spins % 4096 == 0 and (time.monotonic() > deadline or
                                       not all(p.is_alive() for p in self._procs)):
                 raise RuntimeError("host physics pool: a worker died or stalled")
             time.sleep(0)
 
+    def step(self, t: int) -> None:
+        """Advance all envs from step t (every group, then wait for all)."""
+        for g in range(self.groups):
+            self.release(g, t)
+        for g in range(self.groups):
+            self.wait(g)
+
     def close(self) -> None:
         if self._closed:
             return
         self._closed = True
-        self.v["ctrl"][_CTRL_STOP] = 1
+        self.v["ctrl"][:, _CTRL_STOP] = 1
         for p in self._procs:
             p.join(timeout=10)
             if p.is_alive():

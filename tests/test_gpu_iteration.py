@@ -63,7 +63,7 @@ def test_single_minibatch_update_tight(gpu):
 
 def test_bf16_iteration_matches_bf16_emulation(gpu):
     """precision="bf16" (BASELINE configs[1], fused kernels at 2x256): one full iteration
-    against the oracle with the same bf16 operand rounding (oracle.use_bf16_hidden_gemms) on the
+    against the oracle with the same bf16 operand rounding (oracle.use_bf16_gemms) on the
     same torch RNG streams.  Residual: f32 summation order, which occasionally flips the bf16
     rounding of an intermediate (1 bf16 ulp = 2^-8 relative), so the bars are relative: rollout
     values / actions within 2e-3 of their scale, the parameter update (post - init) within 0.5 %
@@ -72,7 +72,7 @@ def test_bf16_iteration_matches_bf16_emulation(gpu):
     algo, agent, ref, env, cfg = _setup(gpu, n=256, t=32, b=2048, epochs=2, hidden=(256, 256),
                                         precision="bf16", p_term=0.02)
     assert agent.engine.fused
-    R.use_bf16_hidden_gemms(ref)
+    R.use_bf16_gemms(ref)
     p0 = R.flat_params(ref).clone()
     mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg)
     for key in ("current_state_value", "action", "action_log_prob"):

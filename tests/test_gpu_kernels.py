@@ -352,7 +352,7 @@ def test_per_kernel_timing_records(gpu):
 def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b, obs, na):
     """precision="bf16": every hidden fc GEMM (forward, dgrad, wgrad) takes bf16-rounded operands
     with f32 accumulation.  Checked against torch autograd on the oracle nets with the same
-    operand rounding (oracle.use_bf16_hidden_gemms); the residual is f32 summation order plus
+    operand rounding (oracle.use_bf16_gemms); the residual is f32 summation order plus
     rare bf16 rounding-boundary flips of intermediates, so the bound is relative, 2e-3 of each
     tensor's largest gradient.  Against plain f32 autograd each tensor is within 10 % relative
     L2 (bf16 operand noise)."""
@@ -386,7 +386,7 @@ def test_minibatch_grad_bf16_matches_emulation(gpu, hidden, act, rows_total, b, 
         import copy
         r = copy.deepcopy(ref)
         if bf16:
-            R.use_bf16_hidden_gemms(r)
+            R.use_bf16_gemms(r)
         idx = rows.long()
         x = states[idx][:, None, :]
         _, dist = r.act(x, return_dist=True)

@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 SEGMENTS = ["0 X stage + W0 frags", "1 L0 fwd (+ W1 ring prime)", "2 L1 fwd MFMA pass",
-            "3 bias/act + A2F + head partial sums", "4 loss heads (per row)",
-            "5 d2 = dz.Wh (VALU) + D2 image + head dW (VALU)", "6 dW1 wgrad (MFMA, tr reads)",
+            "3 bias/act -> A2 image (+ row scalars to LDS)", "4 head z on MFMA + loss (waves 0-3)",
+            "5 d2 = dz.Wh + head dW (MFMA) + D2 image", "6 dW1 wgrad (MFMA, tr reads)",
             "7 dgrad MFMA pass", "8 dgrad epilogue (act', D1 image, bias)", "9 dW0 wgrad", "10 -"]
 
 
