@@ -218,7 +218,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       const bool act_lane = n < A;
       const float sd = act_lane ? expf(hs[8 + n]) : 1.f;
       const float lsd = act_lane ? logf(sd) : 0.f;
-      const float var = sd * sd;
+      const float i2var = 1.f / (2.f * (sd * sd));
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int env = row0 + 16 * tile + 4 * qg + 2 * half + i;
@@ -234,14 +234,15 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
           if (q.action) q.action[idx] = x;
           if (q.mean) q.mean[idx] = mu;
           const float d = x - mu;
-          lp = ((-(d * d)) / (2.f * var) - lsd) - kLogSqrt2Pi;
+          lp = ((-(d * d)) * i2var - lsd) - kLogSqrt2Pi;
         }
-        float s = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
-#pragma unroll
-        for (int aa = 0; aa < NH; ++aa) {
-          const float t = __shfl(lp, (lane & ~15) + aa, 64);
-          if (aa < A) s += t;
-        }
+        // Normal.log_prob(...).sum(1): fixed xor tree over the 16 head lanes (pads are 0), the
+        // same tree as the update kernel's loss head
+        float s = lp;
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
         if (n == 0 && env < q.n && q.logp) q.logp[env] = s;
       }
     } else {

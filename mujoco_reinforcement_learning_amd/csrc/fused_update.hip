@@ -300,10 +300,13 @@ struct Lds {
   static constexpr int A2BYTES = F32A2 ? R * A2P : R * PITCH;
   static constexpr int DZ = A2 + A2BYTES;                       // bf16 dz [64][16]
   static constexpr int DZT = DZ + R * kDzRowBytes;              // bf16 dz^T [16][64 + 8]
-  static constexpr int HS = DZT + 16 * kDzTPitch;               // f32 head bias, logstd, log std, var [16] each
-  static constexpr int SROW = HS + 64 * 4;                      // f32 [64][16] the chunk's row scalars
+  static constexpr int HS = DZT + 16 * kDzTPitch;               // f32 head bias, logstd, log std, 1/var, 1/(2 var) [16] each
+  static constexpr int SROW = HS + 80 * 4;                      // f32 [64][16] the chunk's row scalars
   static constexpr int RED = SROW;                              // epilogue: f32 [8 waves][16 heads][4]
-  static constexpr int TOTAL = SROW + R * kFusedSP * 4;
+  // ReLU: the W0 image (H x 32 bf16, x_off-swizzled 64-B rows) LDS-resident for the whole kernel
+  // (the tanh / ELU instantiations, with their f32 a2 region, read it from L2)
+  static constexpr int W0 = SROW + R * kFusedSP * 4;
+  static constexpr int TOTAL = W0 + (F32A2 ? 0 : H * 64);
   static_assert(TOTAL <= 163840, "LDS budget");
   static_assert(R * PITCH <= A2BYTES, "D1 image must fit in the a2 region");
 };
@@ -374,11 +377,19 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     (reinterpret_cast<float *>(lds + L::HS))[tid] =
         tid < 16 ? ((ok && N.bh) ? N.bh[a] : 0.f) : ((ACTOR && ok) ? q.logstd[a] : 0.f);
   }
-  if (tid < 16) {  // per-head Normal constants: log(std), var = std^2, std = exp(logstd)
+  if (tid < 16) {  // per-head Normal constants: log(std), 1/var, 1/(2 var); std = exp(logstd)
     const bool ok = ACTOR && tid < A;
     const float sd = ok ? expf(q.logstd[tid]) : 1.f;
+    const float var = sd * sd;
     (reinterpret_cast<float *>(lds + L::HS))[32 + tid] = ok ? logf(sd) : 0.f;
-    (reinterpret_cast<float *>(lds + L::HS))[48 + tid] = sd * sd;
+    (reinterpret_cast<float *>(lds + L::HS))[48 + tid] = 1.f / var;
+    (reinterpret_cast<float *>(lds + L::HS))[64 + tid] = 1.f / (2.f * var);
+  }
+  if constexpr (!F32A2) {
+    for (int i = tid; i < H * 4; i += NT) {  // 16-B chunk (row i / 4, chunk i % 4) of W0
+      const uint4 v = reinterpret_cast<const uint4 *>(N.w0b)[i];
+      *reinterpret_cast<uint4 *>(lds + L::W0 + x_off(i >> 2, i & 3)) = v;
+    }
   }
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
   __syncthreads();
@@ -425,7 +436,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   bf16x8 ring[PD + 1];
   for (; chunk < nchunks; chunk += G) {
     // ---- phase 0: X image; W0 fragments; the chunk's row scalars (actions, old log-prob,
-    //      advantage, value target: 64 x 64 B) issued for the head phase, staged at phase 1's end
+    //      advantage, value target: 64 x 64 B) issued for the head phase, staged at phase 2's end
     OPAQUE_LANE();
     *reinterpret_cast<uint2 *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xpre;
     const int srow_j = chunk * R + (tid >> 3);
@@ -434,8 +445,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         : make_uint2(0u, 0u);
     bf16x8 w0f[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      w0f[s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (F32A2)
+        w0f[s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
+      else
+        w0f[s] = lds_b128(lds + L::W0 + x_off(32 * w + r, 2 * s + h));
+    }
     __syncthreads();
     STAMP_AT(0);
 
@@ -468,7 +483,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         }
       }
     }
-    *reinterpret_cast<uint2 *>(lds + L::SROW + tid * 8) = srow_v;
     __syncthreads();
     STAMP_AT(1);
 
@@ -480,6 +494,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
+    *reinterpret_cast<uint2 *>(lds + L::SROW + tid0 * 8) = srow_v;  // landed during phases 1-2
     STAMP_AT(2);
 
     // ---- phase 3: bias + act -> a2 region; the head phase's row scalars issued here ----
@@ -526,7 +541,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       }
       mfma16_drain(zacc);
       const float zr[2] = {half ? zacc[2] : zacc[0], half ? zacc[3] : zacc[1]};
-      const float h_lsd = hbias[32 + n], h_var = hbias[48 + n];
+      const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
       float dz[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -544,14 +559,15 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
             const float mu = q.omv * y;
             const float x = valid ? sp[n] : mu;
             d = x - mu;
-            lp = ((-(d * d)) / (2.f * h_var) - h_lsd) - kLogSqrt2Pi;
+            lp = ((-(d * d)) * (0.5f * h_ivar) - h_lsd) - kLogSqrt2Pi;  // 0.5/var: exact scaling
           }
-          float logp = 0.f;  // sum over a = 0..A-1 in order (Normal.log_prob(...).sum(1))
-#pragma unroll
-          for (int a = 0; a < NH; ++a) {
-            const float t = __shfl(lp, (lane & ~15) + a, 64);
-            if (a < A) logp += t;
-          }
+          // Normal.log_prob(...).sum(1): fixed xor tree over the 16 head lanes (pads are 0), the
+          // same tree as the rollout's policy kernel
+          float logp = lp;
+          logp += __shfl_xor(logp, 1, 64);
+          logp += __shfl_xor(logp, 2, 64);
+          logp += __shfl_xor(logp, 4, 64);
+          logp += __shfl_xor(logp, 8, 64);
           const float old_lp = valid ? sp[A] : logp;
           const float adv = valid ? sp[A + 1] : 0.f;
           const float ratio = expf(logp - old_lp);
@@ -566,10 +582,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
           const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
           const float dlogp = valid ? dratio * ratio : 0.f;
           if (act_lane) {
-            const float dmu = dlogp * (d / h_var);
+            const float dmu = dlogp * (d * h_ivar);
             dz[i] = (dmu * q.omv) * (1.f - y * y);
             if (valid) {
-              g_ls += dlogp * ((d * d) / h_var - 1.f) - q.ent_coef * q.inv_ba;
+              g_ls += dlogp * ((d * d) * h_ivar - 1.f) - q.ent_coef * q.inv_ba;
               g_bh += dz[i];
             }
           }
