@@ -229,20 +229,22 @@ __device__ __forceinline__ void tail_gather(const TailArgs &t, int64_t blk, int 
   else reinterpret_cast<uint4 *>(t.srow + static_cast<int64_t>(j) * kFusedSP)[u - 4] = v;
 }
 
-__global__ __launch_bounds__(256) void step_tail_kernel(ReduceArgs r, TailArgs t, int red_blocks) {
+__global__ __launch_bounds__(kRedThreads) void step_tail_kernel(ReduceArgs r, TailArgs t, int red_blocks) {
   const int tid = threadIdx.x;
-  if (static_cast<int>(blockIdx.x) >= red_blocks) {
-    tail_gather(t, static_cast<int64_t>(blockIdx.x) - red_blocks, tid);
+  if (static_cast<int>(blockIdx.x) >= red_blocks) {  // 2 gather blocks of 256 rows' worth
+    const int64_t gb = 2 * (static_cast<int64_t>(blockIdx.x) - red_blocks) + (tid >> 8);
+    tail_gather(t, gb, tid & 255);
     return;
   }
   const AdamPackArgs &a = t.a;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + 4 * (tid & 63);
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRedParams + 4 * (tid % kRedGroups);
+  const bool lead = tid < kRedGroups;  // chunk 0: the threads that own the reduced sums
   float4 g4;
   if (t.reduce) {
     g4 = reduce_slab_block(r, blockIdx.x);
-    if ((tid >> 6) != 0 || i >= r.total) return;
+    if (!lead || i >= r.total) return;
   } else {
-    if ((tid >> 6) != 0 || i >= a.n) return;
+    if (!lead || i >= a.n) return;
     g4 = *reinterpret_cast<const float4 *>(a.g + i);
   }
   const float ns = i < a.n_actor ? (a.sched ? a.sched[0] : a.neg_a) : (a.sched ? a.sched[1] : a.neg_c);
@@ -892,10 +894,10 @@ int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, 
   PPO_REQUIRE(t.a.H % 4 == 0 && t.a.din >= 1 && t.a.din <= kFusedKX &&
                   (!t.reduce || r.total == t.a.n),
               "step tail: H=%d din=%d", t.a.H, t.a.din);
-  const int red_blocks = static_cast<int>(ceil_div(t.a.n, 256));
-  const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, 256));
-  launch_k(rec, step_tail_kernel, dim3(red_blocks + gather_blocks), dim3(256), 0, st, r, t,
-           red_blocks);
+  const int red_blocks = static_cast<int>(ceil_div(t.a.n, kRedParams));
+  const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, 2 * 256));
+  launch_k(rec, step_tail_kernel, dim3(red_blocks + gather_blocks), dim3(kRedThreads), 0, st, r,
+           t, red_blocks);
   PPO_LAUNCHED();
   return 0;
 }

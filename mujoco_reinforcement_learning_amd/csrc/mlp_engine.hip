@@ -1089,7 +1089,7 @@ __global__ void gather_states_kernel(const float *__restrict__ states, const int
 // ============================================================================================
 // Split-K reduction of the slabs into the flat gradient + loss scalars
 // ============================================================================================
-__global__ __launch_bounds__(256) void reduce_slabs_kernel(ReduceArgs q) {
+__global__ __launch_bounds__(kRedThreads) void reduce_slabs_kernel(ReduceArgs q) {
   (void)reduce_slab_block(q, blockIdx.x);
 }
 
@@ -1526,7 +1526,7 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   const int64_t P = ctx->total_params;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(q.G) * P,
                   4.0 * (static_cast<double>(q.G) + 1) * P},
-           reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);
+           reduce_slabs_kernel, dim3(ceil_div(P, kRedParams)), dim3(kRedThreads), 0, st, r);
   PPO_LAUNCHED();
   return 0;
 }
@@ -2325,7 +2325,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   r.loss_out = loss_d;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(splits) * P,
                   4.0 * (static_cast<double>(splits) + 1) * P},
-           reduce_slabs_kernel, dim3(ceil_div(P, 256)), dim3(256), 0, st, r);  // P % 16 == 0
+           reduce_slabs_kernel, dim3(ceil_div(P, kRedParams)), dim3(kRedThreads), 0, st, r);  // P % 16 == 0
   PPO_LAUNCHED();
   return 0;
 }

@@ -32,24 +32,31 @@ struct ReduceArgs {
   float *loss_out;
 };
 
-// Block = 64 float4 groups x 4 split-chunks (one wave per chunk): each thread sums a quarter of
-// the splits for 4 consecutive parameters (tensors start 16-float aligned, so a group never
-// straddles two tensors), then the chunks combine in a fixed order through LDS.  Block 0 also
-// reduces the per-split loss partials with a fixed-shape tree.  Deterministic run to run.
+// Block = kRedGroups float4 groups x kRedChunks split-chunks (512 threads): each thread sums
+// 1/kRedChunks of the splits for 4 consecutive parameters (tensors start 16-float aligned, so a
+// group never straddles two tensors), then the chunks combine in a fixed order through LDS -- 16
+// chunks of 8 slabs each keep 2x the loads in flight of a 4-chunk block, which is what the
+// 128-slab fused reduction (step_tail_kernel) is bound by.  Block 0 also reduces the per-split
+// loss partials with a fixed-shape tree.  Deterministic run to run; reduce_slabs_kernel and
+// step_tail_kernel share this exact order, so their results are bitwise equal.
 // Returns, on the chunk-0 threads (i < total), the final sums of parameters i..i+3 (also stored
 // to q.grad); other threads get zeros.
+constexpr int kRedGroups = 32;
+constexpr int kRedChunks = 16;
+constexpr int kRedThreads = kRedGroups * kRedChunks;
+constexpr int kRedParams = 4 * kRedGroups;  // parameters per block
 __device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t block) {
-  __shared__ float4 part[4][64];
-  __shared__ float lred[2][256];
-  const int tid = threadIdx.x, grp = tid & 63, chunk = tid >> 6;
-  const int64_t i = block * 256 + 4 * grp;
+  __shared__ float4 part[kRedChunks][kRedGroups];
+  __shared__ float lred[2][kRedThreads];
+  const int tid = threadIdx.x, grp = tid % kRedGroups, chunk = tid / kRedGroups;
+  const int64_t i = block * kRedParams + 4 * grp;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < q.total) {
     int s = 0;
     while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
     const ReduceSeg &g = q.seg[s];
     const int64_t off = i - g.dst;
-    const int k0 = (g.nsplit * chunk) / 4, k1 = (g.nsplit * (chunk + 1)) / 4;
+    const int k0 = (g.nsplit * chunk) / kRedChunks, k1 = (g.nsplit * (chunk + 1)) / kRedChunks;
     // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per
     // thread; the association is fixed, so the result is still deterministic run to run.
     if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
@@ -101,21 +108,24 @@ __device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t
   __syncthreads();
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
   if (chunk == 0 && i < q.total) {
-    const float4 a = part[0][grp], b = part[1][grp], c = part[2][grp], d = part[3][grp];
-    out = make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
-                      ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
+    out = part[0][grp];
+#pragma unroll
+    for (int c = 1; c < kRedChunks; ++c) {
+      const float4 b = part[c][grp];
+      out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
+    }
     *reinterpret_cast<float4 *>(q.grad + i) = out;
   }
   if (block == 0 && q.loss_out) {
     float la = 0.f, lc = 0.f;
-    for (int k = tid; k < q.loss_splits; k += 256) {
+    for (int k = tid; k < q.loss_splits; k += kRedThreads) {
       la += q.loss_part[2 * k];
       lc += q.loss_part[2 * k + 1];
     }
     lred[0][tid] = la;
     lred[1][tid] = lc;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = kRedThreads / 2; w > 0; w >>= 1) {
       if (tid < w) {
         lred[0][tid] += lred[0][tid + w];
         lred[1][tid] += lred[1][tid + w];
