@@ -141,19 +141,38 @@ __device__ __forceinline__ bf16x8 head_t_frag(const char *img, int w, int lane) 
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// Fixed-order reduce-scatter of 16 per-lane values over the 32 lanes of a wave half: after the
-// xor-16/8/4/2 halvings and a final xor-1 add, lane m holds the full sum of value
-// q(m) = 8*b4(m) + 4*b3(m) + 2*b2(m) + b1(m) (bit k of m: bk), duplicated on lanes m, m^1.
+// ---- cross-lane exchange on the VALU (DPP / v_permlane16_swap) instead of ds_bpermute ----------
+// Only lane patterns that are their own inverse are used (quad_perm xor, row_half_mirror,
+// row_mirror, row_ror:8), so a partner pair always exchanges with each other.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // lane i <-> 7 - i within each 8 lanes
+constexpr int kDppRor8 = 0x128;       // lane i <-> i ^ 8 within each 16-lane row
+// Sum over each 16-lane row, every lane ending with the same value: the adds are exactly those of
+// the xor-1/2/4/8 butterfly (the half-mirror partner of a lane holds the other quad's sum).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppRor8>(v);
+  return v;
+}
+
+// Fixed-order reduce-scatter of 16 per-lane values over the 32 lanes of a wave half.  Level 1
+// pairs lanes m, m^16 (v_permlane16_swap: X'+Y' = keep + received on every lane), level 2 m, m^8,
+// level 3 m, m^7 (half mirror: same b4/b3, opposite b2), level 4 m, m^2, then a final m, m^1 add:
+// lane m holds the full sum of value q(m) = 8*b4(m) + 4*b3(m) + 2*b2(m) + b1(m) (bit k of m: bk),
+// duplicated on lanes m, m^1.  All exchanges are VALU ops (no LDS round trips).
 __device__ __forceinline__ float rs16(float (&v)[16], int lane) {
   const int m = lane & 31;
-  {
-    const bool up = m & 16;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float send = up ? v[i] : v[i + 8];
-      const float keep = up ? v[i + 8] : v[i];
-      v[i] = keep + __shfl_xor(send, 16, 64);
-    }
+  for (int i = 0; i < 8; ++i) {  // rows 0/2 keep v[i] (+ partner's v[i]), rows 1/3 v[i + 8]
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    v[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
   }
   {
     const bool up = m & 8;
@@ -161,7 +180,7 @@ __device__ __forceinline__ float rs16(float (&v)[16], int lane) {
     for (int i = 0; i < 4; ++i) {
       const float send = up ? v[i] : v[i + 4];
       const float keep = up ? v[i + 4] : v[i];
-      v[i] = keep + __shfl_xor(send, 8, 64);
+      v[i] = keep + dpp_f<kDppRor8>(send);
     }
   }
   {
@@ -170,16 +189,16 @@ __device__ __forceinline__ float rs16(float (&v)[16], int lane) {
     for (int i = 0; i < 2; ++i) {
       const float send = up ? v[i] : v[i + 2];
       const float keep = up ? v[i + 2] : v[i];
-      v[i] = keep + __shfl_xor(send, 4, 64);
+      v[i] = keep + dpp_f<kDppHalfMirror>(send);
     }
   }
   {
     const bool up = m & 2;
     const float send = up ? v[0] : v[1];
     const float keep = up ? v[1] : v[0];
-    v[0] = keep + __shfl_xor(send, 2, 64);
+    v[0] = keep + dpp_f<kDppXor2>(send);
   }
-  return v[0] + __shfl_xor(v[0], 1, 64);
+  return v[0] + dpp_f<kDppXor1>(v[0]);
 }
 // feature (within a 32-wide tile, lane half h) whose sum rs16 leaves on lane m
 __device__ __forceinline__ int rs16_feature(int lane) {

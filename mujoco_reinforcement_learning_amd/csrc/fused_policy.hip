@@ -238,11 +238,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
         }
         // Normal.log_prob(...).sum(1): fixed xor tree over the 16 head lanes (pads are 0), the
         // same tree as the update kernel's loss head
-        float s = lp;
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
+        const float s = row16_sum(lp);
         if (n == 0 && env < q.n && q.logp) q.logp[env] = s;
       }
     } else {

@@ -17,6 +17,9 @@ constexpr int kFusedKX = 32;        // layer-0 input width padded for the 32x32x
 constexpr int kFusedSP = 16;        // per-row scalar pitch: actions[A], old_logp, adv, vtarget
 constexpr int kFusedMaxAct = 8;
 constexpr int kFusedMaxWG = 128;    // workgroups (= partial-gradient slabs) per net
+// phase-stamp slots per workgroup: 10 chunk-loop phases, prologue, epilogue (slab stores
+// drained), and the body's s_memrealtime ticks (100 MHz) for the cycle -> time calibration
+constexpr int kStampSlots = 13;
 
 struct FusedNet {
   const __bf16 *w0b;   // (H, 32)  bf16(W0), input columns >= din zero

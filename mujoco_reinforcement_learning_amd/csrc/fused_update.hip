@@ -326,7 +326,6 @@ __device__ __forceinline__ void mfma16_drain(f32x4 &acc) { asm volatile("s_nop 1
 
 // STAMP (diagnostic build, ppo_ctx_phase_stamps): wave 0 sums s_memtime deltas per phase segment
 // over the chunks and writes them per workgroup; the product kernel has STAMP = false.
-constexpr int kStampSlots = 11;
 
 // One net's workgroup: 8 waves; wave w owns feature tile w (features 32w..32w+31) in every
 // feature-tiled phase, dW1 tiles (o-tiles 2(w&3)+{0,1}) x (i-tiles 4(w>>2)+{0..3}), dW0 tile w and
@@ -368,6 +367,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   const int nchunks = (q.b + R - 1) / R;
   const int count = q.rows_n ? *q.rows_n : q.b;
 
+  uint64_t t_body0 = 0, t_real0 = 0;
+  if constexpr (STAMP) {
+    t_body0 = __builtin_amdgcn_s_memtime();
+    t_real0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
   stage_head_image<H>(whb, N.wh, ACTOR ? A : 1, tid, NT);
   for (int i = tid; i < 2 * H; i += NT) {
     const float *b = i < H ? N.b0 : N.b1;
@@ -427,6 +432,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 #pragma unroll
     for (int p = 0; p < kStampSlots; ++p) t_acc[p] = 0;
     t_prev = __builtin_amdgcn_s_memtime();
+    t_acc[10] = t_prev - t_body0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 #define STAMP_AT(p)                                       \
   if constexpr (STAMP) {                                  \
@@ -565,11 +572,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
           }
           // Normal.log_prob(...).sum(1): fixed xor tree over the 16 head lanes (pads are 0), the
           // same tree as the rollout's policy kernel
-          float logp = lp;
-          logp += __shfl_xor(logp, 1, 64);
-          logp += __shfl_xor(logp, 2, 64);
-          logp += __shfl_xor(logp, 4, 64);
-          logp += __shfl_xor(logp, 8, 64);
+          const float logp = row16_sum(lp);
           const float old_lp = valid ? sp[A] : logp;
           const float adv = valid ? sp[A + 1] : 0.f;
           const float ratio = expf(logp - old_lp);
@@ -773,13 +776,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   lane = tid & 63;
   r = lane & 31;
   h = lane >> 5;
-  if constexpr (STAMP) {
-    if (tid0 == 0) {
-      uint64_t *dst = stamps + (static_cast<int64_t>(z) * gridDim.x + blockIdx.x) * kStampSlots;
-#pragma unroll
-      for (int p = 0; p < kStampSlots; ++p) dst[p] = t_acc[p];
-    }
-  }
+  if constexpr (STAMP) t_prev = __builtin_amdgcn_s_memtime();
   float *slab = q.slabs + static_cast<int64_t>(blockIdx.x) * q.slab_stride;
   // dW1 (o, i) row-major [H][H]
 #pragma unroll
@@ -844,6 +841,20 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 #pragma unroll
     for (int v = 0; v < NW; ++v) s += red[(v * 16) * 4 + 2];
     q.loss_part[2 * blockIdx.x + z] = s;
+  }
+  if constexpr (STAMP) {  // after every wave's slab stores have drained
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    const uint64_t t_end = __builtin_amdgcn_s_memtime();
+    const uint64_t r_end = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    t_acc[11] = t_end - t_prev;
+    t_acc[12] = r_end - t_real0;
+    if (tid0 == 0) {
+      uint64_t *dst = stamps + (static_cast<int64_t>(z) * gridDim.x + blockIdx.x) * kStampSlots;
+#pragma unroll
+      for (int p = 0; p < kStampSlots; ++p) dst[p] = t_acc[p];
+    }
   }
 }
 

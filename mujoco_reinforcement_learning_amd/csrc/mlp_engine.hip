@@ -2334,7 +2334,7 @@ extern "C" int ppo_ctx_phase_stamps(ppo_ctx *ctx, int enable, uint64_t *host_out
   PPO_REQUIRE(ctx != nullptr, "ppo_ctx_phase_stamps: null ctx");
   PPO_REQUIRE(ctx->fused_ok, "ppo_ctx_phase_stamps: network shape has no fused kernel");
   PPO_HIP_TRY(hipSetDevice(ctx->device));
-  const int n = 2 * kFusedMaxWG * 11;
+  const int n = 2 * kFusedMaxWG * kStampSlots;
   if (enable) {
     if (!ctx->fstamps) PPO_HIP_TRY(hipMalloc(&ctx->fstamps, sizeof(uint64_t) * n));
     PPO_HIP_TRY(hipMemset(ctx->fstamps, 0, sizeof(uint64_t) * n));
@@ -2344,7 +2344,7 @@ extern "C" int ppo_ctx_phase_stamps(ppo_ctx *ctx, int enable, uint64_t *host_out
   ctx->fstamp_on = 0;
   if (!ctx->fstamps) return 0;
   PPO_HIP_TRY(hipDeviceSynchronize());
-  const int got = 2 * ctx->fstamp_g * 11;
+  const int got = 2 * ctx->fstamp_g * kStampSlots;
   if (host_out && max_values > 0)
     PPO_HIP_TRY(hipMemcpy(host_out, ctx->fstamps, sizeof(uint64_t) * std::min(got, max_values),
                           hipMemcpyDeviceToHost));

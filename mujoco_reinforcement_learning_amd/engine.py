@@ -200,14 +200,15 @@ class Engine:
 
     def phase_stamps(self, enable: bool):
         """Diagnostics: enable=True stamps the fused kernel's phases; enable=False returns the
-        last launch's per-phase cycle sums as a (2, G, 11) uint64 tensor (ppo_ctx_phase_stamps)."""
+        last launch's per-phase cycle sums as a (2, G, 13) uint64 tensor (ppo_ctx_phase_stamps;
+        slots 10/11 prologue/epilogue cycles, 12 the body's 100 MHz realtime ticks)."""
         if enable:
             check(self.lib.ppo_ctx_phase_stamps(self._ctx, 1, None, 0))
             return None
-        out = torch.zeros(2 * 128 * 11, dtype=torch.int64)
+        out = torch.zeros(2 * 128 * 13, dtype=torch.int64)
         n = self.lib.ppo_ctx_phase_stamps(self._ctx, 0, ctypes.c_void_p(out.data_ptr()), out.numel())
         check(min(n, 0))
-        return out[:n].view(2, -1, 11)
+        return out[:n].view(2, -1, 13)
 
     def timing_kernels(self) -> dict:
         """Same records per kernel instantiation, keyed by the rocprofv3 kernel name:

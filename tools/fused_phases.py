@@ -17,7 +17,8 @@ import torch  # noqa: E402
 SEGMENTS = ["0 X stage + W0 frags", "1 L0 fwd (+ W1 ring prime)", "2 L1 fwd MFMA pass",
             "3 bias/act -> A2 image (+ row scalars to LDS)", "4 head z on MFMA + loss (waves 0-3)",
             "5 d2 = dz.Wh + head dW (MFMA) + D2 image", "6 dW1 wgrad (MFMA, tr reads)",
-            "7 dgrad MFMA pass", "8 dgrad epilogue (act', D1 image, bias)", "9 dW0 wgrad", "10 -"]
+            "7 dgrad MFMA pass", "8 dgrad epilogue (act', D1 image, bias)", "9 dW0 wgrad",
+            "10 prologue (LDS images, constants)", "11 epilogue: slab stores drained"]
 
 
 def main():
@@ -45,9 +46,14 @@ def main():
         eng.minibatch_grad(states, actions, logp, adv, vt, rows, b, agent.flat_grad, loss,
                            0.9, 1.1, 1e-4, 1 / b, 1 / (b * 6))
         st = eng.phase_stamps(False).double()
-        res = {"actor": st[0].mean(0).tolist(), "critic": st[1].mean(0).tolist(),
-               "actor_total_max": float(st[0].sum(1).max()),
-               "critic_total_max": float(st[1].sum(1).max())}
+        cyc, real = st[..., :12], st[..., 12]
+        res = {"actor": cyc[0].mean(0).tolist(), "critic": cyc[1].mean(0).tolist(),
+               "actor_total_max": float(cyc[0].sum(1).max()),
+               "critic_total_max": float(cyc[1].sum(1).max()),
+               # s_memtime / s_memrealtime x 100 MHz: the shader clock during the launch
+               "clock_mhz": float((cyc.sum(-1) / real.clamp_min(1)).median() * 100.0),
+               "body_us_max": float(real.max()) / 100.0}
+    print(f"clock {res['clock_mhz']:.0f} MHz, slowest workgroup body {res['body_us_max']:.1f} us")
     for k in ("actor", "critic"):
         tot = sum(res[k])
         print(f"{k}: total {tot:.0f} cycles/WG (max {res[k + '_total_max']:.0f})")
