@@ -44,6 +44,8 @@ extern "C" {
 
 /* NetworkConfig.activation_class (features.py:41-54; main.py uses ReLU). */
 enum { PPO_ACT_RELU = 0, PPO_ACT_TANH = 1, PPO_ACT_ELU = 2 };
+/* No activation: the LSTM gate projections and the critic's output layer. */
+#define PPO_ACT_IDENTITY 3
 
 /* Shapes of the actor-critic (models/linear/actor.py:9-23, models/critic.py:6-20,
  * network_block_creator.py:24-72).  The critic flattens the (N, W, O) state like the actor. */
@@ -300,6 +302,60 @@ int ppo_synthetic_test_step(const float *base_obs_d, const float *base_reward_d,
                             const float *action_d, int o, int a, int w, double *window_d,
                             int32_t *step_d, double *reward_sum_d, uint8_t *term_out_d,
                             void *stream);
+
+/* ---- Windowed BiLSTM actor-critic --------------------------------
+ * models/lstm/lstm_actor.py:9-48 + lstm_critic.py:9-41, the PPOAgent binding of
+ * entities/agents/ppo_agent.py:2-3, selected by NetworkConfig.feature_extractor == "LSTM"
+ * (features.py:53).  Actor: nn.LSTM(O, latent, actor_layers, bidirectional, batch_first) over the
+ * (B, W, O) window, act() on its outputs flattened to (B, W*2*latent), mean = tanh(MLP_mu(.)),
+ * std = 0.2*exp(tanh(MLP_ls(.))) per row (B, A) -- the reference's repeat_interleave at
+ * lstm_actor.py:48 returns (B, B, A), the shape bug this engine fixes.  Critic: a one-layer
+ * BiLSTM, value = MLP_v(act(Y[:, W-1, :])).  Every MLP is a NetworkBlock with
+ * hidden[0..n_hidden-1] and act() between layers (network_block_creator.py:24-86).
+ * Flat parameters: torch parameters() order of LSTMActor then LSTMCritic (nn.LSTM: per layer and
+ * direction w_ih[4L][in], w_hh[4L][L], b_ih[4L], b_hh[4L]; gates i, f, g, o), each tensor
+ * 16-float aligned (ppo_lstm_param_layout). */
+typedef struct ppo_lstm_cfg {
+  int32_t obs_dim;          /* NetworkConfig.input_shape (O) */
+  int32_t window;           /* EnvironmentConfig.window_length (W) */
+  int32_t act_dim;          /* NetworkConfig.output_shape (A), <= 32 */
+  int32_t activation;       /* PPO_ACT_* (NetworkConfig.activation_class) */
+  int32_t use_bias;         /* NetworkConfig.use_bias (the MLPs; nn.LSTM always has biases) */
+  int32_t latent;           /* NetworkConfig.feature_extractor_latent_size, multiple of 4 */
+  int32_t actor_layers;     /* NetworkConfig.num_feature_extractor_layers (critic: 1) */
+  int32_t n_hidden;         /* NetworkConfig.num_linear_layers */
+  int32_t hidden[PPO_MAX_LAYERS];  /* NetworkConfig.linear_hidden_shapes */
+  int32_t max_rows;         /* workspace rows = max(num_envs, minibatch) */
+} ppo_lstm_cfg;
+typedef struct ppo_lstm_ctx ppo_lstm_ctx;
+
+/* Replaces PPOAgent.initialize_networks' model construction (ppo_agent.py:11-13). */
+int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm_ctx **out);
+int ppo_lstm_ctx_destroy(ppo_lstm_ctx *ctx);
+/* Offsets (floats) of every parameter tensor in torch order; *total, *n_actor (the actor's
+ * share, for the two Adam groups).  Returns the tensor count. */
+int ppo_lstm_param_layout(const ppo_lstm_ctx *ctx, int64_t *offsets, int max_tensors,
+                          int64_t *total, int64_t *n_actor);
+int ppo_lstm_bind_params(ppo_lstm_ctx *ctx, float *params_d);
+int ppo_lstm_set_precision(ppo_lstm_ctx *ctx, int prec);
+/* LSTMActor.forward + LSTMCritic.forward (lstm_actor.py:41-48, lstm_critic.py:33-41) on
+ * state_d[n][W*O]: mean[n][A], std[n][A], value[n]; optional copies of the top LSTM layers'
+ * outputs [n][W][2*latent] (nullable outputs are skipped). */
+int ppo_lstm_forward(ppo_lstm_ctx *ctx, const float *state_d, int n, float *mean_d, float *std_d,
+                     float *value_d, float *actor_lstm_out_d, float *critic_lstm_out_d,
+                     void *stream);
+/* PPO rollout step with the LSTM agent (ppo.py:22-26): action = eps*std + mean (eps from
+ * eps_d, or Philox(seed, offset + i) when eps_d is null), log_prob summed over actions, V(s). */
+int ppo_lstm_policy_step(ppo_lstm_ctx *ctx, const float *state_d, int n, const float *eps_d,
+                         uint64_t seed, uint64_t offset, float *action_d, float *logp_d,
+                         float *value_d, void *stream);
+/* One minibatch of ppo.py:108-135 for the LSTM agent: the same arguments and gradient layout
+ * contract as ppo_minibatch_grad (rows_d index the rollout rows), grad_d = the flat gradient. */
+int ppo_lstm_minibatch_grad(ppo_lstm_ctx *ctx, const float *states_d, const float *actions_d,
+                            const float *logp_d, const float *adv_d, const float *vt_d,
+                            const int32_t *rows_d, int b, float *grad_d, float *loss_d,
+                            float clip_lo, float clip_hi, float entropy_coef, float inv_b,
+                            float inv_ba, void *stream);
 
 #ifdef __cplusplus
 }

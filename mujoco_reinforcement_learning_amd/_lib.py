@@ -34,6 +34,22 @@ class NetCfg(ctypes.Structure):
     ]
 
 
+class LstmCfg(ctypes.Structure):
+    """``ppo_lstm_cfg`` (include/ppo_engine.h)."""
+    _fields_ = [
+        ("obs_dim", c_int32),
+        ("window", c_int32),
+        ("act_dim", c_int32),
+        ("activation", c_int32),
+        ("use_bias", c_int32),
+        ("latent", c_int32),
+        ("actor_layers", c_int32),
+        ("n_hidden", c_int32),
+        ("hidden", c_int32 * PPO_MAX_LAYERS),
+        ("max_rows", c_int32),
+    ]
+
+
 _SIGNATURES = {
     "ppo_abi_version": (c_int, []),
     "ppo_last_error": (ctypes.c_char_p, []),
@@ -100,6 +116,19 @@ _SIGNATURES = {
     "ppo_adam_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, c_void_p]),
+    # windowed BiLSTM actor-critic (bilstm.hip)
+    "ppo_lstm_ctx_create": (c_int, [POINTER(LstmCfg), c_int, POINTER(c_void_p)]),
+    "ppo_lstm_ctx_destroy": (c_int, [c_void_p]),
+    "ppo_lstm_param_layout": (c_int, [c_void_p, POINTER(c_int64), c_int, POINTER(c_int64),
+                                      POINTER(c_int64)]),
+    "ppo_lstm_bind_params": (c_int, [c_void_p, c_void_p]),
+    "ppo_lstm_set_precision": (c_int, [c_void_p, c_int]),
+    "ppo_lstm_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
+    "ppo_lstm_policy_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_uint64,
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ppo_lstm_minibatch_grad": (c_int, [c_void_p] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]
+                                + [ctypes.c_float] * 5 + [c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -123,6 +123,18 @@ class ExponentialLRFacade:
         self.last_epoch = sd["last_epoch"]
 
 
+def make_agent(run: Optional[Run] = None, device: Optional[torch.device] = None,
+               max_rows: Optional[int] = None):
+    """The agent NetworkConfig.feature_extractor selects: "LSTM" -> the reference PPOAgent's
+    LSTM actor / critic (ppo_agent.py:2-3; lstm.LSTMEngineAgent), anything else -> the MLP
+    actor-critic of north_star (PPOEngineAgent)."""
+    run = run or Run.instance()
+    if str(getattr(run.network_config, "feature_extractor", "MLP")).upper() == "LSTM":
+        from .lstm import LSTMEngineAgent
+        return LSTMEngineAgent(run, device, max_rows)
+    return PPOEngineAgent(run, device, max_rows)
+
+
 class PPOEngineAgent:
     """PPOAgent on the MI355X engine."""
 

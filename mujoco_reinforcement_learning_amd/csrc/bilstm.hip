@@ -1,0 +1,965 @@
+// Windowed BiLSTM actor-critic on gfx950, behind the ppo_lstm_* C-ABI.
+//
+// Reference: models/lstm/lstm_actor.py:9-48 and lstm_critic.py:9-41 -- torch.nn.LSTM(O, Hf,
+// num_layers, bidirectional=True, batch_first=True) over the (B, W, O) observation window, the
+// activation on its outputs, then NetworkBlock MLPs (network_block_creator.py:24-86):
+//   actor : features = act(Y.reshape(B, W*2Hf));  mean = tanh(MLP_mu(features));
+//           std = 0.2 * exp(tanh(MLP_ls(features)))  -- shape (B, A): the reference's
+//           repeat_interleave(std[None], B, 0) (lstm_actor.py:48) makes it (B, B, A), which
+//           torch.distributions.Normal then cannot pair with a (B, A) mean; the engine returns
+//           the per-row std the formula means (the std-shape fix SURVEY.md s0 asks for).
+//   critic: one-layer BiLSTM, value = MLP_v(act(Y[:, W-1, :]))
+// and the PPO losses of ppo.py:93-148 with that per-row std (Normal.log_prob / entropy).
+//
+// One LSTM layer, both directions in every launch (GemmBatch problem z = direction):
+//   Gx = X W_ih^T + b_ih           one GEMM over the B*W rows          (gemm.h FWD, identity)
+//   per step s (t = s forward, W-1-s reverse):
+//     Gh = h_prev W_hh^T + b_hh    one GEMM over the B rows (skipped at s = 0: h_prev = 0)
+//     lstm_cell_fwd_kernel         gates = Gh + Gx (torch: linear_hh(hx).add_(igates)),
+//                                  i,f,o = sigmoid, g = tanh, c = f*c_prev + i*g, h = o*tanh(c);
+//                                  keeps the gate activations (over Gx), c, h and h_prev
+//   backward (BPTT), per step in reverse processing order:
+//     dh_rec = dG(next step) W_hh  one GEMM over the B rows
+//     lstm_cell_bwd_kernel         torch's elementwise backward forms (sigmoid: g*(1-y)*y,
+//                                  tanh: g*(1-y*y)); dG overwrites the gate activations
+//   dW_ih = dG^T X, dW_hh = dG^T H_prev (split-K slabs; bias grads = column sums of dG), and for
+//   stacked layers dX = sum_d dG_d W_ih_d.
+// GEMMs are the engine's MFMA templates (exact-f32 v_mfma_f32_32x32x2_f32 by default, bf16
+// operands in PPO_PREC_BF16); the slabs reduce with reduce_slab_block in a fixed order.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "common.h"
+#include "gemm.h"
+#include "reduce_slabs.h"
+#include "timing.h"
+
+namespace ppo {
+namespace lstm {
+
+constexpr int kMaxA = 32;
+constexpr int kSplits = 32;           // split-K slabs of the weight gradients
+constexpr int64_t kAlign = 16;        // floats: every flat tensor starts 64-B aligned
+constexpr int64_t kWsAlign = 64;
+
+static inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+struct LstmLayer {
+  int in;
+  int64_t w_ih[2], w_hh[2], b_ih[2], b_hh[2];  // flat offsets, direction d
+};
+struct LstmNet {
+  int layers, hidden;
+  LstmLayer l[PPO_MAX_LAYERS];
+};
+struct MlpLayer {
+  int in, out, act;
+  int64_t w, b;  // b < 0: no bias
+};
+struct Mlp {
+  int n;  // layers incl. the output layer
+  MlpLayer l[PPO_MAX_LAYERS + 1];
+};
+
+// ---- kernels --------------------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+struct CellArgs {
+  float *g;            // [B*W][2][4H]: Gx in, gate activations out (dG in the backward)
+  const float *gh;     // [B][2][4H] recurrent projection incl. b_hh (nullptr at the first step)
+  const float *b_hh[2];
+  float *c;            // [B*W][2H] cell states
+  float *y;            // [B*W][2H] layer output h
+  float *hp;           // [B*W][2H] h_prev (zeros at each direction's first step)
+  float *feat;         // optional act(h): mode 1 -> [B*W][2H] (actor), mode 2 -> [B][2H] at t=W-1
+  int feat_mode, act;
+  int b, w, h, s;
+};
+
+__global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int H = q.h, W = q.w;
+  if (i >= static_cast<int64_t>(q.b) * 2 * H) return;
+  const int j = static_cast<int>(i % H);
+  const int d = static_cast<int>((i / H) & 1);
+  const int64_t b = i / (2 * H);
+  const bool first = q.s == 0;
+  const int t = d == 0 ? q.s : W - 1 - q.s;
+  const int tp = d == 0 ? t - 1 : t + 1;
+  float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
+  float pre[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float hg = first ? q.b_hh[d][k * H + j] : q.gh[b * (8 * H) + d * (4 * H) + k * H + j];
+    pre[k] = hg + g[k * H + j];
+  }
+  const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
+              og = sigmoidf_(pre[3]);
+  const int64_t o = (b * W + t) * (2 * H) + d * H + j;
+  const int64_t op = (b * W + tp) * (2 * H) + d * H + j;
+  const float cp = first ? 0.f : q.c[op];
+  const float c = fg * cp + ig * gg;  // (forgetgate * cx).add_(ingate * cellgate)
+  const float h = og * tanhf(c);
+  g[j] = ig;
+  g[H + j] = fg;
+  g[2 * H + j] = gg;
+  g[3 * H + j] = og;
+  q.c[o] = c;
+  q.y[o] = h;
+  q.hp[o] = first ? 0.f : q.y[op];
+  if (q.feat_mode == 1) q.feat[o] = act_forward(h, q.act);
+  else if (q.feat_mode == 2 && t == W - 1) q.feat[b * (2 * H) + d * H + j] = act_forward(h, q.act);
+}
+
+struct CellBwdArgs {
+  float *g;            // gate activations in, dG out
+  const float *c;
+  const float *dy;     // [B*W][2H] gradient of the layer output (nullable rows handled by dy_mode)
+  const float *dy_last;  // mode 2: [B][2H] gradient of h at t = W-1 only
+  int dy_mode;         // 1: dy full, 2: dy_last
+  const float *dh_rec; // [B][2H] recurrent gradient (nullptr at s = 0)
+  float *dcarry;       // [B][2H] dc flowing to the previous forward step
+  int b, w, h, s;
+};
+
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int H = q.h, W = q.w;
+  if (i >= static_cast<int64_t>(q.b) * 2 * H) return;
+  const int j = static_cast<int>(i % H);
+  const int d = static_cast<int>((i / H) & 1);
+  const int64_t b = i / (2 * H);
+  const int t = d == 0 ? W - 1 - q.s : q.s;          // reverse of the forward processing order
+  const bool first_fwd = d == 0 ? t == 0 : t == W - 1;
+  const int tp = d == 0 ? t - 1 : t + 1;
+  const int64_t o = (b * W + t) * (2 * H) + d * H + j;
+  const int64_t r = b * (2 * H) + d * H + j;
+  float dh = 0.f;
+  if (q.dy_mode == 1) dh = q.dy[o];
+  else if (t == W - 1) dh = q.dy_last[r];
+  if (q.s > 0) dh += q.dh_rec[r];
+  const float dc_in = q.s > 0 ? q.dcarry[r] : 0.f;
+  float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
+  const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
+  const float c = q.c[o];
+  const float cp = first_fwd ? 0.f : q.c[(b * W + tp) * (2 * H) + d * H + j];
+  const float tc = tanhf(c);
+  const float d_o = dh * tc;                          // hy = outgate * cy.tanh()
+  const float d_tc = dh * og;
+  const float dc = d_tc * (1.f - tc * tc) + dc_in;    // tanh_backward, + the next step's dcx
+  const float d_f = dc * cp, d_i = dc * gg, d_g = dc * ig;
+  q.dcarry[r] = dc * fg;
+  g[j] = (d_i * (1.f - ig)) * ig;                     // sigmoid_backward: g * (1 - y) * y
+  g[H + j] = (d_f * (1.f - fg)) * fg;
+  g[2 * H + j] = d_g * (1.f - gg * gg);               // tanh_backward
+  g[3 * H + j] = (d_o * (1.f - og)) * og;
+}
+
+__global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) {
+  (void)reduce_slab_block(q, blockIdx.x);
+}
+
+__global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
+                                        const int32_t *__restrict__ rows, int b, int din,
+                                        float *__restrict__ xg) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(b) * din) return;
+  const int64_t j = i / din;
+  xg[i] = states[static_cast<int64_t>(rows[j]) * din + (i - j * din)];
+}
+
+__global__ void add_inplace_kernel(float *__restrict__ a, const float *__restrict__ b, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) a[i] += b[i];
+}
+
+// act_backward against the layer output, in place on dy (the feature activation of the LSTM
+// outputs, lstm_actor.py:45 / lstm_critic.py:37)
+__global__ void act_backward_inplace_kernel(float *__restrict__ dy, const float *__restrict__ y,
+                                            int64_t n, int act) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) dy[i] = act_backward(dy[i], y[i], act);
+}
+
+// ---- heads ----------------------------------------------------------------------------------
+struct HeadArgs {
+  const float *mean;   // [B][A] tanh(MLP_mu)
+  const float *u;      // [B][A] tanh(MLP_ls)
+  const float *value;  // [B] critic output
+  float *std_out;      // [B][A] (forward / policy step)
+  // policy step
+  const float *eps;
+  uint64_t seed, offset;
+  float *action, *logp_out, *value_out;
+  // update
+  const float *actions, *old_logp, *adv, *vt;
+  const int32_t *rows;
+  float *dzm, *dzs, *dv;  // [B][A], [B][A], [B]
+  float *row_part;        // [B][3]: min(s1, s2), sum_a entropy, huber
+  float clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
+  int b, a;
+};
+
+// Normal(mean, std) with std = 0.2 * exp(u) (lstm_actor.py:47): sample (torch.normal: eps*std +
+// mean), log_prob summed over actions (ppo.py:26), critic value passthrough.
+__global__ __launch_bounds__(256) void lstm_policy_head_kernel(HeadArgs q) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= q.b) return;
+  const int A = q.a;
+  float lp = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const int64_t idx = static_cast<int64_t>(n) * A + k;
+    const float mu = q.mean[idx];
+    const float sd = 0.2f * expf(q.u[idx]);
+    if (q.std_out) q.std_out[idx] = sd;
+    if (!q.action) continue;
+    const float e = q.eps ? q.eps[idx] : philox_normal_at(q.seed, q.offset + idx);
+    const float x = e * sd + mu;
+    q.action[idx] = x;
+    const float d = x - mu;
+    lp += (((-(d * d)) / (2.f * (sd * sd))) - logf(sd)) - kLogSqrt2Pi;
+  }
+  if (q.logp_out) q.logp_out[n] = lp;
+  if (q.value_out) q.value_out[n] = q.value[n];
+}
+
+// ppo.py:108-135 per minibatch row: new log-prob, ratio, clipped surrogate, entropy, Huber; the
+// gradients w.r.t. the two actor MLPs' pre-tanh outputs and the critic output.
+__global__ __launch_bounds__(256) void lstm_update_head_kernel(HeadArgs q) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= q.b) return;
+  const int A = q.a;
+  const int64_t src = q.rows[n];
+  float lp = 0.f, ent = 0.f;
+  float mu[kMaxA], sd[kMaxA], dd[kMaxA];
+  for (int k = 0; k < A; ++k) {
+    const int64_t idx = static_cast<int64_t>(n) * A + k;
+    mu[k] = q.mean[idx];
+    sd[k] = 0.2f * expf(q.u[idx]);
+    dd[k] = q.actions[src * A + k] - mu[k];
+    const float ls = logf(sd[k]);
+    lp += (((-(dd[k] * dd[k])) / (2.f * (sd[k] * sd[k]))) - ls) - kLogSqrt2Pi;
+    ent += kEntropyConst + ls;
+  }
+  const float adv = q.adv[src];
+  const float ratio = expf(lp - q.old_logp[src]);
+  const float s1 = ratio * adv;
+  const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+  const float s2 = cl * adv;
+  const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+  const float gg = -q.inv_b;
+  const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+  const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+  const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+  const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+  const float dlogp = dratio * ratio;
+  for (int k = 0; k < A; ++k) {
+    const int64_t idx = static_cast<int64_t>(n) * A + k;
+    const float var = sd[k] * sd[k];
+    const float dmu = dlogp * (dd[k] / var);
+    // d/dstd of -(d^2)/(2 var) - log(std): d^2/std^3 - 1/std; entropy mean: -ent_coef/(B*A*std)
+    const float dstd = dlogp * ((dd[k] * dd[k]) / (var * sd[k]) - 1.f / sd[k]) -
+                       q.ent_coef * q.inv_ba / sd[k];
+    const float du = dstd * sd[k];  // std = 0.2 * exp(u)
+    const float uu = q.u[idx];
+    q.dzm[idx] = dmu * (1.f - mu[k] * mu[k]);
+    q.dzs[idx] = du * (1.f - uu * uu);
+  }
+  const float v = q.value[n];
+  const float diff = v - q.vt[src];
+  const float ad = fabsf(diff);
+  q.dv[n] = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+  q.row_part[3 * n] = mn;
+  q.row_part[3 * n + 1] = ent;
+  q.row_part[3 * n + 2] = (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+}
+
+// loss scalars: one block, fixed-order strided sums + tree (deterministic)
+__global__ __launch_bounds__(256) void lstm_loss_kernel(const float *__restrict__ row_part, int b,
+                                                        float inv_b, float inv_ba, float ent_coef,
+                                                        float *__restrict__ loss_out) {
+  __shared__ float red[3][256];
+  const int tid = threadIdx.x;
+  float s[3] = {0.f, 0.f, 0.f};
+  for (int n = tid; n < b; n += 256)
+    for (int k = 0; k < 3; ++k) s[k] += row_part[3 * n + k];
+  for (int k = 0; k < 3; ++k) red[k][tid] = s[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w)
+      for (int k = 0; k < 3; ++k) red[k][tid] += red[k][tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    loss_out[0] = -(red[0][0] * inv_b) - (red[1][0] * inv_ba) * ent_coef;
+    loss_out[1] = red[2][0] * inv_b;
+  }
+}
+
+}  // namespace lstm
+}  // namespace ppo
+
+using namespace ppo;
+using namespace ppo::lstm;
+
+struct ppo_lstm_ctx {
+  ppo_lstm_cfg cfg;
+  int device;
+  int prec;
+  LstmNet net[2];  // 0 actor, 1 critic
+  Mlp mu, ls, vc;  // actor mean / logstd MLPs, critic MLP
+  int64_t total, n_actor;
+  std::vector<int64_t> offsets;  // torch parameters() order, actor then critic
+  float *params;
+  float *ws;
+  int64_t rows;  // workspace rows
+  // workspace views
+  float *x;                          // [rows][W*O] gathered states
+  float *g[2][PPO_MAX_LAYERS];       // [rows*W][8H]
+  float *c[2][PPO_MAX_LAYERS], *y[2][PPO_MAX_LAYERS], *hp[2][PPO_MAX_LAYERS];  // [rows*W][2H]
+  float *gh, *dhrec, *dcarry;        // [rows][8H], [rows][2H], [rows][2H]
+  float *dy[2], *tmp;                // [rows*W][2H]
+  float *feat_a, *feat_c;            // [rows][W*2H], [rows][2H]
+  float *act_mu[PPO_MAX_LAYERS + 1], *act_ls[PPO_MAX_LAYERS + 1], *act_v[PPO_MAX_LAYERS + 1];
+  float *dz[3][2];                   // ping-pong gradient buffers [rows][maxw]: mu, ls, critic
+  float *slabs;                      // [kSplits][total]
+  float *row_part;                   // [rows][3]
+  int maxw;
+};
+
+namespace {
+
+void add_mlp(Mlp &m, int in, const ppo_lstm_cfg &c, int out, int final_act, int64_t &off,
+             std::vector<int64_t> &offs) {
+  m.n = c.n_hidden + 1;
+  for (int l = 0; l < m.n; ++l) {
+    MlpLayer &L = m.l[l];
+    L.in = in;
+    L.out = l < c.n_hidden ? c.hidden[l] : out;
+    L.act = l < c.n_hidden ? c.activation : final_act;
+    L.w = off;
+    offs.push_back(off);
+    off = align_up(off + static_cast<int64_t>(L.in) * L.out, kAlign);
+    if (c.use_bias) {
+      L.b = off;
+      offs.push_back(off);
+      off = align_up(off + L.out, kAlign);
+    } else {
+      L.b = -1;
+    }
+    in = L.out;
+  }
+}
+
+void add_lstm(LstmNet &n, int layers, int in, int h, int64_t &off, std::vector<int64_t> &offs) {
+  n.layers = layers;
+  n.hidden = h;
+  for (int l = 0; l < layers; ++l) {
+    LstmLayer &L = n.l[l];
+    L.in = l == 0 ? in : 2 * h;
+    for (int d = 0; d < 2; ++d) {  // nn.LSTM order: w_ih, w_hh, b_ih, b_hh, then _reverse
+      L.w_ih[d] = off;
+      offs.push_back(off);
+      off = align_up(off + 4LL * h * L.in, kAlign);
+      L.w_hh[d] = off;
+      offs.push_back(off);
+      off = align_up(off + 4LL * h * h, kAlign);
+      L.b_ih[d] = off;
+      offs.push_back(off);
+      off = align_up(off + 4LL * h, kAlign);
+      L.b_hh[d] = off;
+      offs.push_back(off);
+      off = align_up(off + 4LL * h, kAlign);
+    }
+  }
+}
+
+int gemm_fwd(ppo_lstm_ctx *x, const GemmProblem *p, int np, int k, int rows, int max_n, int act,
+             bool b_kn, hipStream_t st) {
+  GemmBatch gb{};
+  for (int i = 0; i < np; ++i) gb.p[i] = p[i];
+  gb.k = k;
+  gb.act = act;
+  gb.prec = x->prec;
+  return b_kn ? run_rowwise<B_KN, EPI_FWD>(gb, np, rows, max_n, st)
+              : run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+}
+
+int gemm_dx(ppo_lstm_ctx *x, const GemmProblem *p, int np, int k, int rows, int max_n, int act,
+            hipStream_t st) {
+  GemmBatch gb{};
+  for (int i = 0; i < np; ++i) gb.p[i] = p[i];
+  gb.k = k;
+  gb.act = act;
+  gb.prec = x->prec;
+  return run_rowwise<B_KN, EPI_DX>(gb, np, rows, max_n, st);
+}
+
+int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int max_m, int max_n,
+                 hipStream_t st) {
+  GemmBatch gb{};
+  for (int i = 0; i < np; ++i) gb.p[i] = p[i];
+  gb.k = rows;
+  gb.splits = kSplits;
+  gb.slab_stride = x->total;
+  gb.prec = x->prec;
+  return run_partial(gb, np, max_m, max_n, st);
+}
+
+// LSTM net z forward over xin [b*W][O] (batch-major rows); fills g/c/y/hp of every layer and the
+// features of the top layer (actor: all steps, critic: t = W-1).
+int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st) {
+  const LstmNet &N = x->net[z];
+  const int H = N.hidden, W = x->cfg.window;
+  const float *P = x->params;
+  for (int l = 0; l < N.layers; ++l) {
+    const LstmLayer &L = N.l[l];
+    const float *in = l == 0 ? xin : x->y[z][l - 1];
+    GemmProblem p[2] = {};
+    for (int d = 0; d < 2; ++d) {
+      p[d].a = in;
+      p[d].lda = L.in;
+      p[d].b = P + L.w_ih[d];
+      p[d].ldb = L.in;
+      p[d].c = x->g[z][l] + d * 4 * H;
+      p[d].ldc = 8 * H;
+      p[d].bias = P + L.b_ih[d];
+      p[d].m = b * W;
+      p[d].n = 4 * H;
+    }
+    if (int rc = gemm_fwd(x, p, 2, L.in, b * W, 4 * H, PPO_ACT_IDENTITY, false, st)) return rc;
+    for (int s = 0; s < W; ++s) {
+      if (s > 0) {
+        GemmProblem q[2] = {};
+        for (int d = 0; d < 2; ++d) {
+          const int tprev = d == 0 ? s - 1 : W - s;
+          q[d].a = x->y[z][l] + static_cast<int64_t>(tprev) * 2 * H + d * H;
+          q[d].lda = static_cast<int64_t>(W) * 2 * H;
+          q[d].b = P + L.w_hh[d];
+          q[d].ldb = H;
+          q[d].c = x->gh + d * 4 * H;
+          q[d].ldc = 8 * H;
+          q[d].bias = P + L.b_hh[d];
+          q[d].m = b;
+          q[d].n = 4 * H;
+        }
+        if (int rc = gemm_fwd(x, q, 2, H, b, 4 * H, PPO_ACT_IDENTITY, false, st)) return rc;
+      }
+      CellArgs a{};
+      a.g = x->g[z][l];
+      a.gh = s > 0 ? x->gh : nullptr;
+      a.b_hh[0] = P + L.b_hh[0];
+      a.b_hh[1] = P + L.b_hh[1];
+      a.c = x->c[z][l];
+      a.y = x->y[z][l];
+      a.hp = x->hp[z][l];
+      const bool top = l == N.layers - 1;
+      a.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
+      a.feat = z == 0 ? x->feat_a : x->feat_c;
+      a.act = x->cfg.activation;
+      a.b = b;
+      a.w = W;
+      a.h = H;
+      a.s = s;
+      launch_k(TimRec{KC_LSTM, "lstm_cell_fwd_kernel", 0.0, 0.0}, lstm_cell_fwd_kernel,
+               dim3(ceil_div(static_cast<int64_t>(b) * 2 * H, 256)), dim3(256), 0, st, a);
+      PPO_LAUNCHED();
+    }
+  }
+  return 0;
+}
+
+// MLP forward: m1 (and m2 on the same input, the actor's mean / logstd pair) over in [b][in0]
+int mlp_forward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm, const float *in,
+                int b, hipStream_t st) {
+  const float *P = x->params;
+  for (int l = 0; l < m[0]->n; ++l) {
+    GemmProblem p[2] = {};
+    for (int k = 0; k < nm; ++k) {
+      const MlpLayer &L = m[k]->l[l];
+      p[k].a = l == 0 ? in : acts[k][l - 1];
+      p[k].lda = L.in;
+      p[k].b = P + L.w;
+      p[k].ldb = L.in;
+      p[k].c = acts[k][l];
+      p[k].ldc = L.out;
+      p[k].bias = L.b >= 0 ? P + L.b : nullptr;
+      p[k].m = b;
+      p[k].n = L.out;
+    }
+    const MlpLayer &L0 = m[0]->l[l];
+    if (int rc = gemm_fwd(x, p, nm, L0.in, b, L0.out, L0.act, false, st)) return rc;
+  }
+  return 0;
+}
+
+// MLP backward from dz (gradient of the output layer's pre-activation, [b][out]); weight grads
+// into the slabs, the input gradient (times act'(input) of the feature activation) into din.
+int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm, const float *in,
+                 float *const *pp[2], float *din, int64_t ld_din, int feat_act, int b,
+                 hipStream_t st) {
+  // pp[k]: the problem's two ping-pong buffers; pp[k][0] holds the output-layer gradient
+  const float *P = x->params;
+  float *cur[2] = {pp[0][0], nm == 2 ? pp[1][0] : nullptr};
+  for (int l = m[0]->n - 1; l >= 0; --l) {
+    GemmProblem p[2] = {};
+    for (int k = 0; k < nm; ++k) {
+      const MlpLayer &L = m[k]->l[l];
+      p[k].a = cur[k];
+      p[k].lda = L.out;
+      p[k].b = l == 0 ? in : acts[k][l - 1];
+      p[k].ldb = L.in;
+      p[k].c = x->slabs + L.w;
+      p[k].ldc = L.in;
+      p[k].colsum = L.b >= 0 ? x->slabs + L.b : nullptr;
+      p[k].m = L.out;
+      p[k].n = L.in;
+    }
+    const MlpLayer &L0 = m[0]->l[l];
+    if (int rc = gemm_partial(x, p, nm, b, L0.out, L0.in, st)) return rc;
+    // dX = (dZ W) * act'(X): for l > 0 into the other ping-pong buffer; l == 0: the features
+    GemmProblem q[2] = {};
+    float *nxt[2] = {nullptr, nullptr};
+    for (int k = 0; k < nm; ++k) {
+      const MlpLayer &L = m[k]->l[l];
+      q[k].a = cur[k];
+      q[k].lda = L.out;
+      q[k].b = P + L.w;
+      q[k].ldb = L.in;
+      if (l > 0) {
+        nxt[k] = pp[k][(cur[k] == pp[k][0]) ? 1 : 0];
+        q[k].c = nxt[k];
+        q[k].ldc = L.in;
+        q[k].aux = acts[k][l - 1];
+      } else {
+        q[k].c = k == 0 ? din : x->tmp;
+        q[k].ldc = ld_din;
+        q[k].aux = in;
+      }
+      q[k].m = b;
+      q[k].n = L.in;
+    }
+    const int act = l > 0 ? m[0]->l[l - 1].act : feat_act;
+    if (int rc = gemm_dx(x, q, nm, L0.out, b, L0.in, act, st)) return rc;
+    if (l == 0 && nm == 2) {  // the two actor MLPs read the same features: sum their dX
+      const int64_t n = static_cast<int64_t>(b) * ld_din;
+      launch_k(TimRec{KC_LSTM, "add_inplace_kernel", 0.0, 0.0}, add_inplace_kernel,
+               dim3(ceil_div(n, 256)), dim3(256), 0, st, din, x->tmp, n);
+      PPO_LAUNCHED();
+    }
+    cur[0] = nxt[0];
+    cur[1] = nxt[1];
+  }
+  return 0;
+}
+
+// BPTT of LSTM net z given dY of the top layer (actor: full [b*W][2H] in x->dy[0]; critic: the
+// [b][2H] gradient of h at t = W-1 in x->dy[0]); weight grads into the slabs.
+int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st) {
+  const LstmNet &N = x->net[z];
+  const int H = N.hidden, W = x->cfg.window;
+  const float *P = x->params;
+  int cur = 0;
+  for (int l = N.layers - 1; l >= 0; --l) {
+    const LstmLayer &L = N.l[l];
+    const bool top = l == N.layers - 1;
+    for (int s = 0; s < W; ++s) {
+      if (s > 0) {
+        GemmProblem p[2] = {};
+        for (int d = 0; d < 2; ++d) {
+          const int tn = d == 0 ? W - s : s - 1;  // the step back-propagated at s - 1
+          p[d].a = x->g[z][l] + static_cast<int64_t>(tn) * 8 * H + d * 4 * H;
+          p[d].lda = static_cast<int64_t>(W) * 8 * H;
+          p[d].b = P + L.w_hh[d];
+          p[d].ldb = H;
+          p[d].c = x->dhrec + d * H;
+          p[d].ldc = 2 * H;
+          p[d].m = b;
+          p[d].n = H;
+        }
+        if (int rc = gemm_fwd(x, p, 2, 4 * H, b, H, PPO_ACT_IDENTITY, true, st)) return rc;
+      }
+      CellBwdArgs a{};
+      a.g = x->g[z][l];
+      a.c = x->c[z][l];
+      a.dy_mode = (top && z == 1) ? 2 : 1;
+      a.dy = x->dy[cur];
+      a.dy_last = x->dy[cur];
+      a.dh_rec = s > 0 ? x->dhrec : nullptr;
+      a.dcarry = x->dcarry;
+      a.b = b;
+      a.w = W;
+      a.h = H;
+      a.s = s;
+      launch_k(TimRec{KC_LSTM, "lstm_cell_bwd_kernel", 0.0, 0.0}, lstm_cell_bwd_kernel,
+               dim3(ceil_div(static_cast<int64_t>(b) * 2 * H, 256)), dim3(256), 0, st, a);
+      PPO_LAUNCHED();
+    }
+    const float *in = l == 0 ? xin : x->y[z][l - 1];
+    GemmProblem pi[2] = {}, ph[2] = {};
+    for (int d = 0; d < 2; ++d) {
+      pi[d].a = x->g[z][l] + d * 4 * H;
+      pi[d].lda = 8 * H;
+      pi[d].b = in;
+      pi[d].ldb = L.in;
+      pi[d].c = x->slabs + L.w_ih[d];
+      pi[d].ldc = L.in;
+      pi[d].colsum = x->slabs + L.b_ih[d];
+      pi[d].m = 4 * H;
+      pi[d].n = L.in;
+      ph[d] = pi[d];
+      ph[d].b = x->hp[z][l] + d * H;
+      ph[d].ldb = 2 * H;
+      ph[d].c = x->slabs + L.w_hh[d];
+      ph[d].ldc = H;
+      ph[d].colsum = x->slabs + L.b_hh[d];
+      ph[d].n = H;
+    }
+    if (int rc = gemm_partial(x, pi, 2, b * W, 4 * H, L.in, st)) return rc;
+    if (int rc = gemm_partial(x, ph, 2, b * W, 4 * H, H, st)) return rc;
+    if (l > 0) {  // dY of the layer below = sum_d dG_d W_ih_d (no activation between layers)
+      const int nxt = cur ^ 1;
+      for (int d = 0; d < 2; ++d) {
+        GemmProblem p{};
+        p.a = x->g[z][l] + d * 4 * H;
+        p.lda = 8 * H;
+        p.b = P + L.w_ih[d];
+        p.ldb = L.in;
+        p.c = d == 0 ? x->dy[nxt] : x->tmp;
+        p.ldc = L.in;
+        p.m = b * W;
+        p.n = L.in;
+        if (int rc = gemm_fwd(x, &p, 1, 4 * H, b * W, L.in, PPO_ACT_IDENTITY, true, st)) return rc;
+      }
+      const int64_t n = static_cast<int64_t>(b) * W * L.in;
+      launch_k(TimRec{KC_LSTM, "add_inplace_kernel", 0.0, 0.0}, add_inplace_kernel,
+               dim3(ceil_div(n, 256)), dim3(256), 0, st, x->dy[nxt], x->tmp, n);
+      PPO_LAUNCHED();
+      cur = nxt;
+    }
+  }
+  return 0;
+}
+
+int check_rows(ppo_lstm_ctx *x, int b) {
+  PPO_REQUIRE(b >= 0 && b <= x->rows, "ppo_lstm: %d rows exceed the workspace (%lld)", b,
+              static_cast<long long>(x->rows));
+  PPO_REQUIRE(x->params != nullptr, "ppo_lstm: parameters not bound (ppo_lstm_bind_params)");
+  return 0;
+}
+
+int forward_all(ppo_lstm_ctx *x, const float *xin, int b, hipStream_t st) {
+  if (int rc = lstm_forward(x, 0, xin, b, st)) return rc;
+  if (int rc = lstm_forward(x, 1, xin, b, st)) return rc;
+  const Mlp *am[2] = {&x->mu, &x->ls};
+  float *const *aa[2] = {x->act_mu, x->act_ls};
+  if (int rc = mlp_forward(x, am, aa, 2, x->feat_a, b, st)) return rc;
+  const Mlp *cm[2] = {&x->vc, nullptr};
+  float *const *ca[2] = {x->act_v, nullptr};
+  return mlp_forward(x, cm, ca, 1, x->feat_c, b, st);
+}
+
+}  // namespace
+
+extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm_ctx **out) {
+  PPO_REQUIRE(cfg != nullptr && out != nullptr, "ppo_lstm_ctx_create: null argument");
+  const ppo_lstm_cfg &c = *cfg;
+  PPO_REQUIRE(c.obs_dim > 0 && c.window > 0 && c.act_dim > 0 && c.act_dim <= kMaxA,
+              "ppo_lstm_ctx_create: bad obs/window/act (%d, %d, %d)", c.obs_dim, c.window,
+              c.act_dim);
+  PPO_REQUIRE(c.latent > 0 && c.latent % 4 == 0 && c.latent <= 1024,
+              "ppo_lstm_ctx_create: latent size %d must be a multiple of 4 in [4, 1024]", c.latent);
+  PPO_REQUIRE(c.actor_layers >= 1 && c.actor_layers <= PPO_MAX_LAYERS,
+              "ppo_lstm_ctx_create: %d feature-extractor layers", c.actor_layers);
+  PPO_REQUIRE(c.n_hidden >= 1 && c.n_hidden <= PPO_MAX_LAYERS,
+              "ppo_lstm_ctx_create: %d hidden layers", c.n_hidden);
+  PPO_REQUIRE(c.activation >= PPO_ACT_RELU && c.activation <= PPO_ACT_ELU,
+              "ppo_lstm_ctx_create: activation %d", c.activation);
+  PPO_REQUIRE(c.max_rows > 0, "ppo_lstm_ctx_create: max_rows %d", c.max_rows);
+  for (int l = 0; l < c.n_hidden; ++l)
+    PPO_REQUIRE(c.hidden[l] > 0 && c.hidden[l] <= 4096, "ppo_lstm_ctx_create: hidden width %d",
+                c.hidden[l]);
+  ppo_lstm_ctx *x = new (std::nothrow) ppo_lstm_ctx();
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_ctx_create: out of host memory");
+  x->cfg = c;
+  x->device = device;
+  x->prec = PPO_PREC_F32;
+  const int H = c.latent, W = c.window, O = c.obs_dim, A = c.act_dim;
+  int64_t off = 0;
+  // LSTMActor.parameters(): feature_extractor, actor, actor_logstd (lstm_actor.py:12-38)
+  add_lstm(x->net[0], c.actor_layers, O, H, off, x->offsets);
+  add_mlp(x->mu, W * 2 * H, c, A, PPO_ACT_TANH, off, x->offsets);
+  add_mlp(x->ls, W * 2 * H, c, A, PPO_ACT_TANH, off, x->offsets);
+  x->n_actor = off;
+  // LSTMCritic.parameters(): feature_extractor.0 (one layer), network (lstm_critic.py:19-31)
+  add_lstm(x->net[1], 1, O, H, off, x->offsets);
+  add_mlp(x->vc, 2 * H, c, 1, PPO_ACT_IDENTITY, off, x->offsets);
+  x->total = off;
+  int maxw = std::max(A, 1);
+  for (int l = 0; l < c.n_hidden; ++l) maxw = std::max(maxw, c.hidden[l]);
+  x->maxw = maxw;
+  const int64_t R = c.max_rows;
+  x->rows = R;
+  // workspace carve-out
+  int64_t need = 0;
+  auto take = [&](int64_t n) {
+    const int64_t at = need;
+    need = align_up(need + n, kWsAlign);
+    return at;
+  };
+  const int64_t o_x = take(R * W * O);
+  int64_t o_g[2][PPO_MAX_LAYERS], o_c[2][PPO_MAX_LAYERS], o_y[2][PPO_MAX_LAYERS],
+      o_hp[2][PPO_MAX_LAYERS];
+  for (int z = 0; z < 2; ++z)
+    for (int l = 0; l < x->net[z].layers; ++l) {
+      o_g[z][l] = take(R * W * 8 * H);
+      o_c[z][l] = take(R * W * 2 * H);
+      o_y[z][l] = take(R * W * 2 * H);
+      o_hp[z][l] = take(R * W * 2 * H);
+    }
+  const int64_t o_gh = take(R * 8 * H), o_dhrec = take(R * 2 * H), o_dcarry = take(R * 2 * H);
+  const int64_t o_dy0 = take(R * W * 2 * H), o_dy1 = take(R * W * 2 * H);
+  const int64_t o_tmp = take(R * std::max<int64_t>(W * 2 * H, maxw));
+  const int64_t o_fa = take(R * W * 2 * H), o_fc = take(R * 2 * H);
+  int64_t o_mu[PPO_MAX_LAYERS + 1], o_ls[PPO_MAX_LAYERS + 1], o_v[PPO_MAX_LAYERS + 1];
+  for (int l = 0; l <= c.n_hidden; ++l) {
+    o_mu[l] = take(R * x->mu.l[l].out);
+    o_ls[l] = take(R * x->ls.l[l].out);
+    o_v[l] = take(R * x->vc.l[l].out);
+  }
+  int64_t o_dz[3][2];
+  for (int k = 0; k < 3; ++k)
+    for (int p = 0; p < 2; ++p) o_dz[k][p] = take(R * maxw);
+  const int64_t o_slabs = take(kSplits * x->total);
+  const int64_t o_rp = take(R * 3);
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&x->ws, sizeof(float) * std::max<int64_t>(need, 1));
+  if (e != hipSuccess) {
+    set_error("ppo_lstm_ctx_create: hipMalloc(%lld floats) failed: %s",
+              static_cast<long long>(need), hipGetErrorString(e));
+    delete x;
+    return PPO_EHIP;
+  }
+  float *w = x->ws;
+  x->x = w + o_x;
+  for (int z = 0; z < 2; ++z)
+    for (int l = 0; l < x->net[z].layers; ++l) {
+      x->g[z][l] = w + o_g[z][l];
+      x->c[z][l] = w + o_c[z][l];
+      x->y[z][l] = w + o_y[z][l];
+      x->hp[z][l] = w + o_hp[z][l];
+    }
+  x->gh = w + o_gh;
+  x->dhrec = w + o_dhrec;
+  x->dcarry = w + o_dcarry;
+  x->dy[0] = w + o_dy0;
+  x->dy[1] = w + o_dy1;
+  x->tmp = w + o_tmp;
+  x->feat_a = w + o_fa;
+  x->feat_c = w + o_fc;
+  for (int l = 0; l <= c.n_hidden; ++l) {
+    x->act_mu[l] = w + o_mu[l];
+    x->act_ls[l] = w + o_ls[l];
+    x->act_v[l] = w + o_v[l];
+  }
+  for (int k = 0; k < 3; ++k)
+    for (int p = 0; p < 2; ++p) x->dz[k][p] = w + o_dz[k][p];
+  x->slabs = w + o_slabs;
+  // the alignment padding between tensors is never written by a GEMM: zero slabs reduce to 0
+  e = hipMemset(x->slabs, 0, sizeof(float) * kSplits * x->total);
+  if (e != hipSuccess) {
+    set_error("ppo_lstm_ctx_create: hipMemset failed: %s", hipGetErrorString(e));
+    (void)hipFree(x->ws);
+    delete x;
+    return PPO_EHIP;
+  }
+  x->row_part = w + o_rp;
+  *out = x;
+  return 0;
+}
+
+extern "C" int ppo_lstm_ctx_destroy(ppo_lstm_ctx *x) {
+  if (!x) return 0;
+  if (x->ws) (void)hipFree(x->ws);
+  delete x;
+  return 0;
+}
+
+extern "C" int ppo_lstm_param_layout(const ppo_lstm_ctx *x, int64_t *offsets, int max_tensors,
+                                     int64_t *total, int64_t *n_actor) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_param_layout: null ctx");
+  const int n = static_cast<int>(x->offsets.size());
+  if (offsets)
+    for (int i = 0; i < std::min(n, max_tensors); ++i) offsets[i] = x->offsets[i];
+  if (total) *total = x->total;
+  if (n_actor) *n_actor = x->n_actor;
+  return n;
+}
+
+extern "C" int ppo_lstm_bind_params(ppo_lstm_ctx *x, float *params_d) {
+  PPO_REQUIRE(x != nullptr && params_d != nullptr, "ppo_lstm_bind_params: null argument");
+  PPO_REQUIRE(reinterpret_cast<uintptr_t>(params_d) % 64 == 0,
+              "ppo_lstm_bind_params: parameter buffer must be 64-B aligned");
+  x->params = params_d;
+  return 0;
+}
+
+extern "C" int ppo_lstm_set_precision(ppo_lstm_ctx *x, int prec) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_set_precision: null ctx");
+  PPO_REQUIRE(prec == PPO_PREC_F32 || prec == PPO_PREC_BF16, "ppo_lstm_set_precision: %d", prec);
+  x->prec = prec;
+  return 0;
+}
+
+extern "C" int ppo_lstm_forward(ppo_lstm_ctx *x, const float *state_d, int n, float *mean_d,
+                                float *std_d, float *value_d, float *actor_lstm_out_d,
+                                float *critic_lstm_out_d, void *stream) {
+  PPO_REQUIRE(x != nullptr && state_d != nullptr, "ppo_lstm_forward: null argument");
+  if (int rc = check_rows(x, n)) return rc;
+  if (n == 0) return 0;
+  PPO_HIP_TRY(hipSetDevice(x->device));
+  hipStream_t st = as_stream(stream);
+  if (int rc = forward_all(x, state_d, n, st)) return rc;
+  const int A = x->cfg.act_dim, W = x->cfg.window;
+  const int64_t yb = sizeof(float) * static_cast<int64_t>(n) * W * 2 * x->cfg.latent;
+  if (actor_lstm_out_d)
+    PPO_HIP_TRY(hipMemcpyAsync(actor_lstm_out_d, x->y[0][x->net[0].layers - 1], yb,
+                               hipMemcpyDeviceToDevice, st));
+  if (critic_lstm_out_d)
+    PPO_HIP_TRY(hipMemcpyAsync(critic_lstm_out_d, x->y[1][0], yb, hipMemcpyDeviceToDevice, st));
+  const int nl = x->cfg.n_hidden;
+  if (mean_d)
+    PPO_HIP_TRY(hipMemcpyAsync(mean_d, x->act_mu[nl], sizeof(float) * static_cast<int64_t>(n) * A,
+                               hipMemcpyDeviceToDevice, st));
+  HeadArgs h{};
+  h.mean = x->act_mu[nl];
+  h.u = x->act_ls[nl];
+  h.value = x->act_v[nl];
+  h.std_out = std_d;
+  h.value_out = value_d;
+  h.b = n;
+  h.a = A;
+  launch_k(TimRec{KC_POLICY_HEAD, "lstm_policy_head_kernel", 0.0, 0.0}, lstm_policy_head_kernel,
+           dim3(ceil_div(n, 256)), dim3(256), 0, st, h);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_lstm_policy_step(ppo_lstm_ctx *x, const float *state_d, int n,
+                                    const float *eps_d, uint64_t seed, uint64_t offset,
+                                    float *action_d, float *logp_d, float *value_d, void *stream) {
+  PPO_REQUIRE(x != nullptr && state_d != nullptr, "ppo_lstm_policy_step: null argument");
+  PPO_REQUIRE(action_d != nullptr || logp_d == nullptr,
+              "ppo_lstm_policy_step: logp needs the action buffer");
+  if (int rc = check_rows(x, n)) return rc;
+  if (n == 0) return 0;
+  PPO_HIP_TRY(hipSetDevice(x->device));
+  hipStream_t st = as_stream(stream);
+  if (int rc = forward_all(x, state_d, n, st)) return rc;
+  const int nl = x->cfg.n_hidden;
+  HeadArgs h{};
+  h.mean = x->act_mu[nl];
+  h.u = x->act_ls[nl];
+  h.value = x->act_v[nl];
+  h.eps = eps_d;
+  h.seed = seed;
+  h.offset = offset;
+  h.action = action_d;
+  h.logp_out = logp_d;
+  h.value_out = value_d;
+  h.b = n;
+  h.a = x->cfg.act_dim;
+  launch_k(TimRec{KC_POLICY_HEAD, "lstm_policy_head_kernel", 0.0, 0.0}, lstm_policy_head_kernel,
+           dim3(ceil_div(n, 256)), dim3(256), 0, st, h);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
+                                       const float *actions_d, const float *logp_d,
+                                       const float *adv_d, const float *vt_d,
+                                       const int32_t *rows_d, int b, float *grad_d, float *loss_d,
+                                       float clip_lo, float clip_hi, float entropy_coef,
+                                       float inv_b, float inv_ba, void *stream) {
+  PPO_REQUIRE(x != nullptr && states_d && actions_d && logp_d && adv_d && vt_d && rows_d && grad_d,
+              "ppo_lstm_minibatch_grad: null argument");
+  if (int rc = check_rows(x, b)) return rc;
+  PPO_REQUIRE(b > 0, "ppo_lstm_minibatch_grad: empty minibatch");
+  PPO_HIP_TRY(hipSetDevice(x->device));
+  hipStream_t st = as_stream(stream);
+  const ppo_lstm_cfg &c = x->cfg;
+  const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
+  const int din = W * O;
+  launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
+           dim3(ceil_div(static_cast<int64_t>(b) * din, 256)), dim3(256), 0, st, states_d, rows_d,
+           b, din, x->x);
+  PPO_LAUNCHED();
+  if (int rc = forward_all(x, x->x, b, st)) return rc;
+  HeadArgs h{};
+  h.mean = x->act_mu[nl];
+  h.u = x->act_ls[nl];
+  h.value = x->act_v[nl];
+  h.actions = actions_d;
+  h.old_logp = logp_d;
+  h.adv = adv_d;
+  h.vt = vt_d;
+  h.rows = rows_d;
+  h.dzm = x->dz[0][0];
+  h.dzs = x->dz[1][0];
+  h.dv = x->dz[2][0];
+  h.row_part = x->row_part;
+  h.clip_lo = clip_lo;
+  h.clip_hi = clip_hi;
+  h.ent_coef = entropy_coef;
+  h.inv_b = inv_b;
+  h.inv_ba = inv_ba;
+  h.b = b;
+  h.a = A;
+  launch_k(TimRec{KC_UPDATE_HEAD, "lstm_update_head_kernel", 0.0, 0.0}, lstm_update_head_kernel,
+           dim3(ceil_div(b, 256)), dim3(256), 0, st, h);
+  PPO_LAUNCHED();
+  if (loss_d) {
+    launch_k(TimRec{KC_REDUCE, "lstm_loss_kernel", 0.0, 0.0}, lstm_loss_kernel, dim3(1),
+             dim3(256), 0, st, x->row_part, b, inv_b, inv_ba, entropy_coef, loss_d);
+    PPO_LAUNCHED();
+  }
+  {  // critic: MLP, then BiLSTM (the gradient of h at t = W-1 lands in dy[0])
+    const Mlp *cm[2] = {&x->vc, nullptr};
+    float *const *ca[2] = {x->act_v, nullptr};
+    float *const *pp[2] = {x->dz[2], nullptr};
+    if (int rc = mlp_backward(x, cm, ca, 1, x->feat_c, pp, x->dy[0], 2 * H, c.activation, b, st))
+      return rc;
+    if (int rc = lstm_backward(x, 1, x->x, b, st)) return rc;
+  }
+  {  // actor: both MLPs into one feature gradient, then BiLSTM
+    const Mlp *am[2] = {&x->mu, &x->ls};
+    float *const *aa[2] = {x->act_mu, x->act_ls};
+    float *const *pp[2] = {x->dz[0], x->dz[1]};
+    if (int rc = mlp_backward(x, am, aa, 2, x->feat_a, pp, x->dy[0],
+                              static_cast<int64_t>(W) * 2 * H, c.activation, b, st))
+      return rc;
+    if (int rc = lstm_backward(x, 0, x->x, b, st)) return rc;
+  }
+  // slabs -> flat gradient, tensor by tensor in a fixed split order
+  ReduceArgs r{};
+  int ns = 0;
+  for (size_t i = 0; i < x->offsets.size(); ++i) {
+    PPO_REQUIRE(ns < kMaxSegs, "ppo_lstm_minibatch_grad: too many tensors (%zu)", x->offsets.size());
+    ReduceSeg &g = r.seg[ns++];
+    g.dst = x->offsets[i];
+    g.len = (i + 1 < x->offsets.size() ? x->offsets[i + 1] : x->total) - x->offsets[i];
+    g.src = x->slabs + x->offsets[i];
+    g.stride = x->total;
+    g.nsplit = kSplits;
+  }
+  r.nseg = ns;
+  r.total = x->total;
+  r.grad = grad_d;
+  launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 0.0}, lstm_reduce_kernel,
+           dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);
+  PPO_LAUNCHED();
+  return 0;
+}

@@ -43,14 +43,17 @@ inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) 
 // the engine keeps in HBM (ReLU: threshold_backward(grad, y, 0); Tanh: grad*(1-y*y); ELU(alpha=1):
 // y<=0 -> grad*(y+1), the is_result form of elu_backward).
 __device__ __forceinline__ float act_forward(float x, int act) {
-  if (act == PPO_ACT_RELU) return (x != x) ? x : (x > 0.f ? x : 0.f);
+  // IEEE-2019 maximum (v_maximum3_f32): NaN propagates and -0 -> +0, as torch's x > 0 ? x : 0
+  if (act == PPO_ACT_RELU) return __builtin_elementwise_maximum(x, 0.f);
   if (act == PPO_ACT_TANH) return tanhf(x);
+  if (act == PPO_ACT_IDENTITY) return x;
   return x > 0.f ? x : expm1f(x);  // ELU alpha=1
 }
 
 __device__ __forceinline__ float act_backward(float grad, float y, int act) {
   if (act == PPO_ACT_RELU) return (y <= 0.f) ? 0.f : grad;
   if (act == PPO_ACT_TANH) return grad * (1.f - y * y);
+  if (act == PPO_ACT_IDENTITY) return grad;
   return (y <= 0.f) ? grad * (y + 1.f) : grad;
 }
 

@@ -28,6 +28,7 @@ enum {
   KC_PERM,   // minibatch row selection
   KC_ENV,    // synthetic VecEnv step + Philox normals (bench harness)
   KC_FUSED,  // persistent fused minibatch forward + loss + backward (bf16)
+  KC_LSTM,   // BiLSTM cell steps and elementwise glue (bilstm.hip)
   KC_COUNT
 };
 

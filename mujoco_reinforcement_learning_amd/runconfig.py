@@ -22,13 +22,17 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
              rng: str = "torch", seed: int = 0, dp_mode: str = "local",
              rollout_graph: bool = True, train_graph: bool = True, precision: str = "f32",
              experiment_path: str = "/tmp/ppo_engine_run",
+             feature_extractor: str = "MLP", latent: int = 256, extractor_layers: int = 1,
              replace: bool = True) -> Run:
     """Defaults: the headline HalfCheetah config (BASELINE.json configs[1]) with main.py's PPO
     hyper-parameters (lr 1e-4, gamma 0.99, lambda 0.98, clip 0.1, entropy 1e-4, E=10).
 
     critic_hidden: None -> the actor's widths (the BASELINE configs name one MLP shape for actor
     and critic); pass "reference" for the reference critic's hard-coded [128, 128]
-    (models/critic.py:14, main.py's network)."""
+    (models/critic.py:14, main.py's network).
+    feature_extractor="LSTM" selects the reference PPOAgent's BiLSTM actor / critic
+    (latent = feature_extractor_latent_size, extractor_layers = num_feature_extractor_layers;
+    main.py:63-75 uses 256 and 1); their MLPs use ``hidden``."""
     if critic_hidden is None:
         critic_hidden = hidden
     elif critic_hidden == "reference":
@@ -49,8 +53,10 @@ def make_run(num_envs: int = 4096, horizon: int = 128, obs_dim: int = 17, act_di
                NetworkConfig(input_shape=obs_dim, output_shape=act_dim,
                              output_max_value=output_max_value, activation_class=_ACT[activation],
                              num_linear_layers=len(hidden), linear_hidden_shapes=list(hidden),
-                             num_feature_extractor_layers=1, feature_extractor_latent_size=256,
-                             use_bias=use_bias, use_batch_norm=False, feature_extractor="MLP",
+                             num_feature_extractor_layers=extractor_layers,
+                             feature_extractor_latent_size=latent,
+                             use_bias=use_bias, use_batch_norm=False,
+                             feature_extractor=feature_extractor,
                              last_layer_std=0.01),
                DynamicConfig(0, 0, 0, 0), processors=1, device="cuda",
                experiment_path=experiment_path, verbose=False, central_critic=True,

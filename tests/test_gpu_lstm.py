@@ -1,0 +1,200 @@
+"""GPU: the windowed BiLSTM actor-critic (csrc/bilstm.hip through the
+ppo_lstm_* C-ABI) against the reference's own LSTMActor / LSTMCritic (golden fixtures of
+tests/golden/gen_golden_lstm.py) and against the oracle (oracle/lstm_ref.py) where the shapes
+are too large to store.
+
+Bars (f32 parity mode, exact-f32 MFMA GEMMs vs torch CPU): LSTM outputs, mean, std, value within
+rtol 1e-5 / atol 1e-5; minibatch losses within 1e-5 relative; gradients within 1e-4 of each
+tensor's largest entry; one full PPO iteration at the north_star parameter bar (parity_util).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import lstm_ref as L
+from oracle import ppo_ref as R
+from oracle.ppo_ref import RefConfig
+from parity_util import assert_params_match, compare_step_grads, make_pair, run_iteration_pair
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "reference_lstm.npz")
+SMALL = ["lstm_relu_small", "lstm_tanh_2layer", "lstm_elu_w1"]
+
+
+def _case(z, name):
+    meta = z[f"{name}/meta"]
+    seed, obs, window, act, latent, layers, nh = (int(v) for v in meta[:7])
+    hidden = tuple(int(v) for v in meta[7:7 + nh])
+    return seed, obs, window, act, latent, layers, hidden, str(z[f"{name}/activation"])
+
+
+def _agent(gpu, obs, window, act, latent, layers, hidden, activation, rows, seed=0, **kw):
+    from mujoco_reinforcement_learning_amd.agent import make_agent
+    from mujoco_reinforcement_learning_amd.lstm import LSTMEngineAgent
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    run = make_run(num_envs=rows, horizon=1, obs_dim=obs, act_dim=act, window=window,
+                   hidden=hidden, activation=activation, batch_size=rows,
+                   feature_extractor="LSTM", latent=latent, extractor_layers=layers, **kw)
+    torch.manual_seed(seed)
+    agent = make_agent(run, device=gpu)
+    assert isinstance(agent, LSTMEngineAgent)
+    return agent
+
+
+def _load_golden_params(agent, z, name):
+    for net in ("actor", "critic"):
+        sd = {k[len(net) + 1:]: torch.from_numpy(z[f"{name}/param/{k}"])
+              for k in z[f"{name}/names"] if k.startswith(net + ".")}
+        agent.networks[net].load_state_dict(sd)
+
+
+def _forward(agent, x):
+    n, a = len(x), agent.engine.act_dim
+    dev = agent.device
+    s = x.reshape(n, -1).contiguous().to(dev)
+    k = agent.engine.window * 2 * agent.engine.latent
+    out = {"mean": torch.empty(n, a, device=dev), "std": torch.empty(n, a, device=dev),
+           "value": torch.empty(n, 1, device=dev), "y_actor": torch.empty(n, k, device=dev),
+           "y_critic": torch.empty(n, k, device=dev)}
+    agent.engine.forward(s, mean=out["mean"], std=out["std"], value=out["value"],
+                         actor_lstm_out=out["y_actor"], critic_lstm_out=out["y_critic"])
+    return {k: v.cpu() for k, v in out.items()}
+
+
+def _grad(agent, x, actions, old_logp, adv, vt, clip=0.1, ent=1e-4):
+    dev = agent.device
+    b, a = actions.shape
+    loss = torch.zeros(2, device=dev)
+    rows = torch.arange(b, dtype=torch.int32, device=dev)
+    agent.flat_grad.zero_()
+    agent.engine.minibatch_grad(x.reshape(b, -1).contiguous().to(dev), actions.contiguous().to(dev),
+                                old_logp.reshape(-1).contiguous().to(dev),
+                                adv.reshape(-1).contiguous().to(dev),
+                                vt.reshape(-1).contiguous().to(dev), rows, b, agent.flat_grad,
+                                loss, 1 - clip, 1 + clip, ent, 1.0 / b, 1.0 / (b * a))
+    return agent.packed(agent.flat_grad).cpu(), loss.cpu()
+
+
+def _assert_grads(g, g_ref, sizes, rel=1e-4, label=""):
+    worst = 0.0
+    for i, (a, b) in enumerate(zip(torch.split(g, sizes), torch.split(g_ref, sizes))):
+        scale = max(float(b.abs().max()), 1e-12)
+        err = float((a - b).abs().max()) / scale
+        worst = max(worst, err)
+        assert err <= rel, (label, i, err)
+    print(f"{label}: worst grad error {worst:.3e} of the tensor max")
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_forward_matches_reference_golden(gpu, name):
+    z = np.load(GOLDEN)
+    seed, obs, window, act, latent, layers, hidden, activation = _case(z, name)
+    x = torch.from_numpy(z[f"{name}/x"])
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, activation, len(x))
+    _load_golden_params(agent, z, name)
+    got = _forward(agent, x)
+    for k in ("y_actor", "y_critic", "mean", "std", "value"):
+        ref = torch.from_numpy(z[f"{name}/{k}"]).reshape(got[k].shape)
+        err = float((got[k] - ref).abs().max())
+        print(f"{name} {k}: max abs err {err:.3e}")
+        torch.testing.assert_close(got[k], ref, rtol=1e-5, atol=1e-5, msg=f"{name} {k}")
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_minibatch_grad_matches_reference_golden(gpu, name):
+    z = np.load(GOLDEN)
+    seed, obs, window, act, latent, layers, hidden, activation = _case(z, name)
+    t = {k: torch.from_numpy(z[f"{name}/{k}"]) for k in ("x", "actions", "old_logp", "adv", "vt")}
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, activation, len(t["x"]))
+    _load_golden_params(agent, z, name)
+    g, loss = _grad(agent, t["x"], t["actions"], t["old_logp"], t["adv"], t["vt"])
+    la, lc = z[f"{name}/loss"]
+    assert abs(float(loss[0]) - la) <= 1e-5 * max(1.0, abs(la)), (float(loss[0]), la)
+    assert abs(float(loss[1]) - lc) <= 1e-5 * max(1.0, abs(lc)), (float(loss[1]), lc)
+    sizes = [p.numel() for p in agent.networks.parameters()]
+    _assert_grads(g, torch.from_numpy(z[f"{name}/grad"]), sizes, label=name)
+
+
+def test_main_py_network_matches_oracle(gpu):
+    """The reference's own LSTM network (main.py:63-75: O=348, W=5, latent 256, one layer,
+    [256, 256, 128, 128], A=17): engine vs oracle on the same init (same seed, same host)."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    b = 64
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=24)
+    cfg = RefConfig(obs_dim=obs, act_dim=act, window=window, actor_hidden=hidden,
+                    critic_hidden=hidden, activation="relu")
+    torch.manual_seed(24)
+    ref = L.RefLSTMAgent(cfg, latent, layers)
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref))
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    with torch.no_grad():
+        mean, std = ref.networks["actor"](x)
+        value = ref.networks["critic"](x)
+        lp = torch.distributions.Normal(mean, std).log_prob(actions).sum(1)
+    old_logp = lp + 0.15 * torch.randn(b, generator=gen)
+    got = _forward(agent, x)
+    for k, r in (("mean", mean), ("std", std), ("value", value)):
+        print(f"main.py net {k}: max abs err {float((got[k] - r).abs().max()):.3e}")
+        torch.testing.assert_close(got[k], r, rtol=1e-5, atol=1e-5, msg=k)
+    g_ref, la, lc = L.minibatch_grads(ref, x, actions, old_logp, adv, vt, 0.1, 1e-4)
+    g, loss = _grad(agent, x, actions, old_logp, adv, vt)
+    assert abs(float(loss[0]) - la) <= 1e-5 * max(1.0, abs(la))
+    assert abs(float(loss[1]) - lc) <= 1e-5 * max(1.0, abs(lc))
+    _assert_grads(g, g_ref, [p.numel() for p in agent.networks.parameters()], label="main.py net")
+
+
+def test_minibatch_grad_deterministic_and_bf16_close(gpu):
+    """Fixed-order split-K reductions: two launches are bitwise equal; bf16 operands (8 mantissa
+    bits, compounded through the W recurrent steps) stay within 6e-2 relative L2 per tensor of
+    the f32 gradient."""
+    z = np.load(GOLDEN)
+    name = "lstm_relu_small"
+    seed, obs, window, act, latent, layers, hidden, activation = _case(z, name)
+    t = {k: torch.from_numpy(z[f"{name}/{k}"]) for k in ("x", "actions", "old_logp", "adv", "vt")}
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, activation, len(t["x"]))
+    _load_golden_params(agent, z, name)
+    g1, _ = _grad(agent, t["x"], t["actions"], t["old_logp"], t["adv"], t["vt"])
+    g2, _ = _grad(agent, t["x"], t["actions"], t["old_logp"], t["adv"], t["vt"])
+    assert torch.equal(g1, g2)
+    agent.engine.set_precision("bf16")
+    g3, _ = _grad(agent, t["x"], t["actions"], t["old_logp"], t["adv"], t["vt"])
+    sizes = [p.numel() for p in agent.networks.parameters()]
+    for i, (a, b) in enumerate(zip(torch.split(g3, sizes), torch.split(g1, sizes))):
+        rel = float((a - b).norm() / (b.norm() + 1e-20))
+        print(f"bf16 vs f32 grad tensor {i}: rel L2 {rel:.3e}")
+        assert rel <= 6e-2, (i, rel)
+
+
+@pytest.mark.parametrize("kw", [{"latent": 8, "window": 3, "hidden": (32, 32)},
+                                {"latent": 12, "window": 2, "hidden": (24, 16), "extractor_layers": 2,
+                                 "activation": "tanh"}])
+def test_lstm_iteration_matches_oracle(gpu, kw):
+    """One PPO iteration (rollout -> GAE -> 2 epochs) with the LSTM agent, engine vs oracle."""
+    algo, agent, ref, env, cfg = make_pair(gpu, n=16, t=16, b=64, epochs=2, p_term=0.05,
+                                           feature_extractor="LSTM", **kw)
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref))
+    mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg)
+    for key in ("current_state_value", "next_state_value", "action", "action_log_prob",
+                "advantage", "current_state_value_target"):
+        a, r = mem[key].cpu(), ref_mem[key]
+        torch.testing.assert_close(a.to(r.dtype), r, rtol=1e-5, atol=1e-5, msg=key)
+    compare_step_grads(g_eng, g_ref, ref, rel=1e-4, steps=1)
+    assert_params_match(agent.packed_params().cpu(), R.flat_params(ref), g_ref, ref,
+                        cfg.learning_rate, label=f"lstm iteration {kw}")
+
+
+def test_lstm_eval_rollout_matches_oracle(gpu):
+    """Algorithm.test (base_algorithm.py:21-48) with the LSTM agent's mean action."""
+    algo, agent, ref, env, cfg = make_pair(gpu, n=8, t=8, b=32, epochs=1, p_term=0.05,
+                                           feature_extractor="LSTM", latent=8, window=3,
+                                           hidden=(16, 16))
+    got = algo.test(steps=40)
+    want = R.test(env, ref, steps=40)
+    assert abs(got - float(want)) <= 1e-5 * max(1.0, abs(float(want))), (got, want)
