@@ -255,6 +255,8 @@ int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d, const 
 int ppo_host_register(void *host, int64_t bytes);
 int ppo_host_unregister(void *host);
 int ppo_memcpy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
+/* Device address of registered host memory (zero-copy access from kernels over PCIe). */
+int ppo_host_device_ptr(void *host, void **dev);
 
 /* ---- measurement: per-kernel-class timing (no reference counterpart; replaces @timeit,
  * error_handling_utils.py:5-17, with device-side timing) -----------------------------------------
@@ -302,6 +304,46 @@ int ppo_synthetic_test_step(const float *base_obs_d, const float *base_reward_d,
                             const float *action_d, int o, int a, int w, double *window_d,
                             int32_t *step_d, double *reward_sum_d, uint8_t *term_out_d,
                             void *stream);
+
+/* ---- Native pipelined host-physics rollout ----------------------
+ * The shared-memory worker pool of host_pool.HostPhysicsPool, described for the C driver:
+ * groups of workers over contiguous env ranges [group_lo, group_hi), each released by bumping
+ * ctrl[g][2] (generation; ctrl[g][0] = step) and finished when done[worker_lo..worker_hi) all
+ * equal that generation.  action / obs / reward / term are the page-locked shared-memory arrays
+ * (N, A) f32, (N, O) f64, (N,) f64, (N,) u8.  gen[] is updated in place. */
+#define PPO_MAX_GROUPS 4
+typedef struct ppo_host_pool_desc {
+  int32_t groups;
+  int32_t group_lo[PPO_MAX_GROUPS], group_hi[PPO_MAX_GROUPS];
+  int32_t worker_lo[PPO_MAX_GROUPS], worker_hi[PPO_MAX_GROUPS];
+  int64_t gen[PPO_MAX_GROUPS];
+  int64_t *ctrl;
+  int64_t *done;
+  float *action;      /* host addresses (the workers' view) ... */
+  double *obs;
+  double *reward;
+  uint8_t *term;
+  float *action_dev;  /* ... and their device addresses (ppo_host_device_ptr) */
+  double *obs_dev;
+  double *reward_dev;
+  uint8_t *term_dev;
+} ppo_host_pool_desc;
+
+/* One whole T-step rollout over a host-physics pool (ppo.py:13-60 driving
+ * running_gym_sequential_vectorized.py:40-59), pipelined per group from one native thread:
+ * the group's rewards / terminations of the last step read from the shared memory into the
+ * rollout buffer, ppo_observe_act on its rows reading the observations straight from the shared
+ * memory, its actions written back into the shared memory (all zero-copy over PCIe, one compute
+ * stream), then -- host side -- release of the group's workers and the wait for them.  Buffers are the rollout buffer's
+ * time-major arrays: states (T+1, N, W*O), actions (T, N, A), logp (T, N), values (T+1, N),
+ * reward (T, N) f64, term (T, N) u8; obs_next (N, O) f64 scratch.  eps_d (T, N, A) or NULL
+ * (Philox(seed, base_offset + row*A)).  The window must hold the reset observations. */
+int ppo_host_rollout(ppo_ctx *ctx, ppo_host_pool_desc *pool, double *window_d,
+                     const int32_t *bounds, int n_bounds, int normalize, float *states_d,
+                     float *actions_d, float *logp_d, float *values_d, double *reward_d,
+                     uint8_t *term_d, double *obs_next_d, int n, int obs_dim, int window,
+                     int act_dim, int horizon, const float *eps_d, uint64_t seed,
+                     uint64_t base_offset, void *stream);
 
 /* ---- Windowed BiLSTM actor-critic --------------------------------
  * models/lstm/lstm_actor.py:9-48 + lstm_critic.py:9-41, the PPOAgent binding of

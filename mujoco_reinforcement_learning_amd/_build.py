@@ -12,12 +12,28 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip",
-           "csrc/fused_policy.hip", "csrc/bilstm.hip"]
+           "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 
 
+def build_host_env(verbose: bool = True) -> str:
+    """libppo_hostenv.so: the host physics pool workers' per-slice dynamics (plain C, gcc)."""
+    out = os.path.join(HERE, "libppo_hostenv.so")
+    src = os.path.join(HERE, "csrc", "host", "synthetic_physics.c")
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    cmd = [os.environ.get("CC", "gcc"), "-O3", "-ffp-contract=off", "-fPIC", "-shared",
+           "-o", out + ".tmp", src]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=HERE)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_library(verbose: bool = True) -> str:
+    build_host_env(verbose)
     out = os.path.join(HERE, "libppo_engine.so")
     srcs = [os.path.join(HERE, s) for s in SOURCES]
     deps = srcs + glob.glob(os.path.join(HERE, "csrc", "*.h")) + \

@@ -50,6 +50,31 @@ class LstmCfg(ctypes.Structure):
     ]
 
 
+PPO_MAX_GROUPS = 4
+
+
+class HostPoolDesc(ctypes.Structure):
+    """``ppo_host_pool_desc`` (include/ppo_engine.h)."""
+    _fields_ = [
+        ("groups", c_int32),
+        ("group_lo", c_int32 * PPO_MAX_GROUPS),
+        ("group_hi", c_int32 * PPO_MAX_GROUPS),
+        ("worker_lo", c_int32 * PPO_MAX_GROUPS),
+        ("worker_hi", c_int32 * PPO_MAX_GROUPS),
+        ("gen", c_int64 * PPO_MAX_GROUPS),
+        ("ctrl", c_void_p),
+        ("done", c_void_p),
+        ("action", c_void_p),
+        ("obs", c_void_p),
+        ("reward", c_void_p),
+        ("term", c_void_p),
+        ("action_dev", c_void_p),
+        ("obs_dev", c_void_p),
+        ("reward_dev", c_void_p),
+        ("term_dev", c_void_p),
+    ]
+
+
 _SIGNATURES = {
     "ppo_abi_version": (c_int, []),
     "ppo_last_error": (ctypes.c_char_p, []),
@@ -103,6 +128,7 @@ _SIGNATURES = {
     "ppo_host_register": (c_int, [c_void_p, c_int64]),
     "ppo_host_unregister": (c_int, [c_void_p]),
     "ppo_memcpy_async": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "ppo_host_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
     "ppo_stage_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_void_p]),
     "ppo_minibatch_grad_staged": (c_int, [c_void_p, c_void_p, c_int, c_void_p, ctypes.c_float,
@@ -116,6 +142,9 @@ _SIGNATURES = {
     "ppo_adam_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, c_void_p]),
+    "ppo_host_rollout": (c_int, [c_void_p, POINTER(HostPoolDesc), c_void_p, POINTER(c_int32), c_int,
+                                 c_int] + [c_void_p] * 7 + [c_int] * 5 + [c_void_p, c_uint64,
+                                                                       c_uint64, c_void_p]),
     # windowed BiLSTM actor-critic (bilstm.hip)
     "ppo_lstm_ctx_create": (c_int, [POINTER(LstmCfg), c_int, POINTER(c_void_p)]),
     "ppo_lstm_ctx_destroy": (c_int, [c_void_p]),

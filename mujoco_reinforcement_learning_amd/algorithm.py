@@ -169,6 +169,19 @@ class PPOEngine:
         norm = bool(self.run.normalize_observations)
         seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
         halves = helper.halves
+        if hasattr(eng, "host_rollout") and hasattr(helper, "native_desc"):
+            # the whole T-step pipeline in one native call (csrc/host_rollout.hip); the noise of
+            # every step is drawn up front in the same order as the per-step draws below
+            eps = None
+            if self._rng() == "torch":
+                eps = torch.empty(t_len, n, a, device=self.agent.device)
+                for t in range(t_len):
+                    eps[t].copy_(self._eps(n, a)[0])
+            desc = helper.native_desc()
+            eng.host_rollout(desc, window, norm, buf.states, buf.actions, buf.logp, buf.values,
+                             buf.reward, buf.terminated, helper._obs_next, eps, seed, base_off)
+            helper.native_done(desc, buf.reward[t_len - 1], buf.terminated[t_len - 1])
+            return buf
 
         def act(t, obs_rows=None, reset_rows=None, eps=None, g=0, last=False):
             lo, hi = halves[g]

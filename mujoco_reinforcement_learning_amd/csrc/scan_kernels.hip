@@ -739,7 +739,13 @@ extern "C" int ppo_synthetic_test_step(const float *base_obs_d, const float *bas
 // ---- host physics pool transfers (north_star: pinned hipMemcpyAsync obs->GPU / action->CPU) ----
 extern "C" int ppo_host_register(void *host, int64_t bytes) {
   PPO_REQUIRE(host && bytes > 0, "ppo_host_register: bad args");
-  PPO_HIP_TRY(hipHostRegister(host, static_cast<size_t>(bytes), hipHostRegisterDefault));
+  PPO_HIP_TRY(hipHostRegister(host, static_cast<size_t>(bytes), hipHostRegisterMapped));
+  return 0;
+}
+
+extern "C" int ppo_host_device_ptr(void *host, void **dev) {
+  PPO_REQUIRE(host && dev, "ppo_host_device_ptr: null");
+  PPO_HIP_TRY(hipHostGetDevicePointer(dev, host, 0));
   return 0;
 }
 

@@ -163,6 +163,35 @@ class Engine:
                                        ptr(state), n, ptr(eps), seed, offset, ptr(action),
                                        ptr(logp), ptr(value), ptr(mean), _stream(self.device)))
 
+    def host_rollout(self, desc, window: torch.Tensor, normalize: bool, states, actions, logp,
+                     values, reward, terminated, obs_next, eps: Optional[torch.Tensor], seed: int,
+                     base_offset: int) -> None:
+        """The whole pipelined host-physics rollout in one native call (ppo_host_rollout): per
+        step and worker group, observe + act, action D2H, worker release / wait and result H2D
+        from one host thread.  ``desc`` is the pool's ``_lib.HostPoolDesc`` (gen updated in
+        place); the buffers are the rollout buffer's time-major arrays."""
+        n, o, w = window.shape
+        t = actions.shape[0]
+        _need(window, "window", torch.float64, device=self.device)
+        _need(states, "states", torch.float32, device=self.device)
+        _need(actions, "actions", torch.float32, (t, n, self.act_dim), self.device)
+        _need(logp, "logp", torch.float32, (t, n), self.device)
+        _need(values, "values", torch.float32, (t + 1, n), self.device)
+        _need(reward, "reward", torch.float64, (t, n), self.device)
+        _need(terminated, "terminated", None, (t, n), self.device)
+        _need(obs_next, "obs_next", torch.float64, (n, o), self.device)
+        if states.numel() != (t + 1) * n * o * w:
+            raise RuntimeError("states must hold (T+1, N, W*O) floats")
+        if eps is not None:
+            _need(eps, "eps", torch.float32, (t, n, self.act_dim), self.device)
+        edges = slice_edges(o)
+        arr = (ctypes.c_int32 * len(edges))(*edges)
+        check(self.lib.ppo_host_rollout(
+            self._ctx, ctypes.byref(desc), ptr(window), arr, len(edges) - 1, int(normalize),
+            ptr(states), ptr(actions), ptr(logp), ptr(values), ptr(reward), ptr(terminated),
+            ptr(obs_next), n, o, w, self.act_dim, t, ptr(eps), seed, base_offset,
+            _stream(self.device)))
+
     def set_precision(self, precision: str) -> None:
         """GEMM precision: "f32" (parity with the reference, default) or "bf16" (bf16 operands,
         f32 accumulation; activations, params and optimizer state stay f32)."""

@@ -14,6 +14,8 @@ The observation window (N, O, W) f64 and its per-sample standardisation are the 
 """
 from __future__ import annotations
 
+import ctypes
+
 from dataclasses import dataclass, field
 from types import SimpleNamespace
 from typing import Optional
@@ -233,6 +235,34 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
         self._registered = []
         self.pool.close()
         self.pool = None
+
+    # ---- native pipelined rollout (ppo_host_rollout) --------------------------------------------
+    def native_desc(self):
+        """The pool as a ``ppo_host_pool_desc`` for the native rollout driver."""
+        pool, v = self.pool, self.pool.v
+        d = E._lib.HostPoolDesc()
+        d.groups = pool.groups
+        for g in range(pool.groups):
+            d.group_lo[g], d.group_hi[g] = self.halves[g]
+            ids = pool._group_workers[g]
+            d.worker_lo[g], d.worker_hi[g] = ids[0], ids[-1] + 1
+            d.gen[g] = pool._gen[g]
+        d.ctrl, d.done = v["ctrl"].ctypes.data, v["done"].ctypes.data
+        d.action, d.obs = v["action"].ctypes.data, v["obs"].ctypes.data
+        d.reward, d.term = v["reward"].ctypes.data, v["term"].ctypes.data
+        for key in ("action", "obs", "reward", "term"):
+            dev = ctypes.c_void_p()
+            E.check(self._lib.ppo_host_device_ptr(v[key].ctypes.data, ctypes.byref(dev)))
+            setattr(d, key + "_dev", dev.value)
+        return d
+
+    def native_done(self, desc, reward_last: torch.Tensor, term_last: torch.Tensor) -> None:
+        """Bookkeeping after a native rollout: the generations it advanced, the step counter."""
+        for g in range(self.pool.groups):
+            self.pool._gen[g] = int(desc.gen[g])
+        self.t = self.horizon
+        self.timestep.reward = reward_last
+        self.timestep.terminated = term_last
 
     # ---- pipelined protocol (one half = one worker group + one side stream) -------------------
     def begin_half(self, g: int, action_rows: torch.Tensor) -> None:

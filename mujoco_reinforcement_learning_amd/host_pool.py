@@ -32,7 +32,9 @@ worker's gymnasium envs.
 """
 from __future__ import annotations
 
+import ctypes
 import multiprocessing as mp
+import os
 import time
 from multiprocessing import shared_memory
 from typing import Dict, Tuple
@@ -50,6 +52,28 @@ def _attach(specs: Dict[str, Tuple[str, tuple, str]]):
         shms.append(shm)
         views[key] = np.ndarray(shape, dtype=np.dtype(dtype), buffer=shm.buf)
     return shms, views
+
+
+_HOSTENV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libppo_hostenv.so")
+
+
+def _native_step():
+    """The C form of step_slice (csrc/host/synthetic_physics.c -> libppo_hostenv.so), or None
+    when the library is not built (numpy form below; same values)."""
+    if not os.path.exists(_HOSTENV):
+        return None
+    fn = ctypes.CDLL(_HOSTENV).ppo_host_step_slice
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+    return fn
+
+
+def step_slice_native(fn, v: Dict[str, np.ndarray], t: int, lo: int, hi: int) -> None:
+    n, o = v["obs"].shape
+    fn(v["base_obs"].ctypes.data, v["base_reward"].ctypes.data, v["base_term"].ctypes.data,
+       v["action"].ctypes.data, v["obs"].ctypes.data, v["reward"].ctypes.data,
+       v["term"].ctypes.data, n, o, v["action"].shape[1], t, lo, hi)
 
 
 def step_slice(v: Dict[str, np.ndarray], t: int, lo: int, hi: int) -> None:
@@ -78,13 +102,17 @@ def _wait_change(word: np.ndarray, idx: int, old: int, stop: np.ndarray = None) 
 def _worker(wid: int, grp: int, lo: int, hi: int, specs) -> None:
     shms, v = _attach(specs)
     ctrl, done = v["ctrl"][grp], v["done"]
+    native = _native_step()
     gen = 0
     try:
         while True:
             gen = _wait_change(ctrl, _CTRL_GEN, gen, stop=ctrl)
             if ctrl[_CTRL_STOP]:
                 break
-            step_slice(v, int(ctrl[_CTRL_T]), lo, hi)
+            if native is not None:
+                step_slice_native(native, v, int(ctrl[_CTRL_T]), lo, hi)
+            else:
+                step_slice(v, int(ctrl[_CTRL_T]), lo, hi)
             done[wid] = gen  # publish after the slice's outputs are written
     finally:
         for s in shms:

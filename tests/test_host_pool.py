@@ -67,3 +67,29 @@ def test_step_slice_partitions_compose():
     step_slice(parts, 2, 7, n)
     for k in ("obs", "reward", "term"):
         assert np.array_equal(whole[k], parts[k])
+
+
+def test_native_step_slice_matches_numpy():
+    """The workers' C dynamics (libppo_hostenv.so) equal the numpy form bit for bit."""
+    from mujoco_reinforcement_learning_amd._build import build_host_env
+    from mujoco_reinforcement_learning_amd.host_pool import _native_step, step_slice_native
+    build_host_env(verbose=False)
+    fn = _native_step()
+    assert fn is not None
+    base_obs, base_reward, base_term, a = _streams(n=29, t=4)
+    n, o = base_obs.shape[1:]
+    rng = np.random.default_rng(3)
+
+    def views():
+        return {"base_obs": base_obs, "base_reward": base_reward,
+                "base_term": base_term.astype(np.uint8),
+                "action": rng.standard_normal((n, a)).astype(np.float32),
+                "obs": np.zeros((n, o)), "reward": np.zeros(n), "term": np.zeros(n, np.uint8)}
+
+    for t in range(base_reward.shape[0]):
+        v1 = views()
+        v2 = {k: x.copy() for k, x in v1.items()}
+        step_slice(v1, t, 3, n - 2)
+        step_slice_native(fn, v2, t, 3, n - 2)
+        for k in ("obs", "reward", "term"):
+            assert np.array_equal(v1[k], v2[k]), (t, k)
