@@ -38,6 +38,13 @@ PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--model", choices=("mlp", "lstm"), default="mlp",
+                   help="mlp: the north_star MLP actor-critic (the headline metric); lstm: the "
+                        "reference PPOAgent's BiLSTM actor / critic on main.py's network (O=348, "
+                        "W=5, latent 256, [256,256,128,128], A=17) at N=1024, B=16384 unless "
+                        "overridden -- a separate measurement, not the headline line")
+    p.add_argument("--window", type=int, default=None)
+    p.add_argument("--latent", type=int, default=256)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--num-envs", type=int, default=4096)
@@ -71,7 +78,19 @@ def parse():
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.model == "lstm":
+        defaults = {"num_envs": 1024, "obs_dim": 348, "act_dim": 17, "hidden": "256,256,128,128",
+                    "batch": 16384, "window": 5}
+        for k, v in defaults.items():
+            if getattr(args, k) == p.get_default(k):
+                setattr(args, k, v)
+        args.no_timing = True  # per-kernel times for this leg come from rocprofv3
+        args.no_legs = True
+        args.cpu_baseline = False
+    if args.window is None:
+        args.window = 1
+    return args
 
 
 def load_traffic(path):
@@ -84,7 +103,8 @@ def load_traffic(path):
 
 
 # gymnasium observation / action sizes of the BASELINE configs (SURVEY.md s8 notation)
-_ENV_NAMES = {(17, 6): "HalfCheetah-v4", (27, 8): "Ant-v4", (376, 17): "Humanoid-v4"}
+_ENV_NAMES = {(17, 6): "HalfCheetah-v4", (27, 8): "Ant-v4", (376, 17): "Humanoid-v4",
+              (348, 17): "main.py humanoid (O=348)"}
 
 
 def roofline(name, c, traffic, force_hbm=False):
@@ -121,12 +141,35 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share() -> int:
+    """The cores this process may really use: its affinity set, capped by the cgroup CPU quota
+    (a GPU box's affinity lists the whole machine while its quota is a share of it) and by
+    OMP_NUM_THREADS when the environment sets one."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def _progress(msg: str) -> None:
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(args, hidden):
     """Oracle on the host cores: rollout_steps of the T-step rollout, the full GAE, cpu_epochs of
     the E-epoch update; extrapolated linearly to one full iteration."""
     from oracle import ppo_ref as R
-    threads = len(os.sched_getaffinity(0))  # every core this process may run on (SURVEY s8(d))
+    threads = cpu_share()  # every core this process may use (SURVEY s8(d))
     torch.set_num_threads(threads)
+    _progress(f"cpu baseline on {threads} threads ({cpu_model()})")
     n, t = args.num_envs, args.horizon
     cfg = R.RefConfig(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
                       actor_hidden=hidden, critic_hidden=hidden, batch_size=args.batch,
@@ -142,6 +185,7 @@ def cpu_baseline(args, hidden):
     t0 = time.perf_counter()
     mem = R.rollout(env, agent)  # k steps
     t_roll = (time.perf_counter() - t0) * (t / k)
+    _progress(f"cpu baseline rollout: {k} steps in {t_roll * k / t:.2f} s")
     cfg.horizon = t
     # full-size buffer for GAE / update: tile the k sampled steps to T
     reps = (t + k - 1) // k
@@ -153,6 +197,7 @@ def cpu_baseline(args, hidden):
     t0 = time.perf_counter()
     R.train(agent, full, 0)
     t_epoch = (time.perf_counter() - t0) / args.cpu_epochs
+    _progress(f"cpu baseline update: {args.cpu_epochs} epoch(s) in {t_epoch * args.cpu_epochs:.2f} s")
     t_iter = t_roll + t_gae + t_epoch * args.epochs
     return {"value": n * t / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "torch": torch.__version__,
@@ -165,7 +210,7 @@ def cpu_baseline(args, hidden):
 
 def build(args, precision, env_kind, dev, rank):
     """(run, agent, helper, algo) for one leg of the workload (BASELINE configs[1] shapes)."""
-    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.agent import make_agent
     from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
     from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
                                                                 make_synthetic_streams)
@@ -173,11 +218,13 @@ def build(args, precision, env_kind, dev, rank):
     hidden = tuple(int(h) for h in args.hidden.split(","))
     n, t = args.num_envs, args.horizon
     run = make_run(num_envs=n, horizon=t, obs_dim=args.obs_dim, act_dim=args.act_dim,
-                   hidden=hidden, batch_size=args.batch, epochs=args.epochs, rng=args.rng,
-                   seed=rank, precision=precision, rollout_graph=not args.no_graphs,
-                   train_graph=not args.no_graphs)
+                   window=args.window, hidden=hidden, batch_size=args.batch, epochs=args.epochs,
+                   rng=args.rng, seed=rank, precision=precision,
+                   rollout_graph=not args.no_graphs, train_graph=not args.no_graphs,
+                   feature_extractor="LSTM" if args.model == "lstm" else "MLP",
+                   latent=args.latent)
     torch.manual_seed(0)  # identical initial parameters on every rank
-    agent = PPOEngineAgent(run, device=dev)
+    agent = make_agent(run, device=dev)
     streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
     if env_kind == "host":
         from mujoco_reinforcement_learning_amd.environments import HostPhysicsVecEnvHelper
@@ -212,6 +259,7 @@ def time_iterations(algo, steps, warmup, world, dev) -> float:
 
 def leg(args, precision, env_kind, dev) -> dict:
     """One extra single-GPU leg of the same workload (not `value`): its env-steps/s."""
+    _progress(f"leg: precision {precision}, env {env_kind}")
     run, agent, helper, algo = build(args, precision, env_kind, dev, 0)
     try:
         elapsed = time_iterations(algo, args.leg_steps, 1, 1, dev)
@@ -223,8 +271,9 @@ def leg(args, precision, env_kind, dev) -> dict:
             "ms_per_step": 1000 * elapsed / args.leg_steps, "steps": args.leg_steps,
             "warmup": 1, "precision": precision,
             "env": ("device (synthetic dynamics on the GPU)" if env_kind == "device" else
-                    f"host pool ({args.env_workers} worker processes, page-locked shared memory, "
-                    "hipMemcpyAsync on a side stream: obs H2D + action D2H every step)")}
+                    f"host pool ({args.env_workers} worker processes in 2 groups, page-locked "
+                    "device-mapped shared memory: obs / reward / terminated read and actions "
+                    "written over PCIe every step, pipelined by ppo_host_rollout)")}
 
 
 def main():
@@ -252,6 +301,8 @@ def main():
     n, t = args.num_envs, args.horizon
     run, agent, helper, algo = build(args, args.precision, args.env, dev, rank)
     elapsed = time_iterations(algo, args.steps, args.warmup, world, dev)
+    if rank == 0:
+        _progress(f"timed: {1000 * elapsed / args.steps:.2f} ms per iteration")
     classes, kernels = {}, {}
     if not args.no_timing:
         # Per-kernel durations: HIP event pairs on each dispatch packet, over --timing-iters
@@ -277,13 +328,15 @@ def main():
             "config": {"workload": (f"{_ENV_NAMES.get((args.obs_dim, args.act_dim), 'custom')} "
                                     f"shapes: {n} envs/GPU x {t} steps, obs "
                                     f"{args.obs_dim}, act {args.act_dim}, actor+critic "
-                                    f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
+                                    + (f"BiLSTM(latent {args.latent}, window {args.window}) + "
+                                       if args.model == "lstm" else "")
+                                    + f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
                                     f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
                        "epochs": args.epochs, "rng": args.rng, "hipgraphs": not args.no_graphs,
                        "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
                                else f"host pool ({args.env_workers} worker processes, page-locked "
-                                    "shared memory, hipMemcpyAsync on a side stream)"),
+                                    "device-mapped shared memory, ppo_host_rollout)"),
                        "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
     if kernels:
         traffic = load_traffic(args.traffic)

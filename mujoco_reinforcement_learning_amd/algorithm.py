@@ -91,7 +91,7 @@ class PPOEngine:
 
     # ---- ppo.py:13-60 ----------------------------------------------------------------------
     def _graph_ok(self) -> bool:
-        return (self._rng() == "philox" and
+        return (self._rng() == "philox" and hasattr(self.agent.engine, "set_rng_counter") and
                 bool(getattr(self.run.engine_config, "rollout_graph", False)) and
                 bool(getattr(self.environment_helper, "graph_safe", False)) and
                 bool(getattr(self.environment_helper, "writes_into_buffer", False)))

@@ -11,6 +11,8 @@
 #   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
 #   phases    fused-update phase stamps (tools/fused_phases.py)
 #   micro     tools/micro_fused.py timing of the fused update kernel alone
+#   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
+#   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -70,6 +72,15 @@ for S in $STEPS; do
     phases)
       timeout -k 10 200 python tools/fused_phases.py > gpurun_out/phases_${TAG}.txt 2>&1 || fail phases gpurun_out/phases_${TAG}.txt
       cat gpurun_out/phases_${TAG}.txt ;;
+    lstm)
+      timeout -k 10 600 python bench.py --model lstm $LSTM_ARGS > gpurun_out/bench_${TAG}_lstm.json \
+        2> gpurun_out/bench_${TAG}_lstm.err || fail lstm gpurun_out/bench_${TAG}_lstm.err
+      cat gpurun_out/bench_${TAG}_lstm.json ;;
+    lstmtrace)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_${TAG}_lstm -o lstm --output-format csv \
+        -- python3 bench.py --model lstm --steps 1 --warmup 1 $LSTM_ARGS > gpurun_out/rp_${TAG}_lstm.json \
+        2> gpurun_out/rp_${TAG}_lstm.log || fail lstmtrace gpurun_out/rp_${TAG}_lstm.log
+      head -12 $(find gpurun_out/rp_${TAG}_lstm -name "*kernel_stats.csv") ;;
     micro)
       timeout -k 10 200 python tools/micro_fused.py 20 > gpurun_out/micro_${TAG}.txt 2>&1 || fail micro gpurun_out/micro_${TAG}.txt
       cat gpurun_out/micro_${TAG}.txt ;;
