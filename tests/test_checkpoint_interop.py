@@ -76,3 +76,48 @@ def test_reference_restores_engine_configurations(reference):
     assert run.network_config.linear_hidden_shapes == [64, 64]
     assert run.network_config.activation_class is torch.nn.ReLU
     assert run.dtype is torch.float32
+
+
+def test_reference_lstm_modules_load_engine_state_dict(tmp_path):
+    """The LSTM agent's networks (lstm.EngineLSTMActor / EngineLSTMCritic, the state_dict that
+    LSTMEngineAgent.save writes to networks.pth) load strictly into the reference's own
+    LSTMActor / LSTMCritic (weights_only), and the reference forward on those parameters equals
+    the oracle's restated BiLSTM forward."""
+    sys.path.insert(0, REF_SRC)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from entities import features as F
+    from gen_golden_lstm import _make_run
+    from models.lstm.lstm_actor import LSTMActor
+    from models.lstm.lstm_critic import LSTMCritic
+    from mujoco_reinforcement_learning_amd.lstm import EngineLSTMActor, EngineLSTMCritic
+    from oracle import lstm_ref as L
+    from oracle.ppo_ref import RefConfig
+    try:
+        obs, window, act, latent, hidden = 17, 3, 6, 8, [16, 16]
+        torch.manual_seed(5)
+        nets = torch.nn.ModuleDict()
+        nets["actor"] = EngineLSTMActor(obs, latent, 1, window, hidden, act, torch.nn.ReLU, True,
+                                        0.01)
+        nets["critic"] = EngineLSTMCritic(obs, latent, hidden, torch.nn.ReLU, True, 0.01)
+        torch.save({k: v.detach().cpu() for k, v in nets.state_dict().items()},
+                   tmp_path / "networks.pth")
+        _make_run(obs, window, act, latent, 1, hidden, "ReLU")
+        ref = torch.nn.ModuleDict()
+        ref["actor"] = LSTMActor()
+        ref["critic"] = LSTMCritic()
+        ref.load_state_dict(torch.load(tmp_path / "networks.pth", weights_only=True))  # strict
+        cfg = RefConfig(obs_dim=obs, act_dim=act, window=window, actor_hidden=tuple(hidden),
+                        critic_hidden=tuple(hidden))
+        oracle = L.RefLSTMAgent(cfg, latent, 1)
+        oracle.networks.load_state_dict(torch.load(tmp_path / "networks.pth", weights_only=True))
+        x = torch.randn(9, window, obs, generator=torch.Generator().manual_seed(3))
+        with torch.no_grad():
+            mean, std_rep = ref["actor"](x)
+            value = ref["critic"](x)
+            m2, s2 = oracle.networks["actor"](x)
+            v2 = oracle.networks["critic"](x)
+        torch.testing.assert_close(mean, m2, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(std_rep[0], s2, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(value, v2, rtol=1e-6, atol=1e-7)
+    finally:
+        F.Run._instances.clear()
