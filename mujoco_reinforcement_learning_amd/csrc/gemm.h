@@ -49,6 +49,23 @@ struct GemmBatch {
   int prec;                // PPO_PREC_F32 / PPO_PREC_BF16 (host-side dispatch only)
 };
 
+// XCD-aware tile order (cdna_hip_programming.md T1).  Workgroups are dealt round-robin to the
+// 8 XCDs (b % 8 names the XCD group), each with its own L2.  When a problem's tile count is a
+// multiple of 8, block b works on logical tile (b % 8) * (tiles / 8) + b / 8 (row-major over
+// (tile_m, tile_n)): every XCD owns one contiguous run of row tiles with all their column tiles,
+// so an A row panel is fetched into one L2 and reused there, instead of once per XCD.  Other
+// tile counts keep the identity order.  Blocks beyond the problem's tiles return.
+constexpr int kXcds = 8;
+__device__ __forceinline__ bool xcd_tile(int b, int tiles_m, int tiles_n, int &tile_m,
+                                         int &tile_n) {
+  const int tiles = tiles_m * tiles_n;
+  if (b >= tiles) return false;
+  const int id = (tiles % kXcds == 0) ? (b % kXcds) * (tiles / kXcds) + b / kXcds : b;
+  tile_m = id / tiles_n;
+  tile_n = id - tile_m * tiles_n;
+  return true;
+}
+
 // One operand's share of a k-tile: NV vectors of V floats per thread, staged in registers.
 // KC: the stored rows run along k ([rows][k], transposed on the LDS store); otherwise they run
 // along the tile dimension ([k][rows]).  load(): bounds-checked, out-of-range elements load as
@@ -196,9 +213,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(GemmBatch gb) {
     if (EPI == EPI_PARTIAL) K = *gb.rows_n;
     else M = *gb.rows_n;
   }
-  const int tiles_n = (N + BN - 1) / BN;
-  const int tile_m = blockIdx.x / tiles_n;
-  const int tile_n = blockIdx.x - tile_m * tiles_n;
+  int tile_m, tile_n;
+  if (!xcd_tile(static_cast<int>(blockIdx.x), (M + BM - 1) / BM, (N + BN - 1) / BN, tile_m, tile_n))
+    return;  // uniform per block
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   if (m0 >= M || n0 >= N) return;  // uniform per block
   int kbeg = 0, kend = K;
@@ -429,9 +446,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(GemmBatch gb) {
     if (EPI == EPI_PARTIAL) K = *gb.rows_n;
     else M = *gb.rows_n;
   }
-  const int tiles_n = (N + BN - 1) / BN;
-  const int tile_m = blockIdx.x / tiles_n;
-  const int tile_n = blockIdx.x - tile_m * tiles_n;
+  int tile_m, tile_n;
+  if (!xcd_tile(static_cast<int>(blockIdx.x), (M + BM - 1) / BM, (N + BN - 1) / BN, tile_m, tile_n))
+    return;  // uniform per block
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   if (m0 >= M || n0 >= N) return;  // uniform per block
   int kbeg = 0, kend = K;
