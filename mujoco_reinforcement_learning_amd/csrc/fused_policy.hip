@@ -207,13 +207,20 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   //      16 (w & 3) + 4 (lane >> 4) + 2 (w >> 2) + {0, 1} ----
   {
     const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
+    // K split between the wave pair (the update kernel's head order): half 0 sums k-steps
+    // 0..H/64-1, half 1 the rest; partners swap their kept rows through the free A1 region
     f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < H / 32; ++s)
+    for (int s = half * (H / 64); s < (half + 1) * (H / 64); ++s)
       zacc = mfma16(lds_b128(a2img + img_off(16 * tile + n, 4 * s + qg, L::PITCH)),
                     lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
     asm volatile("s_nop 15" : "+v"(zacc));
-    const float zr[2] = {half ? zacc[2] : zacc[0], half ? zacc[3] : zacc[1]};
+    float *const xch = reinterpret_cast<float *>(a1img);  // [8 waves][64 lanes][2]
+    *reinterpret_cast<float2 *>(xch + 2 * (w * 64 + lane)) =
+        half ? make_float2(zacc[0], zacc[1]) : make_float2(zacc[2], zacc[3]);
+    __syncthreads();
+    const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
+    const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
     if constexpr (ACTOR) {
       const bool act_lane = n < A;
       const float sd = act_lane ? expf(hs[8 + n]) : 1.f;

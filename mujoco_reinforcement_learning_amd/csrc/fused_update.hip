@@ -536,9 +536,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     {
       const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
       const float *const srl = reinterpret_cast<const float *>(lds + L::SROW);
+      // K split between the wave pair: wave half 0 sums k-steps 0..H/64-1, half 1 the rest
+      // (half the LDS reads and MFMAs per wave); each hands the partner the two rows it keeps
+      // through the (still free) D2 region.  z = P_lo + P_hi on both sides (commutative), the
+      // same order as the rollout's policy kernel.
       f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < H / 32; ++s) {
+      for (int s = half * (H / 64); s < (half + 1) * (H / 64); ++s) {
         bf16x8 av;
         if constexpr (F32A2) {
           const float *p = a2f + (16 * tile + n) * (L::A2P / 4) + 32 * s + 8 * qg;
@@ -549,7 +553,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         zacc = mfma16(av, lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
       }
       mfma16_drain(zacc);
-      const float zr[2] = {half ? zacc[2] : zacc[0], half ? zacc[3] : zacc[1]};
+      float *const xch = reinterpret_cast<float *>(lds + L::D2);  // [8 waves][64 lanes][2]
+      *reinterpret_cast<float2 *>(xch + 2 * (w * 64 + lane)) =
+          half ? make_float2(zacc[0], zacc[1]) : make_float2(zacc[2], zacc[3]);
+      __syncthreads();
+      const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
+      const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
       const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
       float dz[2];
 #pragma unroll
@@ -755,10 +764,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       }
       gb0 += rs16(bsum, lane);
     }
-    __syncthreads();
     STAMP_AT(8);
 
-    // ---- phase 7: dW0 += D1^T X ----
+    // ---- phase 7: dW0 += D1^T X (the wave's own D1 columns, written by this wave above: no
+    //      barrier before it; the chunk's closing barrier follows) ----
     OPAQUE_LANE();
 #pragma unroll
     for (int ks = 0; ks < R / 16; ++ks) {

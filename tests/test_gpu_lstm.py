@@ -198,3 +198,25 @@ def test_lstm_eval_rollout_matches_oracle(gpu):
     got = algo.test(steps=40)
     want = R.test(env, ref, steps=40)
     assert abs(got - float(want)) <= 1e-5 * max(1.0, abs(float(want))), (got, want)
+
+
+def test_lstm_checkpoint_roundtrip(gpu, tmp_path):
+    """LSTMEngineAgent.save / load (agent.py:47-72 layout): parameters and Adam moments restore
+    exactly; networks.pth carries the reference LSTMActor / LSTMCritic keys."""
+    algo, agent, *_ = make_pair(gpu, n=8, t=8, b=32, epochs=1, feature_extractor="LSTM",
+                                latent=8, window=2, hidden=(16, 16),
+                                experiment_path=str(tmp_path))
+    algo.iterate(verbose=False)
+    agent.run.dynamic_config.current_episode = 2
+    agent.save()
+    saved = agent.packed_params().clone()
+    m_saved = agent.packed(agent.flat_m).clone()
+    agent.flat_params.add_(1.0)
+    agent.flat_m.zero_()
+    agent.load()
+    assert torch.equal(agent.packed_params(), saved)
+    assert torch.equal(agent.packed(agent.flat_m), m_saved)
+    sd = torch.load(tmp_path / "networks" / "2" / "networks.pth", weights_only=True)
+    for key in ("actor.feature_extractor.weight_ih_l0_reverse", "actor.actor_logstd.last_layer.weight",
+                "critic.feature_extractor.0.bias_hh_l0", "critic.network.last_layer.bias"):
+        assert key in sd, key
