@@ -182,6 +182,91 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
   }
 }
 
+// Pipelined variant (the default for T <= 16*KMAX): a block of EB*16 threads owns EB envs and
+// walks the horizon backwards in chunks of TC = 16 time rows, thread (tt, c) holding slot k =
+// time row T-1-(16k+tt) of env c.  Every load of every slot is issued up front (chunk 0 first, so
+// chunk 0 lands first chip-wide); then per chunk: delta and the f64 discount go to LDS, ONE
+// barrier, the EB chain lanes run the chunk's 16 dependent steps while every thread stores the
+// previous chunk's adv / vtarget (the chain that produced them finished before the barrier).  The
+// chain starts when the first chunk has landed instead of after the whole tile, and the stores
+// drain under the chain.  Same operations as gae_kernel: bit-identical.
+template <typename RT, int EB, int KMAX>
+__global__ __launch_bounds__(EB * 16) void gae_pipe_kernel(const float *__restrict__ value,
+                                                           const float *__restrict__ next_value,
+                                                           const RT *__restrict__ reward,
+                                                           const uint8_t *__restrict__ done,
+                                                           const uint8_t *__restrict__ term,
+                                                           int force_last, int n, int t_len,
+                                                           float gamma_f, float lg_f,
+                                                           float *__restrict__ adv,
+                                                           float *__restrict__ vtarget) {
+  constexpr int TC = 16;
+  __shared__ RT s_d[2][TC][EB];     // delta
+  __shared__ RT s_q[2][TC][EB];     // (RT) disc
+  __shared__ float s_o[2][TC][EB];  // f32 advantage
+  const int tid = threadIdx.x, c = tid % EB, tt = tid / EB;
+  const int env = blockIdx.x * EB + c;
+  float lv[KMAX], lvn[KMAX];
+  RT lr[KMAX];
+  uint8_t ltm[KMAX], ldn[KMAX];
+  // unconditional loads from clamped (valid) addresses: no branches or register merges between
+  // them, so every load of every slot is in flight before the first use
+  const int envc = env < n ? env : n - 1;
+  const uint8_t *const dsrc = done ? done : term;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int t = t_len - 1 - (TC * k + tt);
+    const int64_t idx = static_cast<int64_t>(t >= 0 ? t : 0) * n + envc;
+    lv[k] = value[idx];
+    lvn[k] = next_value[idx];
+    lr[k] = reward[idx];
+    ltm[k] = term[idx];
+    ldn[k] = dsrc[idx];
+  }
+  RT prev = 0;
+  // a fixed KMAX chunks (no data-dependent control flow, so no load is sunk into a branch);
+  // rows t < 0 (T < 16 KMAX) carry delta = disc = 0 and come after t = 0 in the chain
+#pragma unroll
+  for (int k = 0; k <= KMAX; ++k) {
+    const int buf = k & 1;
+    if (k < KMAX) {
+      const int t = t_len - 1 - (TC * k + tt);
+      const float g_nt = gamma_f * (ltm[k] ? 0.f : 1.f);
+      const float gv = g_nt * lvn[k];
+      const RT delta = (lr[k] + static_cast<RT>(gv)) - static_cast<RT>(lv[k]);
+      const bool is_done = ldn[k] != 0 || (force_last && t == t_len - 1);
+      const RT q = static_cast<RT>(lg_f * (is_done ? 0.f : 1.f));
+      const bool ok = t >= 0 && env < n;
+      s_d[buf][tt][c] = ok ? delta : static_cast<RT>(0);
+      s_q[buf][tt][c] = ok ? q : static_cast<RT>(0);
+    }
+    __syncthreads();
+    if (k < KMAX && tid < EB) {  // the chain: rows of this chunk in descending time
+      RT d[TC], qq[TC];
+#pragma unroll
+      for (int j = 0; j < TC; ++j) {
+        d[j] = s_d[buf][j][tid];
+        qq[j] = s_q[buf][j][tid];
+      }
+#pragma unroll
+      for (int j = 0; j < TC; ++j) {
+        prev = d[j] + prev * qq[j];
+        s_o[buf][j][tid] = static_cast<float>(prev);
+      }
+    }
+    if (k > 0) {  // chunk k-1: its chain ran before this iteration's barrier
+      const int kp = k - 1;
+      const int t = t_len - 1 - (TC * kp + tt);
+      if (t >= 0 && env < n) {
+        const int64_t idx = static_cast<int64_t>(t) * n + env;
+        const float a = s_o[buf ^ 1][tt][c];
+        adv[idx] = a;
+        vtarget[idx] = a + lv[kp];  // value_target = advantage + state_value (f32)
+      }
+    }
+  }
+}
+
 // ============================================================================================
 // Per-env standardisation over T (ppo.py:66-69 rewards f64, :81-88 advantage / value target f32)
 // x <- ((x - mean_T) / std_T) * scale, unbiased std.  torch computes mean in the tensor dtype and
@@ -561,13 +646,47 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
   while (eb > 1 && (static_cast<size_t>(t) * eb * per_elem > 131072 || t * eb > 16 * 256))
     eb >>= 1;
   const size_t shm = static_cast<size_t>(t) * eb * per_elem + 16;
-  static const int kind = [] {  // PPO_GAE_KERNEL=reg forces the register-chunked scan
-    const char *v = getenv("PPO_GAE_KERNEL");
-    return (v && v[0] == 'r') ? 1 : 0;
+  static const int kind = [] {  // PPO_GAE_KERNEL=reg / lds forces the register-chunked / the
+    const char *v = getenv("PPO_GAE_KERNEL");  // whole-tile LDS scan (experiments)
+    return (v && v[0] == 'r') ? 1 : ((v && v[0] == 'l') ? 2 : 0);
   }();
+  if (kind == 0 && t <= 16 * 16 && n < 131072) {
+    // pipelined scan: 16 envs per block (>= 256 blocks at N = 4096), 32 from N = 16384.
+    // Measured (tools/gae_sweep.py, per-dispatch events, T = 128): N = 4096 6.2 us (LDS-staged
+    // 9.2 us), 16384 12.7 us, 65536 37.7 us = 69 % of HBM (LDS-staged 42 %); at T = 16 a launch
+    // still takes 4.8 us -- the load -> chain -> store latency floor that bounds N = 4096
+    const int peb = (eb_knob == 8 || eb_knob == 16 || eb_knob == 32) ? eb_knob : (n >= 16384 ? 32 : 16);
+    hipStream_t st = as_stream(stream);
+    FreeTimingScope timing_scope;
+    auto go = [&](auto rt_tag, auto eb_tag, auto k_tag) {
+      using RT = decltype(rt_tag);
+      constexpr int EB = decltype(eb_tag)::value, KM = decltype(k_tag)::value;
+      const TimRec rec{KC_GAE,
+                       tim_active() ? intern_name("gae_pipe_kernel<%s, %d, %d>",
+                                                  sizeof(RT) == 8 ? "double" : "float", EB, KM)
+                                    : nullptr,
+                       0.0, gae_bytes(sizeof(RT), done_d != nullptr, n, t)};
+      launch_k(rec, gae_pipe_kernel<RT, EB, KM>, dim3(ceil_div(n, EB)), dim3(EB * 16), 0, st,
+               value_d, next_value_d, static_cast<const RT *>(reward_d), done_d, terminated_d,
+               force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+    };
+    auto by_k = [&](auto rt_tag, auto eb_tag) {
+      if (t <= 16 * 8) go(rt_tag, eb_tag, std::integral_constant<int, 8>{});
+      else go(rt_tag, eb_tag, std::integral_constant<int, 16>{});
+    };
+    auto by_eb = [&](auto rt_tag) {
+      if (peb == 8) by_k(rt_tag, std::integral_constant<int, 8>{});
+      else if (peb == 16) by_k(rt_tag, std::integral_constant<int, 16>{});
+      else by_k(rt_tag, std::integral_constant<int, 32>{});
+    };
+    if (reward_is_f64) by_eb(double{});
+    else by_eb(float{});
+    PPO_LAUNCHED();
+    return 0;
+  }
   // measured (tools/gae_sweep.py, T=128): LDS-staged wins up to N = 65,536, the register-
   // chunked scan from N = 262,144 (its ~16k waves stream near 4.2 TB/s)
-  if (kind == 0 && n < 131072 && shm <= 131072 && t * eb <= 16 * 256) {
+  if (kind != 1 && n < 131072 && shm <= 131072 && t * eb <= 16 * 256) {
     const int blocks = ceil_div(n, eb);
     const int it = ceil_div(static_cast<int64_t>(t) * eb, 256);
     hipStream_t st = as_stream(stream);
