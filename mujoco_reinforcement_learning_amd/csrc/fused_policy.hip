@@ -22,7 +22,13 @@ namespace ppo {
 
 using namespace fu;
 
-constexpr int kPolicyXsPitch = 33;  // f32 state staging pitch (floats)
+constexpr int kPolicyXsPitch = 33;  // f64 observation staging pitch (doubles)
+
+// a pointer as address space 1 (global): loads through it are global_load, not flat_load
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
 
 template <int H>
 struct PolicyLds {
@@ -33,8 +39,11 @@ struct PolicyLds {
   static constexpr int WH = A2 + R * PITCH;                     // bf16 head image [16][H + 8]
   static constexpr int BIAS = WH + HeadImg<H>::BYTES;           // f32 b0[H], b1[H]
   static constexpr int HS = BIAS + 2 * H * 4;                   // f32 head bias[8], logstd[8]
-  static constexpr int XS = HS + 16 * 4;                        // f32 [64][33] standardised states
-  static constexpr int TOTAL = XS + R * kPolicyXsPitch * 4;
+  static constexpr int XD = HS + 16 * 4;                        // f64 [64][33] raw observations
+  static constexpr int ST = XD + R * kPolicyXsPitch * 8;        // f64 [64][16][2] slice mean, std
+  static constexpr int EPS = ST + R * 16 * 2 * 8;               // f32 [64][8] sampling noise
+  static constexpr int SMAP = EPS + R * 8 * 4;                  // int [32] slice of feature f (-1: none)
+  static constexpr int TOTAL = SMAP + kFusedKX * 4;
   static_assert(TOTAL <= 163840, "LDS budget");
 };
 
@@ -42,7 +51,7 @@ template <int H, int ACT, int NH, bool ACTOR, bool STAMP = false>
 __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const FusedNet &N,
                                             char *lds) {
   // STAMP (diagnostic build): wave 0 records s_memtime at each phase boundary
-  uint64_t tst[8];
+  uint64_t tst[9];
 #define PSTAMP(k)                                      \
   if constexpr (STAMP) {                               \
     tst[k] = __builtin_amdgcn_s_memtime();             \
@@ -55,94 +64,153 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   char *const whb = lds + L::WH;
   float *const bias = reinterpret_cast<float *>(lds + L::BIAS);
   float *const hs = reinterpret_cast<float *>(lds + L::HS);
-  float *const xs = reinterpret_cast<float *>(lds + L::XS);
+  double *const xd = reinterpret_cast<double *>(lds + L::XD);
+  double *const st = reinterpret_cast<double *>(lds + L::ST);
+  float *const eps_s = reinterpret_cast<float *>(lds + L::EPS);
+  int *const smap = reinterpret_cast<int *>(lds + L::SMAP);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * R;
   const int A = q.act_dim;
   const int O = q.obs_dim;
-
-  // ---- stage head (bf16 image) / bias parameters ----
-  stage_head_image<H>(whb, N.wh, ACTOR ? A : 1, tid, NT);
-  for (int i = tid; i < 2 * H; i += NT) {
-    const float *b = i < H ? N.b0 : N.b1;
-    bias[i] = b ? b[i % H] : 0.f;
-  }
-  if (tid < 8) hs[tid] = (tid < (ACTOR ? A : 1) && N.bh) ? N.bh[tid] : 0.f;
-  if (ACTOR && tid >= 8 && tid < 16) hs[tid] = (tid - 8 < A) ? q.logstd[tid - 8] : 0.f;
-
-  PSTAMP(1);
+  const int nrow = min(R, q.n - row0);
   // the window / state writer: the actor's workgroups, or the critic's on a value-only call
   const bool writer = ACTOR || !q.do_actor;
-  // ---- observe (A1): thread per env row, the A1 kernels' f64 loops ----
-  if (tid < R) {
-    const int env = row0 + tid;
-    float *dst = xs + tid * kPolicyXsPitch;
-    if (env < q.n) {
-      const double *src = q.obs_d ? q.obs_d + static_cast<int64_t>(env) * O
-                                  : q.window_d + static_cast<int64_t>(env) * O;  // W = 1
-      double x[kFusedKX];
+
+  // ---- prologue: every global load of the step issued before any use (one memory latency for
+  //      the whole prologue).  Observations: element e = (row e/32, feature e%32) of the block's
+  //      rows, from clamped valid addresses (no load behind a branch).  Parameters: the bf16 head
+  //      image's f32 sources, b0 / b1, head bias / log-std.  Sampling noise: host eps or Philox,
+  //      computed here by every thread for (row tid/8, action tid%8) ----
+  // Nullable inputs are read from a valid stand-in address (the head weights) and masked only
+  // where the values are stored to LDS: a load behind a branch, or a select the compiler turns
+  // into one, makes it wait for every load issued before it.  Pointer choices are wave-uniform
+  // (scalar selects) and the loads go through address-space-1 pointers (global, not flat).
+  const float *const fb = N.wh;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  // the Philox counter base first: the noise below waits only for this load
+  const uint64_t obraw =
+      *gptr(q.offset_base ? q.offset_base : reinterpret_cast<const uint64_t *>(fb));
+  const int erow = tid >> 3, ea = tid & 7;
+  const int64_t eidx = static_cast<int64_t>(row0 + erow) * A + ea;
+  float eraw = 0.f;
+  if constexpr (ACTOR) {
+    const int64_t eidx_c = static_cast<int64_t>(row0 + min(erow, nrow - 1)) * A + min(ea, A - 1);
+    eraw = gptr(q.eps ? q.eps : fb)[q.eps ? eidx_c : 0];
+  }
+  const double *const xsrc = q.obs_d ? q.obs_d : q.window_d;  // W = 1: the window is the obs
+  constexpr int XE = R * kFusedKX / NT;                          // 4 elements per thread
+  double xv[XE];
 #pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) x[f] = f < O ? src[f] : 0.0;
+  for (int k = 0; k < XE; ++k) {
+    const int e = tid + NT * k, row = e >> 5, f = e & 31;
+    const int64_t gi = static_cast<int64_t>(row0 + min(row, nrow - 1)) * O + min(f, O - 1);
+    xv[k] = gptr(xsrc)[gi];
+  }
+  constexpr int WHE = 16 * (H / 2) / NT;  // head-image f32 pairs per thread
+  float2 whv[WHE];
+  const int nh_real = ACTOR ? A : 1;
 #pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) dst[f] = (!q.normalize && f < O) ? static_cast<float>(x[f]) : 0.f;
-      if (q.normalize) {
-        for (int sl = 0; sl < q.tab.count; ++sl) {
-          const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
-          const int cnt = hi - lo;
-          if (cnt <= 0) continue;
-          double sum = 0.0;
+  for (int k = 0; k < WHE; ++k) {
+    const int i = tid + NT * k, a = i / (H / 2), f = 2 * (i % (H / 2));
+    const uint64_t u = *gptr(reinterpret_cast<const uint64_t *>(N.wh + min(a, nh_real - 1) * H + f));
+    whv[k] = make_float2(__uint_as_float(static_cast<uint32_t>(u)), __uint_as_float(static_cast<uint32_t>(u >> 32)));
+  }
+  static_assert(2 * H == NT, "one bias value per thread: waves 0..NW/2-1 b0, the rest b1");
+  const float braw = gptr(wu < NW / 2 ? (N.b0 ? N.b0 : fb) : (N.b1 ? N.b1 : fb))[tid % H];
+  // hs[0..7] head bias, hs[8..15] the actor's log-std (wave 0)
+  const float hraw = gptr(wu == 0 && (lane & 8) ? (q.logstd ? q.logstd : fb)
+                                                : (N.bh ? N.bh : fb))[tid & 7];
+  float epsv = 0.f;
+  if (ACTOR && !q.eps && ea < A && erow < nrow)
+    epsv = philox_normal_at(q.seed, q.offset + (q.offset_base ? obraw : 0) + eidx);
+  PSTAMP(1);
+  // ---- LDS images of the loaded values (masking happens here); the raw window row out
+  //      (writer, obs given) ----
 #pragma unroll
-          for (int f = 0; f < kFusedKX; ++f)
-            if (f >= lo && f < hi) sum += x[f];
-          const double mean = sum / cnt;
-          double csum = 0.0;
+  for (int k = 0; k < WHE; ++k) {
+    const int i = tid + NT * k, a = i / (H / 2), f = 2 * (i % (H / 2));
+    const bool ok = a < nh_real;
+    *reinterpret_cast<uint32_t *>(whb + a * HeadImg<H>::PITCH + 2 * f) =
+        pack2(ok ? whv[k].x : 0.f, ok ? whv[k].y : 0.f);
+  }
+  bias[tid] = (wu < NW / 2 ? N.b0 != nullptr : N.b1 != nullptr) ? braw : 0.f;
+  if (tid < 16)
+    hs[tid] = (tid < 8 ? (tid < nh_real && N.bh != nullptr) : (ACTOR && tid - 8 < A)) ? hraw : 0.f;
+  if constexpr (ACTOR) eps_s[tid] = q.eps ? ((ea < A && erow < nrow) ? eraw : 0.f) : epsv;
+  if (tid < kFusedKX) {  // feature -> slice map (the edges are uniform: scalar loads)
+    int sl_of = -1;
+    for (int sl = 0; sl < q.tab.count; ++sl)
+      if (tid >= q.tab.edge[sl] && tid < q.tab.edge[sl + 1]) sl_of = sl;
+    smap[tid] = q.normalize ? sl_of : -1;
+  }
 #pragma unroll
-          for (int f = 0; f < kFusedKX; ++f)
-            if (f >= lo && f < hi) csum += x[f] - mean;
-          const double cmean = csum / cnt;
-          double ss = 0.0;
-#pragma unroll
-          for (int f = 0; f < kFusedKX; ++f)
-            if (f >= lo && f < hi) {
-              const double d = (x[f] - mean) - cmean;
-              ss += d * d;
-            }
-          double sd = sqrt(ss / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
-          if (sd == 0.0) sd = 1.0;
-#pragma unroll
-          for (int f = 0; f < kFusedKX; ++f)
-            if (f >= lo && f < hi) dst[f] = static_cast<float>((x[f] - mean) / sd);
-        }
-      }
-      if (writer && q.obs_d) {
-        double *wrow = q.window_d + static_cast<int64_t>(env) * O;
-#pragma unroll
-        for (int f = 0; f < kFusedKX; ++f)
-          if (f < O) wrow[f] = x[f];
-      }
-    } else {
-#pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) dst[f] = 0.f;
-    }
+  for (int k = 0; k < XE; ++k) {
+    const int e = tid + NT * k, row = e >> 5, f = e & 31;
+    const bool ok = row < nrow && f < O;
+    xd[row * kPolicyXsPitch + f] = ok ? xv[k] : 0.0;
+    if (ok && writer && q.obs_d)
+      q.window_d[static_cast<int64_t>(row0 + row) * O + f] = xv[k];
   }
   __syncthreads();
   PSTAMP(2);
-  // states -> rollout buffer (writer workgroups; coalesced) and the bf16 X image
-  if (writer) {
-    for (int idx = tid; idx < R * O; idx += NT) {
-      const int lrow = idx / O, e = idx - lrow * O, env = row0 + lrow;
-      if (env < q.n) q.state_d[static_cast<int64_t>(env) * O + e] = xs[lrow * kPolicyXsPitch + e];
+  // ---- per-(row, slice) mean and std: wave 0, lane = row, the A1 kernels' f64 loops (same
+  //      order, bit-identical) ----
+  if (q.normalize && tid < R) {
+    double x[kFusedKX];  // the row in registers: the slice loops below are unrolled over f
+#pragma unroll
+    for (int f = 0; f < kFusedKX; ++f) x[f] = xd[tid * kPolicyXsPitch + f];
+    for (int sl = 0; sl < q.tab.count; ++sl) {
+      const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
+      const int cnt = hi - lo;
+      if (cnt <= 0) continue;
+      // The sums add +0.0 for features outside [lo, hi): exact, since each sum starts at +0.0
+      // and so is never -0.0 (x + +0.0 == x for every other x).  The select sits on the operand,
+      // off the dependent chain, and there are no branches (uniform branches per feature cost
+      // more than the extra adds: measured).
+      double sum = 0.0;
+#pragma unroll
+      for (int f = 0; f < kFusedKX; ++f) sum += (f >= lo && f < hi) ? x[f] : 0.0;
+      const double mean = sum / cnt;
+      double csum = 0.0;
+#pragma unroll
+      for (int f = 0; f < kFusedKX; ++f) csum += (f >= lo && f < hi) ? x[f] - mean : 0.0;
+      const double cmean = csum / cnt;
+      double ss = 0.0;
+#pragma unroll
+      for (int f = 0; f < kFusedKX; ++f) {
+        const double d = (x[f] - mean) - cmean;
+        ss += (f >= lo && f < hi) ? d * d : 0.0;
+      }
+      double sd = sqrt(ss / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
+      if (sd == 0.0) sd = 1.0;
+      st[(tid * 16 + sl) * 2] = mean;
+      st[(tid * 16 + sl) * 2 + 1] = sd;
     }
-  }
-  for (int idx = tid; idx < R * 16; idx += NT) {
-    const int xr = idx >> 4, c2 = (idx & 15) * 2;
-    *reinterpret_cast<uint32_t *>(ximg + x_off(xr, c2 >> 3) + 2 * (c2 & 7)) =
-        pack2(xs[xr * kPolicyXsPitch + c2], xs[xr * kPolicyXsPitch + c2 + 1]);
   }
   __syncthreads();
   PSTAMP(3);
+  // ---- standardised states: thread -> (row, feature pair); bf16 X image and the f32 state
+  //      (writer workgroups) ----
+#pragma unroll
+  for (int k = 0; k < R * 16 / NT; ++k) {
+    const int idx = tid + NT * k, xr = idx >> 4, c2 = (idx & 15) * 2;
+    float y[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int f = c2 + u;
+      const double x = xd[xr * kPolicyXsPitch + f];
+      const int sl = smap[f];
+      float v = (!q.normalize && f < O) ? static_cast<float>(x) : 0.f;
+      if (sl >= 0) v = static_cast<float>((x - st[(xr * 16 + sl) * 2]) / st[(xr * 16 + sl) * 2 + 1]);
+      y[u] = xr < nrow ? v : 0.f;
+      if (writer && xr < nrow && f < O) q.state_d[static_cast<int64_t>(row0 + xr) * O + f] = y[u];
+    }
+    *reinterpret_cast<uint32_t *>(ximg + x_off(xr, c2 >> 3) + 2 * (c2 & 7)) = pack2(y[0], y[1]);
+  }
+  __syncthreads();
+  PSTAMP(4);
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----
   bf16x8 ring[PD + 1];
@@ -177,7 +245,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
-  PSTAMP(4);
+  PSTAMP(5);
 
   // ---- L1: a2 = act(W1 a1 + b1) -> A2 image (bf16: the head's operand) ----
   {
@@ -187,7 +255,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
-    PSTAMP(5);
+    PSTAMP(6);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * w + 8 * g + 4 * h;
@@ -200,7 +268,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
   }
   __syncthreads();
-  PSTAMP(6);
+  PSTAMP(7);
 
   // ---- heads: z = a2 . W_h^T on the 16x16x32 MFMA (the update kernel's bf16 products); waves w
   //      and w + 4 form the same 16-row tile and split its rows: lane -> head n = lane & 15, rows
@@ -235,8 +303,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
           if (N.bh) zz += hs[n];
           const float mu = q.omv * tanhf(zz);
           const int64_t idx = static_cast<int64_t>(env) * A + n;
-          const float e = q.eps ? q.eps[idx]
-                                : philox_normal_at(q.seed, q.offset + (q.offset_base ? *q.offset_base : 0) + idx);
+          const float e = eps_s[(env - row0) * 8 + n];  // staged in the prologue
           const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
           if (q.action) q.action[idx] = x;
           if (q.mean) q.mean[idx] = mu;
@@ -256,13 +323,13 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       }
     }
   }
-  PSTAMP(7);
+  PSTAMP(8);
   if constexpr (STAMP) {
     if (tid == 0 && blockIdx.x < 128) {
       uint64_t *dst = q.stamps + (static_cast<int64_t>(blockIdx.y) * 128 + blockIdx.x) * 11;
 #pragma unroll
-      for (int k = 0; k < 7; ++k) dst[k] = tst[k + 1] - tst[k];
-      dst[9] = tst[7] - tst[0];
+      for (int k = 0; k < 8; ++k) dst[k] = tst[k + 1] - tst[k];
+      dst[9] = tst[8] - tst[0];
       dst[10] = tst[0];
     }
   }

@@ -9,9 +9,10 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-PHASES = ["param staging (global -> LDS)", "observe: f64 standardise (thread per env)",
-          "states out + X image", "L0 MFMA + act -> A1", "L1 MFMA pass (issue)",
-          "act + head partials -> zp", "heads (tanh, sample, logp / value) + writes"]
+PHASES = ["prologue: obs / param / eps loads issued, Philox noise", "LDS images + raw window out",
+          "per-(row, slice) f64 mean / std (wave 0)", "standardised states -> X image + state out",
+          "L0 MFMA + act -> A1", "L1 MFMA pass (issue)", "act -> A2 image",
+          "heads (tanh, sample, logp / value) + writes"]
 
 
 def main():
@@ -31,7 +32,8 @@ def main():
     for rep in range(3):
         e.phase_stamps(True)
         e.observe_act(win, st, obs=obs, seed=1, offset=rep, action=a, logp=lp, value=v)
-        s = e.phase_stamps(False).double()
+        # the policy kernel writes 11 slots per workgroup (phase_stamps views them as 13)
+        s = e.phase_stamps(False).flatten()[:2 * 128 * 11].view(2, 128, 11).double()
     g = n // 64
     for y, name in ((0, "actor"), (1, "critic")):
         rows = s[y, :g]
