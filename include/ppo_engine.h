@@ -204,6 +204,11 @@ int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
                          float bc2_sqrt, float one_minus_beta1, float beta2,
                          float one_minus_beta2, float eps, const int32_t *next_rows_d,
                          int next_b, void *stream);
+/* The minibatch row gather alone (ppo.py:106 `batch = memory[indices]` on the staged records):
+ * rows_d (b int32) -> the ctx's gathered-minibatch workspace, so a later
+ * ppo_minibatch_grad_staged(..., PPO_STAGED_ROWS_GATHERED) reads them.  The data-parallel loop
+ * issues it while the gradient all-reduce is in flight (it depends on the row indices only). */
+int ppo_gather_staged_rows(ppo_ctx *ctx, const int32_t *rows_d, int b, void *stream);
 
 /* One whole optimizer step of the staged single-rank path (ppo.py:109-135 for one minibatch,
  * then both optimizers' step()), in at most three launches: [row gather / weight refresh],

@@ -137,6 +137,7 @@ _SIGNATURES = {
     "ppo_update_step_staged": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int]
                                + [ctypes.c_float] * 5 + [c_void_p] * 5 + [ctypes.c_float] * 7
                                + [c_int, c_void_p]),
+    "ppo_gather_staged_rows": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "ppo_adam_pack_gather": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
                              + [ctypes.c_float] * 7 + [c_void_p, c_int, c_void_p]),
     "ppo_adam_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,

@@ -332,10 +332,16 @@ class PPOEngine:
                         eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
                                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
                                                   weights_current=k > 0, rows_gathered=k > 0)
-                        self.dp.allreduce_grad(agent.flat_grad)
+                        # the next minibatch's row gather depends on the row indices only: it
+                        # runs on the compute stream while the gradient all-reduce is in flight
+                        work = self.dp.allreduce_grad_async(agent.flat_grad)
+                        if nxt is not None:
+                            eng.gather_staged_rows(nxt)
+                        if work is not None:
+                            work.wait()
                         eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
                                       one_minus_beta1=1 - beta1, beta2=beta2,
-                                      one_minus_beta2=1 - beta2, eps=eps, next_rows=nxt)
+                                      one_minus_beta2=1 - beta2, eps=eps)
                         continue
                     if staged:
                         eng.update_step_staged(

@@ -38,6 +38,12 @@ __device__ __forceinline__ int img_off(int r, int c, int pitch) {
 // X image: 64-B rows (4 chunks), chunk c of row r at r*64 + 16*(c ^ ((r>>2)&3)).
 __device__ __forceinline__ int x_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 2) & 3)); }
 
+// a pointer as address space 1 (global): loads through it are global_load, not flat_load
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
+
 __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
 
 __device__ __forceinline__ bf16x8 tr_pair(const char *a, const char *b) {
@@ -245,21 +251,32 @@ __device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, i
   static_assert(KS % (PD + 1) == 0, "ring period must divide the k-steps");
   const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
   const char *rowp = img + r * (2 * H);
+  // rolled over all ring periods but the last (one load per k-step: the vmcnt waits of the rolled
+  // loop assume a uniform count) ...
 #pragma unroll 1
-  for (int s0 = 0; s0 < KS; s0 += PD + 1) {
+  for (int s0 = 0; s0 < KS - (PD + 1); s0 += PD + 1) {
 #pragma unroll
     for (int u = 0; u <= PD; ++u) {
       const int s = s0 + u;
       const bf16x8 af = ring[u];
-      // one load per k-step on every path (the last PD re-read step KS-1): a conditional load
-      // would make the in-flight count differ between loop iterations, and the vmcnt waits of
-      // the rolled loop assume a uniform count
-      ring[(u + PD) % (PD + 1)] =
-          *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * min(s + PD, KS - 1));
+      ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * (s + PD));
       const char *p = rowp + 16 * ((2 * s + h) ^ swz);
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
     }
+  }
+  // ... and the last period peeled: only its first k-step still prefetches (step KS-1), so no
+  // redundant weight loads are in flight when the pass ends (a wait on them, forced by a
+  // register reuse after the pass, cost a full L2 round trip per pass)
+#pragma unroll
+  for (int u = 0; u <= PD; ++u) {
+    const int s = KS - (PD + 1) + u;
+    const bf16x8 af = ring[u];
+    if (s + PD < KS)
+      ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * (s + PD));
+    const char *p = rowp + 16 * ((2 * s + h) ^ swz);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
   }
   mfma_drain(acc);
 }

@@ -24,12 +24,6 @@ using namespace fu;
 
 constexpr int kPolicyXsPitch = 33;  // f64 observation staging pitch (doubles)
 
-// a pointer as address space 1 (global): loads through it are global_load, not flat_load
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p) {
-  return (const __attribute__((address_space(1))) T *)(p);
-}
-
 template <int H>
 struct PolicyLds {
   static constexpr int PITCH = 2 * H;

@@ -1307,6 +1307,18 @@ extern "C" int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, 
   return step_tail_launch(r, t, rec, as_stream(stream));
 }
 
+extern "C" int ppo_gather_staged_rows(ppo_ctx *ctx, const int32_t *rows_d, int b, void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx) && ctx->frec && ctx->frec_rows > 0,
+              "ppo_gather_staged_rows: no staged records (ppo_stage_records first)");
+  PPO_REQUIRE(rows_d && b > 0 && b <= ctx->cfg.max_rows,
+              "ppo_gather_staged_rows: b=%d outside [1, max_rows=%d]", b, ctx->cfg.max_rows);
+  TimingScope timing_scope(ctx);
+  const FusedArgs q = fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b,
+                                 nullptr, 0.f, 0.f, 0.f, 0.f, 0.f, true, false);
+  return fused_prep(ctx, q, as_stream(stream));
+}
+
 extern "C" int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
                              const float *sched_d, float neg_step_actor, float neg_step_critic,
                              float bc2_sqrt, float one_minus_beta1, float beta2,

@@ -48,13 +48,22 @@ constexpr int kRedParams = 4 * kRedGroups;  // parameters per block
 __device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t block) {
   __shared__ float4 part[kRedChunks][kRedGroups];
   __shared__ float lred[2][kRedThreads];
+  __shared__ ReduceSeg sseg[kMaxSegs];
   const int tid = threadIdx.x, grp = tid % kRedGroups, chunk = tid / kRedGroups;
   const int64_t i = block * kRedParams + 4 * grp;
+  // The segment table, staged once per block: a per-lane lookup straight from the kernel
+  // arguments compiled to a chain of dependent loads (one round trip per probe and per field).
+  if (tid < q.nseg) sseg[tid] = q.seg[tid];
+  __syncthreads();
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < q.total) {
-    int s = 0;
-    while (s + 1 < q.nseg && q.seg[s + 1].dst <= i) ++s;
-    const ReduceSeg &g = q.seg[s];
+    int s = 0, hi = q.nseg - 1;  // the last segment with dst <= i (dst ascending)
+    while (s < hi) {
+      const int mid = (s + hi + 1) >> 1;
+      if (sseg[mid].dst <= i) s = mid;
+      else hi = mid - 1;
+    }
+    const ReduceSeg &g = sseg[s];
     const int64_t off = i - g.dst;
     const int k0 = (g.nsplit * chunk) / kRedChunks, k1 = (g.nsplit * (chunk + 1)) / kRedChunks;
     // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per

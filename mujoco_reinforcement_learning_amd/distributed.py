@@ -54,6 +54,14 @@ class DataParallel:
             torch.distributed.all_reduce(flat_grad, op=torch.distributed.ReduceOp.SUM,
                                          group=self.pg)
 
+    def allreduce_grad_async(self, flat_grad: torch.Tensor):
+        """Start the SUM all-reduce and return its work handle (None on one rank); the caller
+        issues independent work on the compute stream, then ``wait()``s before using the sum."""
+        if self.world > 1:
+            return torch.distributed.all_reduce(flat_grad, op=torch.distributed.ReduceOp.SUM,
+                                                group=self.pg, async_op=True)
+        return None
+
     def broadcast_params(self, flat: torch.Tensor, src: int = 0) -> None:
         """Start every replica from rank ``src``'s parameters."""
         if self.world > 1:

@@ -340,6 +340,13 @@ class Engine:
             neg_step_critic, bc2_sqrt, one_minus_beta1, beta2, one_minus_beta2, eps, flags,
             _stream(self.device)))
 
+    def gather_staged_rows(self, rows) -> None:
+        """ppo_gather_staged_rows: the minibatch's rows from the staged records into the gathered
+        workspace (read by minibatch_grad_staged(rows_gathered=True))."""
+        _need(rows, "rows", torch.int32, device=self.device)
+        check(self.lib.ppo_gather_staged_rows(self._ctx, ptr(rows), rows.numel(),
+                                              _stream(self.device)))
+
     def adam_pack(self, g, m, v, sched: Optional[torch.Tensor] = None, neg_step_actor: float = 0.0,
                   neg_step_critic: float = 0.0, bc2_sqrt: float = 1.0,
                   one_minus_beta1: float = 0.1, beta2: float = 0.999,

@@ -140,5 +140,6 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu):
     assert all(abs(x) < 1e6 for x in got[0][2])
     kernels = got[0][1]
     assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
-    assert "step_tail_kernel" in kernels, kernels           # Adam + images + next gather
+    assert "adam_pack_kernel" in kernels, kernels           # Adam + weight images
+    assert "fused_prep_kernel" in kernels, kernels          # next gather, under the all-reduce
     assert "reduce_slabs_kernel" in kernels, kernels         # grad folded before the all-reduce

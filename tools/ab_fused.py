@@ -43,7 +43,13 @@ for k in range(50):
     call(1)
 e1.record()
 torch.cuda.synchronize()
-print(json.dumps({"us": 1000 * e0.elapsed_time(e1) / 50}))
+eng.timing(True, capacity=4096)
+for k in range(50):
+    call(1)
+torch.cuda.synchronize()
+ks = {n: 1000 * r["ms"] / r["launches"] for n, r in eng.timing_kernels().items()}
+eng.timing(False)
+print(json.dumps({"us": 1000 * e0.elapsed_time(e1) / 50, "kernels_us": ks}))
 '''
 
 
@@ -58,9 +64,11 @@ def main():
             if out.returncode != 0:
                 print(out.stderr[-2000:])
                 raise SystemExit(f"{tag} failed")
-            us = json.loads(out.stdout.strip().splitlines()[-1])["us"]
+            rec = json.loads(out.stdout.strip().splitlines()[-1])
+            us = rec["us"]
             res[tag].append(us)
-            print(f"round {r} {tag}: {us:.2f} us per fused minibatch gradient", flush=True)
+            kus = ", ".join(f"{k} {v:.2f}" for k, v in sorted(rec["kernels_us"].items()))
+            print(f"round {r} {tag}: {us:.2f} us per fused minibatch gradient ({kus})", flush=True)
     med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
     print(json.dumps({"median_us": med, "rounds": res}))
 
