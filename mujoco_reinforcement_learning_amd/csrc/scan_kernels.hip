@@ -648,13 +648,14 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
   const size_t shm = static_cast<size_t>(t) * eb * per_elem + 16;
   static const int kind = [] {  // PPO_GAE_KERNEL=reg / lds forces the register-chunked / the
     const char *v = getenv("PPO_GAE_KERNEL");  // whole-tile LDS scan (experiments)
-    return (v && v[0] == 'r') ? 1 : ((v && v[0] == 'l') ? 2 : 0);
+    return (v && v[0] == 'r') ? 1 : ((v && v[0] == 'l') ? 2 : ((v && v[0] == 'p') ? 3 : 0));
   }();
-  if (kind == 0 && t <= 16 * 16 && n < 131072) {
+  if ((kind == 0 || kind == 3) && t <= 16 * 16) {
     // pipelined scan: 16 envs per block (>= 256 blocks at N = 4096), 32 from N = 16384.
     // Measured (tools/gae_sweep.py, per-dispatch events, T = 128): N = 4096 6.2 us (LDS-staged
-    // 9.2 us), 16384 12.7 us, 65536 37.7 us = 69 % of HBM (LDS-staged 42 %); at T = 16 a launch
-    // still takes 4.8 us -- the load -> chain -> store latency floor that bounds N = 4096
+    // 9.2 us), 16384 12.7 us, 65536 37.7 us = 69 % of HBM (LDS-staged 42 %), 131072 60 %,
+    // 1048576 58 % (register-chunked scan 38 % / 54 %); at T = 16 a launch still takes 4.8 us --
+    // the load -> chain -> store latency floor that bounds N = 4096
     const int peb = (eb_knob == 8 || eb_knob == 16 || eb_knob == 32) ? eb_knob : (n >= 16384 ? 32 : 16);
     hipStream_t st = as_stream(stream);
     FreeTimingScope timing_scope;
