@@ -62,7 +62,9 @@ for S in $STEPS; do
         $(find gpurun_out/rp_${TAG}_write -name "*counter_collection.csv") gpurun_out/traffic_${TAG}.json ;;
     pmc)
       i=0
-      for P in ${PASSES:-"SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_INSTS_VALU,SQ_INSTS_LDS SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}; do
+      # one pass per space-separated word (at most 8 SQ_ counters each)
+      PASSES=${PASSES:-"SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_INSTS_VALU,SQ_INSTS_LDS SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}
+      for P in $PASSES; do
         i=$((i+1))
         timeout -s KILL 120 rocprofv3 --pmc ${P//,/ } -d gpurun_out/pmc_${TAG}/p$i -o pmc --output-format csv \
           -- python3 tools/micro_fused.py 10 > gpurun_out/pmc_${TAG}_p$i.log 2>&1 || fail pmc$i gpurun_out/pmc_${TAG}_p$i.log
