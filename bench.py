@@ -201,7 +201,9 @@ def cpu_baseline(args, hidden):
     t_iter = t_roll + t_gae + t_epoch * args.epochs
     return {"value": n * t / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "torch": torch.__version__,
-            "sample": (f"oracle/ppo_ref.py (torch {torch.__version__} CPU, {threads} threads): "
+            "sample": (f"oracle/ppo_ref.py, the torch-CPU restatement of ppo.py (the reference itself "
+                       f"was not run: its PPO modules import tensordict / torchrl, which are not "
+                       f"installed; torch {torch.__version__} CPU, {threads} threads): "
                        f"{k} of {t} rollout steps + full GAE + {args.cpu_epochs} of {args.epochs} "
                        f"epochs at N={n}, B={args.batch}, 2x{hidden[0]} MLP; extrapolated "
                        f"(rollout {t_roll:.2f}s, gae {t_gae:.3f}s, epoch {t_epoch:.2f}s/iter-scaled)"),

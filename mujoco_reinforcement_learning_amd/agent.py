@@ -14,11 +14,12 @@ import torch
 from torch import nn
 
 from . import engine as E
-from .features import Run
+from .features import REFERENCE_CRITIC_HIDDEN, Run
+
+ENGINE_RNG_FILE = "engine_rng.pth"  # the per-rank torch generator of local data parallelism
 from .models import EngineActor, EngineCritic, move_to_flat
 
 _ACT_NAMES = {nn.ReLU: "relu", nn.Tanh: "tanh", nn.ELU: "elu"}
-REFERENCE_CRITIC_HIDDEN = (128, 128)  # models/critic.py:14
 
 
 class FlatAdam:
@@ -298,6 +299,10 @@ class PPOEngineAgent:
             sd["state"] = {i: {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in s.items()}
                            for i, s in sd["state"].items()}
             torch.save(sd, f"{path}/optimizer_{name}.pth")
+        algo = getattr(self, "_algorithm", None)
+        state = algo.rng_state() if algo is not None else None
+        if state is not None:  # engine-only file: the reference never reads it
+            torch.save(state, f"{path}/{ENGINE_RNG_FILE}")
         run.save()
 
     def load(self):
@@ -314,3 +319,6 @@ class PPOEngineAgent:
         for name, opt in self.optimizers.items():
             opt.load_state_dict(torch.load(f"{path}/optimizer_{name}.pth", map_location="cpu",
                                            weights_only=True))
+        algo = getattr(self, "_algorithm", None)
+        if algo is not None and os.path.exists(f"{path}/{ENGINE_RNG_FILE}"):
+            algo.set_rng_state(torch.load(f"{path}/{ENGINE_RNG_FILE}", weights_only=True))

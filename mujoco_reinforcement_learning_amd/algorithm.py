@@ -43,6 +43,7 @@ class PPOEngine:
                                                            "local"))
         self.world = self.dp.world
         self.dp.broadcast_params(agent.flat_params)  # every replica starts from rank 0's params
+        agent._algorithm = self  # agent.save / load carry the per-rank generator (engine_rng.pth)
         ec, nc = self.run.environment_config, self.run.network_config
         self.buffer = RolloutBuffer(ec.num_envs, ec.maximum_timesteps, nc.input_shape,
                                     ec.window_length, nc.output_shape, agent.device)
@@ -81,13 +82,38 @@ class PPOEngine:
         """Generator for the torch-RNG draws: the global CPU generator (the reference's stream)
         except in local data-parallel mode, where every rank starts from the same seeded
         parameters and would otherwise draw identical noise and row orders on every env shard;
-        there each rank forks its own generator keyed by (seed, rank)."""
+        there each rank forks its own generator.  Its key mixes the user's global seed
+        (torch.initial_seed(), so torch.manual_seed changes the run), the engine seed and the
+        rank; it is a CPU Mersenne-Twister stream, independent of the device Philox key
+        (seed * 1_000_003 + 17 + 7919 * rank) that only keys counter-based rollout noise.  Its
+        state is checkpointed by agent.save() (engine_rng.pth) and restored by agent.load()."""
         if not (self.dp.active and self.dp.mode == "local"):
             return None
         if getattr(self, "_rank_gen", None) is None:
-            self._rank_gen = torch.Generator().manual_seed(
-                self._seed() * 1_000_003 + 7919 * (self.dp.rank + 1))
+            key = (torch.initial_seed() * 1_000_003 + self._seed() * 7_919_993
+                   + 7919 * (self.dp.rank + 1)) % (1 << 63)
+            self._rank_gen = torch.Generator().manual_seed(key)
+            if getattr(self, "_pending_rng_state", None) is not None:
+                self._rank_gen.set_state(self._pending_rng_state)
+                self._pending_rng_state = None
         return self._rank_gen
+
+    def rng_state(self) -> Optional[dict]:
+        """The per-rank generator's state (local data-parallel torch-RNG runs), for checkpoints."""
+        gen = getattr(self, "_rank_gen", None)
+        return None if gen is None else {"rank": self.dp.rank, "state": gen.get_state()}
+
+    def set_rng_state(self, state: Optional[dict]) -> None:
+        if not state:
+            return
+        if state.get("rank") != self.dp.rank:
+            raise ValueError(f"engine_rng.pth holds rank {state.get('rank')}'s generator, "
+                             f"this is rank {self.dp.rank}")
+        gen = getattr(self, "_rank_gen", None)
+        if gen is None:
+            self._pending_rng_state = state["state"]
+        else:
+            gen.set_state(state["state"])
 
     # ---- ppo.py:13-60 ----------------------------------------------------------------------
     def _graph_ok(self) -> bool:

@@ -22,6 +22,7 @@
 // release_half / finish_half), tested bit for bit against the device env.
 #include <sched.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -150,6 +151,11 @@ extern "C" int ppo_host_rollout(ppo_ctx *ctx, ppo_host_pool_desc *pool, double *
     step[g] = 0;
   }
   const auto t0 = std::chrono::steady_clock::now();
+  // Watchdog: the call fails only when NO group has advanced for the stall limit (default 120 s,
+  // PPO_HOST_ROLLOUT_STALL_MS overrides it per call), however long the whole rollout takes.
+  const char *stall_env = getenv("PPO_HOST_ROLLOUT_STALL_MS");
+  const long stall_ms = stall_env ? std::max(1L, atol(stall_env)) : 120000L;
+  auto last_progress = t0;
   // PPO_HOST_ROLLOUT_STATS=1: per-phase host wall time (diagnostics on stderr)
   static const bool stats = getenv("PPO_HOST_ROLLOUT_STATS") != nullptr;
   double w_d2h = 0, w_phys = 0, w_enq = 0;
@@ -159,6 +165,7 @@ extern "C" int ppo_host_rollout(ppo_ctx *ctx, ppo_host_pool_desc *pool, double *
   std::chrono::steady_clock::time_point mark[PPO_MAX_GROUPS];
   for (int g = 0; g < G; ++g) mark[g] = t0;
   int remaining = G;
+  bool stalled = false;
   for (long spins = 0; remaining > 0 && !rc; ++spins) {
     bool progress = false;
     for (int g = 0; g < G && !rc; ++g) {
@@ -197,13 +204,36 @@ extern "C" int ppo_host_rollout(ppo_ctx *ctx, ppo_host_pool_desc *pool, double *
         progress = true;
       }
     }
-    if (!progress && (spins & 1023) == 1023) {
+    if (progress) {
+      last_progress = std::chrono::steady_clock::now();
+    } else if ((spins & 1023) == 1023) {
       sched_yield();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
-        ppo::set_error("ppo_host_rollout: no progress for 120 s (a host physics worker died?)");
+      if (std::chrono::steady_clock::now() - last_progress > std::chrono::milliseconds(stall_ms)) {
+        ppo::set_error("ppo_host_rollout: no group advanced for %ld ms (a host physics worker "
+                       "died or stalled)", stall_ms);
         rc = PPO_EHIP;
+        stalled = true;
       }
     }
+  }
+  if (stalled) {
+    // Released groups' workers may still be writing the shared memory: give them a grace period
+    // (the stall limit again) to publish, so a caller that closes or reuses the pool after the
+    // error does not race them; report the pool unusable when they do not.
+    const auto g0 = std::chrono::steady_clock::now();
+    bool settled = false;
+    while (!settled && std::chrono::steady_clock::now() - g0 < std::chrono::milliseconds(stall_ms)) {
+      settled = true;
+      for (int g = 0; g < G; ++g) {
+        if (state[g] != kRunning) continue;
+        for (int w = pool->worker_lo[g]; w < pool->worker_hi[g]; ++w)
+          settled = settled && __atomic_load_n(&pool->done[w], __ATOMIC_ACQUIRE) == pool->gen[g];
+      }
+      if (!settled) sched_yield();
+    }
+    if (!settled)
+      ppo::set_error("ppo_host_rollout: no group advanced for %ld ms and released workers did not "
+                     "finish; the pool is unusable (close it)", stall_ms);
   }
   if (stats)
     fprintf(stderr,

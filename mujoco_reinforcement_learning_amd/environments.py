@@ -196,8 +196,9 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
 
     def __init__(self, streams: Optional[dict] = None, run: Optional[Run] = None,
                  device: Optional[torch.device] = None, seed: int = 0, p_terminate: float = 0.0,
-                 workers: int = 4, overlap: bool = True):
+                 workers: int = 4, overlap: bool = True, step_delay: float = 0.0):
         self._workers = workers
+        self._step_delay = step_delay  # test hook: seconds every worker sleeps per physics step
         self._overlap = overlap
         self.pool = None
         super().__init__(streams, run, device, seed, p_terminate)
@@ -213,7 +214,7 @@ class HostPhysicsVecEnvHelper(SyntheticVecEnvHelper):
         groups = 2 if (self._overlap and n >= 2 and self._workers >= 2) else 1
         self.pool = HostPhysicsPool(self.base_obs.cpu().numpy(), self.base_reward.cpu().numpy(),
                                     self.base_terminated.cpu().numpy(), a, self._workers,
-                                    groups=groups)
+                                    groups=groups, step_delay=self._step_delay)
         gb = self.pool.group_bounds
         self.halves = [(gb[g], gb[g + 1]) for g in range(self.pool.groups)]
         self._registered = []

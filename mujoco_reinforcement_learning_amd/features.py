@@ -150,6 +150,9 @@ class EngineConfig:
     precision: str = "f32"
 
 
+REFERENCE_CRITIC_HIDDEN = (128, 128)  # models/critic.py:14
+
+
 @dataclass
 class Run(metaclass=Singleton):
     rewards_config: RewardConfig
@@ -192,6 +195,8 @@ class Run(metaclass=Singleton):
         resume); the engine-only knobs go to engine_configuration.json beside it."""
         cfg = {"run": asdict(self)}
         engine = cfg["run"].pop("engine_config")
+        if engine.get("critic_hidden_shapes") is None:  # persist the critic widths explicitly
+            engine["critic_hidden_shapes"] = list(REFERENCE_CRITIC_HIDDEN)
         cfg["run"]["dtype"] = str(cfg["run"]["dtype"]).split(".")[-1]
         cfg["run"]["network_config"]["activation_class"] = (
             self.network_config.activation_class.__name__)
@@ -219,6 +224,12 @@ class Run(metaclass=Singleton):
             DynamicConfig(*cfg.pop("dynamic_config").values()),
         ]
         engine_kw = cfg.pop("engine_config", None)
+        if engine_kw is not None and engine_kw.get("critic_hidden_shapes") is None:
+            # a run directory of the earlier format embedded engine_config, where a null critic
+            # width meant "the actor's widths": keep building the critic it saved
+            nc = parts[6]
+            engine_kw["critic_hidden_shapes"] = [
+                int(h) for h in list(nc.linear_hidden_shapes)[:nc.num_linear_layers]]
         side = f"{experiment_path}/{ENGINE_CONFIG_FILE}"
         if engine_kw is None and os.path.exists(side):
             with open(side) as fh:

@@ -99,7 +99,7 @@ def _wait_change(word: np.ndarray, idx: int, old: int, stop: np.ndarray = None) 
         time.sleep(0)
 
 
-def _worker(wid: int, grp: int, lo: int, hi: int, specs) -> None:
+def _worker(wid: int, grp: int, lo: int, hi: int, specs, step_delay: float = 0.0) -> None:
     shms, v = _attach(specs)
     ctrl, done = v["ctrl"][grp], v["done"]
     native = _native_step()
@@ -113,6 +113,8 @@ def _worker(wid: int, grp: int, lo: int, hi: int, specs) -> None:
                 step_slice_native(native, v, int(ctrl[_CTRL_T]), lo, hi)
             else:
                 step_slice(v, int(ctrl[_CTRL_T]), lo, hi)
+            if step_delay > 0:  # test hook: a slow physics step (the native driver's watchdog)
+                time.sleep(step_delay)
             done[wid] = gen  # publish after the slice's outputs are written
     finally:
         for s in shms:
@@ -123,7 +125,7 @@ class HostPhysicsPool:
     """P worker processes stepping env slices in shared memory (see the module docstring)."""
 
     def __init__(self, base_obs: np.ndarray, base_reward: np.ndarray, base_term: np.ndarray,
-                 act_dim: int, workers: int = 4, groups: int = 1):
+                 act_dim: int, workers: int = 4, groups: int = 1, step_delay: float = 0.0):
         t1, n, o = base_obs.shape
         self.num_envs, self.obs_dim, self.act_dim = n, o, act_dim
         self.groups = max(1, min(int(groups), n))
@@ -165,7 +167,7 @@ class HostPhysicsPool:
             for k, wid in enumerate(ids):
                 self._procs.append(ctx.Process(target=_worker, daemon=True,
                                                args=(wid, g, int(wb[k]), int(wb[k + 1]),
-                                                     self.specs)))
+                                                     self.specs, float(step_delay))))
         for p in self._procs:
             p.start()
         self._closed = False

@@ -164,11 +164,27 @@ def test_checkpoint_roundtrip(gpu, tmp_path):
     assert "actor.actor.first_layers.0.weight" in sd and "critic.network.last_layer.bias" in sd
 
 
-@pytest.mark.parametrize("prec,hidden", [("f32", (64, 64)), ("bf16", (256, 256))])
-def test_host_physics_pool_matches_device_env(gpu, prec, hidden):
-    """HostPhysicsVecEnvHelper (P=2 worker processes, page-locked shared memory, hipMemcpyAsync
-    on a side stream) drives two PPO iterations to the same rollout buffers, losses and
-    parameters, bit for bit, as the device-resident synthetic env on the same streams."""
+def _python_pipelined(cls):
+    """The helper without its native descriptor: PPOEngine drives the per-half Python protocol
+    (begin_half / release_half / finish_half, algorithm.py _rollout_pipelined) instead of
+    ppo_host_rollout -- the path any engine without host_rollout (the LSTM agent) takes."""
+    class _Py(cls):
+        @property
+        def native_desc(self):
+            raise AttributeError("native_desc")
+    return _Py
+
+
+@pytest.mark.parametrize("prec,hidden,path,rng", [("f32", (64, 64), "native", "philox"),
+                                                  ("bf16", (256, 256), "native", "philox"),
+                                                  ("f32", (64, 64), "python", "torch"),
+                                                  ("bf16", (256, 256), "python", "philox")])
+def test_host_physics_pool_matches_device_env(gpu, prec, hidden, path, rng):
+    """HostPhysicsVecEnvHelper (P=2 worker processes, page-locked shared memory) drives two PPO
+    iterations to the same rollout buffers, losses and parameters, bit for bit, as the
+    device-resident synthetic env on the same streams -- through the native driver
+    (ppo_host_rollout) and through the Python pipelined protocol, with host (torch) and device
+    (Philox) noise."""
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
     from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
     from mujoco_reinforcement_learning_amd.environments import (HostPhysicsVecEnvHelper,
@@ -177,16 +193,19 @@ def test_host_physics_pool_matches_device_env(gpu, prec, hidden):
     from mujoco_reinforcement_learning_amd.runconfig import make_run
     n, t, b = 96, 16, 512
     streams = make_synthetic_streams(n, t, 17, seed=9, p_terminate=0.05)
+    host_cls = HostPhysicsVecEnvHelper if path == "native" else _python_pipelined(
+        HostPhysicsVecEnvHelper)
     res = []
-    for cls in (SyntheticVecEnvHelper, HostPhysicsVecEnvHelper):
-        run = make_run(num_envs=n, horizon=t, hidden=hidden, batch_size=b, epochs=2, rng="philox",
+    for cls in (SyntheticVecEnvHelper, host_cls):
+        run = make_run(num_envs=n, horizon=t, hidden=hidden, batch_size=b, epochs=2, rng=rng,
                        seed=2, precision=prec)
         torch.manual_seed(2)
         agent = PPOEngineAgent(run, device=gpu)
-        kw = {"workers": 2} if cls is HostPhysicsVecEnvHelper else {}
+        kw = {"workers": 2} if cls is host_cls else {}
         helper = cls(streams, run, device=gpu, **kw)
         algo = PPOEngine(helper, agent, log=lambda m: None)
         snaps = []
+        torch.manual_seed(11)  # the torch-RNG draws start from the same global state
         for _ in range(2):
             algo.iterate(verbose=False)
             torch.cuda.synchronize()
@@ -194,10 +213,52 @@ def test_host_physics_pool_matches_device_env(gpu, prec, hidden):
             snaps.append([x.cpu().clone() for x in (buf.states, buf.actions, buf.reward,
                                                    buf.terminated, buf.values, buf.advantage,
                                                    agent.packed_params())])
-        if cls is HostPhysicsVecEnvHelper:
+        if cls is host_cls:
+            assert hasattr(helper, "native_desc") == (path == "native")
             helper.close()
         res.append(snaps)
     names = ("states", "actions", "reward", "terminated", "values", "advantage", "params")
     for it, (d, h) in enumerate(zip(*res)):
         for name, x, y in zip(names, d, h):
             assert torch.equal(x, y), f"iteration {it}: {name} differs (host pool vs device env)"
+
+
+def _host_algo(gpu, n, t, step_delay):
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (HostPhysicsVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    streams = make_synthetic_streams(n, t, 17, seed=3)
+    run = make_run(num_envs=n, horizon=t, hidden=(64, 64), batch_size=n * t, epochs=1,
+                   rng="philox", seed=1)
+    agent = PPOEngineAgent(run, device=gpu)
+    helper = HostPhysicsVecEnvHelper(streams, run, device=gpu, workers=2, step_delay=step_delay)
+    return PPOEngine(helper, agent, log=lambda m: None), helper
+
+
+def test_host_rollout_watchdog_measures_stalls_not_total_time(gpu, monkeypatch):
+    """ppo_host_rollout's watchdog fires only when no group advances for the stall limit: a
+    rollout whose physics steps take 60 ms each runs 16 steps (~1 s in total) under a 400 ms
+    limit; a worker that takes 1.5 s for one step fails the call with the stall message, after
+    which the pool can still be closed cleanly."""
+    from mujoco_reinforcement_learning_amd._lib import EngineError
+    import time
+    monkeypatch.setenv("PPO_HOST_ROLLOUT_STALL_MS", "400")
+    algo, helper = _host_algo(gpu, 64, 16, 0.06)
+    try:
+        t0 = time.perf_counter()
+        algo.rollout()
+        torch.cuda.synchronize()
+        took = time.perf_counter() - t0
+        print(f"steady rollout: {took:.2f} s under a 0.4 s stall limit")
+        assert took > 0.4
+        assert bool(torch.isfinite(algo.buffer.values).all())
+    finally:
+        helper.close()
+    algo, helper = _host_algo(gpu, 64, 4, 1.5)
+    try:
+        with pytest.raises(EngineError, match="no group advanced"):
+            algo.rollout()
+    finally:
+        helper.close()
