@@ -404,6 +404,73 @@ int ppo_lstm_minibatch_grad(ppo_lstm_ctx *ctx, const float *states_d, const floa
                             float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                             float inv_ba, void *stream);
 
+/* ---- Pixel-observation actor-critic (BASELINE.json configs[4]) ----------------------------
+ * dm_control cheetah-run pixel observations: u8 frames (H, W, C) = (84, 84, 3), HWC.  The
+ * reference has NO pixel / CNN path (running_dm_control.py:56-91 is state-observation humanoid),
+ * so this model is the engine's own declaration: each net is the Nature-DQN
+ * encoder -- Conv2d(3, 32, 8, 4) ReLU, Conv2d(32, 64, 4, 2) ReLU, Conv2d(64, 64, 3, 1) ReLU,
+ * flatten (torch CHW order, 3136 features) -- followed by the reference's NetworkBlock heads:
+ * actor mean = output_max_value * tanh(MLP(features)) with the state-independent actor_logstd of
+ * models/linear/actor.py:9-30, critic value = MLP(features) (models/critic.py:6-25); actor and
+ * critic keep separate encoders (they have separate optimizers, ppo_agent.py:15-22).  Pixels are
+ * scaled by 1/255 (x / 255.f).  Flat parameters, torch parameters() order with 16-float aligned
+ * tensors:  actor: actor_logstd[A], encoder.{0,2,4}.weight [co][ci][k][k] + .bias,
+ * actor.first_layers.* / last_layer.*;  critic: encoder.*, network.*  (ppo_cnn_param_layout).
+ * The convolutions are implicit GEMMs on MFMA (csrc/conv.h): exact f32 operands in PPO_PREC_F32,
+ * bf16 operands with f32 accumulation in PPO_PREC_BF16. */
+typedef struct ppo_cnn_cfg {
+  int32_t height, width, channels;  /* pixel frame: 84, 84, 3 (the compiled encoder geometry) */
+  int32_t act_dim;                  /* NetworkConfig.output_shape (A), <= 32 */
+  int32_t activation;               /* PPO_ACT_* of the MLP hidden layers (the encoder: ReLU) */
+  int32_t use_bias;                 /* NetworkConfig.use_bias of the actor MLP */
+  int32_t n_hidden;                 /* NetworkConfig.num_linear_layers (actor and critic) */
+  int32_t hidden[PPO_MAX_LAYERS];   /* NetworkConfig.linear_hidden_shapes */
+  float output_max_value;           /* NetworkConfig.output_max_value (actor.py:30) */
+  int32_t max_rows;                 /* workspace rows = max(num_envs, minibatch) */
+} ppo_cnn_cfg;
+typedef struct ppo_cnn_ctx ppo_cnn_ctx;
+
+/* Replaces PPOAgent.initialize_networks' model construction (ppo_agent.py:11-13). */
+int ppo_cnn_ctx_create(const ppo_cnn_cfg *cfg, int device, ppo_cnn_ctx **out);
+int ppo_cnn_ctx_destroy(ppo_cnn_ctx *ctx);
+int ppo_cnn_param_layout(const ppo_cnn_ctx *ctx, int64_t *offsets, int max_tensors,
+                         int64_t *total, int64_t *n_actor);
+int ppo_cnn_bind_params(ppo_cnn_ctx *ctx, float *params_d);
+int ppo_cnn_set_precision(ppo_cnn_ctx *ctx, int prec);
+int ppo_cnn_set_rng_counter(ppo_cnn_ctx *ctx, const uint64_t *counter_d);
+/* Actor.forward + Critic.forward on frames_d[n][H*W*C] u8: mean[n][A], value[n]; optionally the
+ * encoder outputs (the flattened features [n][3136], f32) of both nets.  Nullable outputs are
+ * skipped. */
+int ppo_cnn_forward(ppo_cnn_ctx *ctx, const uint8_t *frames_d, int n, float *mean_d,
+                    float *value_d, float *feat_actor_d, float *feat_critic_d, void *stream);
+/* The PPO rollout step (ppo.py:22-26) on pixel frames: action = eps*std + mean (eps from eps_d,
+ * or Philox(seed, offset + counter + i) when eps_d is null), log_prob summed over actions, V(s). */
+int ppo_cnn_policy_step(ppo_cnn_ctx *ctx, const uint8_t *frames_d, int n, const float *eps_d,
+                        uint64_t seed, uint64_t offset, float *action_d, float *logp_d,
+                        float *value_d, float *mean_d, void *stream);
+/* One minibatch of ppo.py:108-135 with the pixel actor-critic: frames_d = the rollout buffer's
+ * frames [(T+1)*N][H*W*C] u8, rows_d the minibatch's storage rows (t*N + n), the other arrays as
+ * ppo_minibatch_grad; grad_d = the flat gradient, loss_d[2] = (actor, critic) loss. */
+int ppo_cnn_minibatch_grad(ppo_cnn_ctx *ctx, const uint8_t *frames_d, const float *actions_d,
+                           const float *logp_d, const float *adv_d, const float *vt_d,
+                           const int32_t *rows_d, int b, float *grad_d, float *loss_d,
+                           float clip_lo, float clip_hi, float entropy_coef, float inv_b,
+                           float inv_ba, void *stream);
+/* Per-launch event timing of this context (as ppo_ctx_timing / ppo_ctx_timing_kernel). */
+int ppo_cnn_timing(ppo_cnn_ctx *ctx, int enable, int capacity);
+int ppo_cnn_timing_kernel(ppo_cnn_ctx *ctx, int index, const char **name, int *kclass,
+                          double *total_ms, int64_t *launches, double *flops, double *bytes);
+/* Synthetic pixel VecEnv step (bench / test harness; physics is out of scope): frame t of env n,
+ *   pix[y][x][c] = (mix32(seed, t, n, (y*W + x)*C + c) + q[(2c + ((x + y) & 1)) % A]) & 255,
+ *   q[j] = clamp(floor(8 * action[n][j]), -64, 63)   (q = 0 when action_d is NULL: the reset frame)
+ * written to frames_out_d[n][H*W*C]; with base_reward_d / base_term_d (T, N) and t >= 1 also
+ * reward_out[n] = base_reward[t-1][n] - 0.01 * sum_a a^2 (f64, a summed in order) and
+ * term_out[n] = base_term[t-1][n] (the state-env formulas of ppo_synthetic_env_step). */
+int ppo_synthetic_pixel_step(uint32_t seed, int t, const float *action_d, int n, int h, int w,
+                             int c, int a, uint8_t *frames_out_d, const float *base_reward_d,
+                             const uint8_t *base_term_d, double *reward_out_d,
+                             uint8_t *term_out_d, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

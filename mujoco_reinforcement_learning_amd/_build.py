@@ -12,7 +12,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip",
-           "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip"]
+           "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip",
+           "csrc/cnn_engine.hip", "csrc/gemm_ops.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 

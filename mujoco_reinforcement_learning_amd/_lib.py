@@ -50,6 +50,22 @@ class LstmCfg(ctypes.Structure):
     ]
 
 
+class CnnCfg(ctypes.Structure):
+    """``ppo_cnn_cfg`` (include/ppo_engine.h)."""
+    _fields_ = [
+        ("height", c_int32),
+        ("width", c_int32),
+        ("channels", c_int32),
+        ("act_dim", c_int32),
+        ("activation", c_int32),
+        ("use_bias", c_int32),
+        ("n_hidden", c_int32),
+        ("hidden", c_int32 * PPO_MAX_LAYERS),
+        ("output_max_value", c_float),
+        ("max_rows", c_int32),
+    ]
+
+
 PPO_MAX_GROUPS = 4
 
 
@@ -159,6 +175,26 @@ _SIGNATURES = {
                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_lstm_minibatch_grad": (c_int, [c_void_p] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]
                                 + [ctypes.c_float] * 5 + [c_void_p]),
+    # pixel-observation actor-critic (cnn_engine.hip, conv.h)
+    "ppo_cnn_ctx_create": (c_int, [POINTER(CnnCfg), c_int, POINTER(c_void_p)]),
+    "ppo_cnn_ctx_destroy": (c_int, [c_void_p]),
+    "ppo_cnn_param_layout": (c_int, [c_void_p, POINTER(c_int64), c_int, POINTER(c_int64),
+                                     POINTER(c_int64)]),
+    "ppo_cnn_bind_params": (c_int, [c_void_p, c_void_p]),
+    "ppo_cnn_set_precision": (c_int, [c_void_p, c_int]),
+    "ppo_cnn_set_rng_counter": (c_int, [c_void_p, c_void_p]),
+    "ppo_cnn_forward": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 5),
+    "ppo_cnn_policy_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_uint64, c_uint64]
+                            + [c_void_p] * 5),
+    "ppo_cnn_minibatch_grad": (c_int, [c_void_p] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]
+                               + [ctypes.c_float] * 5 + [c_void_p]),
+    "ppo_cnn_timing": (c_int, [c_void_p, c_int, c_int]),
+    "ppo_cnn_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
+                                      POINTER(c_double), POINTER(c_int64), POINTER(c_double),
+                                      POINTER(c_double)]),
+    "ppo_synthetic_pixel_step": (c_int, [ctypes.c_uint32, c_int, c_void_p, c_int, c_int, c_int,
+                                         c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -127,12 +127,17 @@ class ExponentialLRFacade:
 def make_agent(run: Optional[Run] = None, device: Optional[torch.device] = None,
                max_rows: Optional[int] = None):
     """The agent NetworkConfig.feature_extractor selects: "LSTM" -> the reference PPOAgent's
-    LSTM actor / critic (ppo_agent.py:2-3; lstm.LSTMEngineAgent), anything else -> the MLP
-    actor-critic of north_star (PPOEngineAgent)."""
+    LSTM actor / critic (ppo_agent.py:2-3; lstm.LSTMEngineAgent), "CNN" -> the pixel actor /
+    critic of BASELINE configs[4] (cnn.CNNEngineAgent), anything else -> the MLP actor-critic of
+    north_star (PPOEngineAgent)."""
     run = run or Run.instance()
-    if str(getattr(run.network_config, "feature_extractor", "MLP")).upper() == "LSTM":
+    kind = str(getattr(run.network_config, "feature_extractor", "MLP")).upper()
+    if kind == "LSTM":
         from .lstm import LSTMEngineAgent
         return LSTMEngineAgent(run, device, max_rows)
+    if kind == "CNN":  # pixel observations (BASELINE configs[4]; cnn.py)
+        from .cnn import CNNEngineAgent
+        return CNNEngineAgent(run, device, max_rows)
     return PPOEngineAgent(run, device, max_rows)
 
 

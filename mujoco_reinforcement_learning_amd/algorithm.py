@@ -45,8 +45,11 @@ class PPOEngine:
         self.dp.broadcast_params(agent.flat_params)  # every replica starts from rank 0's params
         agent._algorithm = self  # agent.save / load carry the per-rank generator (engine_rng.pth)
         ec, nc = self.run.environment_config, self.run.network_config
-        self.buffer = RolloutBuffer(ec.num_envs, ec.maximum_timesteps, nc.input_shape,
-                                    ec.window_length, nc.output_shape, agent.device)
+        if hasattr(agent, "make_buffer"):  # agents with their own state storage (u8 frames)
+            self.buffer = agent.make_buffer(ec.num_envs, ec.maximum_timesteps)
+        else:
+            self.buffer = RolloutBuffer(ec.num_envs, ec.maximum_timesteps, nc.input_shape,
+                                        ec.window_length, nc.output_shape, agent.device)
         self.iteration = 0
         self.last_losses = (float("nan"), float("nan"))
         self.last_mean_reward = float("nan")

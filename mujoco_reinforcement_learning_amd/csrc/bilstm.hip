@@ -34,6 +34,7 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "gemm_ops.h"
 #include "reduce_slabs.h"
 #include "timing.h"
 
@@ -384,8 +385,8 @@ int gemm_fwd(ppo_lstm_ctx *x, const GemmProblem *p, int np, int k, int rows, int
   gb.k = k;
   gb.act = act;
   gb.prec = x->prec;
-  return b_kn ? run_rowwise<B_KN, EPI_FWD>(gb, np, rows, max_n, st)
-              : run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+  return b_kn ? gemm_rows_fwd_kn(gb, np, rows, max_n, st)
+              : gemm_rows_fwd_nk(gb, np, rows, max_n, st);
 }
 
 int gemm_dx(ppo_lstm_ctx *x, const GemmProblem *p, int np, int k, int rows, int max_n, int act,
@@ -395,7 +396,7 @@ int gemm_dx(ppo_lstm_ctx *x, const GemmProblem *p, int np, int k, int rows, int 
   gb.k = k;
   gb.act = act;
   gb.prec = x->prec;
-  return run_rowwise<B_KN, EPI_DX>(gb, np, rows, max_n, st);
+  return gemm_rows_dx(gb, np, rows, max_n, st);
 }
 
 int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int max_m, int max_n,
@@ -406,7 +407,7 @@ int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int ma
   gb.splits = kSplits;
   gb.slab_stride = x->total;
   gb.prec = x->prec;
-  return run_partial(gb, np, max_m, max_n, st);
+  return gemm_wgrad_partial(gb, np, max_m, max_n, st);
 }
 
 // LSTM net z forward over xin [b*W][O] (batch-major rows); fills g/c/y/hp of every layer and the

@@ -31,6 +31,7 @@
 #include "fused_policy.h"
 #include "fused_update.h"
 #include "gemm.h"
+#include "gemm_ops.h"
 #include "reduce_slabs.h"
 #include "timing.h"
 
@@ -611,7 +612,7 @@ struct NetDesc {
 static const char *const kClassNames[KC_COUNT] = {
     "gemm_fwd",     "gemm_dgrad", "gemm_wgrad", "update_head", "policy_head", "reduce_slabs",
     "gather_states", "gae",       "adam",       "normalize_rows", "obs", "minibatch_rows",
-    "env_harness", "fused_update", "lstm"};
+    "env_harness", "fused_update", "lstm", "conv"};
 
 thread_local Timing *g_tim = nullptr;
 Timing *g_free_tim = nullptr;
@@ -702,7 +703,7 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
       if (!use[z] || l >= nd.n_hidden) continue;
       const LayerDesc &L = nd.layer[l];
       if (kdim >= 0 && kdim != L.in) {  // shapes differ: flush what we have
-        int rc = run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+        int rc = gemm_rows_fwd_nk(gb, np, rows, max_n, st);
         if (rc) return rc;
         np = 0;
         max_n = 0;
@@ -722,7 +723,7 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
       max_n = std::max(max_n, L.out);
     }
     if (np) {
-      int rc = run_rowwise<B_NK, EPI_FWD>(gb, np, rows, max_n, st);
+      int rc = gemm_rows_fwd_nk(gb, np, rows, max_n, st);
       if (rc) return rc;
     }
   }
@@ -1613,10 +1614,10 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
         ((gb.p[0].m <= 32) != (gb.p[1].m <= 32) || (gb.p[0].n <= 32) != (gb.p[1].n <= 32))) {
       GemmBatch g1 = gb;
       g1.p[0] = gb.p[1];
-      if (int rc = run_partial(gb, 1, gb.p[0].m, gb.p[0].n, st)) return rc;
-      return run_partial(g1, 1, g1.p[0].m, g1.p[0].n, st);
+      if (int rc = gemm_wgrad_partial(gb, 1, gb.p[0].m, gb.p[0].n, st)) return rc;
+      return gemm_wgrad_partial(g1, 1, g1.p[0].m, g1.p[0].n, st);
     }
-    return run_partial(gb, np, max_m, max_n, st);
+    return gemm_wgrad_partial(gb, np, max_m, max_n, st);
   };
   auto input_grad = [&](int layer_from_top) -> int {
     // dH_{l-1} = (dY_l W_l) * act'(H_{l-1}), written over H_{l-1}; l = n_hidden - layer_from_top
@@ -1631,7 +1632,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
       if (l < 1 || l >= nd.n_hidden) continue;  // head handled in the head kernel
       const LayerDesc &L = nd.layer[l];
       if (kdim >= 0 && kdim != L.out) {
-        if (int rc = run_rowwise<B_KN, EPI_DX>(gb, np, b, max_n, st)) return rc;
+        if (int rc = gemm_rows_dx(gb, np, b, max_n, st)) return rc;
         np = 0;
         max_n = 0;
       }
@@ -1650,7 +1651,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
       max_n = std::max(max_n, L.in);
     }
     if (!np) return 0;
-    return run_rowwise<B_KN, EPI_DX>(gb, np, b, max_n, st);
+    return gemm_rows_dx(gb, np, b, max_n, st);
   };
   const int depth = std::max(NA.n_hidden, NC.n_hidden);
   for (int s = 0; s <= depth; ++s) {
@@ -1745,9 +1746,8 @@ extern "C" int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d) 
   return 0;
 }
 
-extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing: null ctx");
-  Timing &t = ctx->tim;
+namespace ppo {
+int timing_enable(Timing &t, int enable, int capacity) {
   if (enable && capacity > t.capacity) {
     for (int i = 0; i < 2 * t.capacity; ++i) (void)hipEventDestroy(t.ev[i]);
     delete[] t.ev;
@@ -1774,7 +1774,6 @@ extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
   return 0;
 }
 
-namespace ppo {
 // Folds pending records into the per-class and per-kernel totals (host sync on their events).
 static int timing_fold(Timing &t) {
   for (int i = 0; i < t.used; ++i) {
@@ -1802,14 +1801,11 @@ static int timing_fold(Timing &t) {
   t.used = 0;
   return 0;
 }
-}  // namespace ppo
 
-extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
-                                   double *flops, double *bytes) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_read: null ctx");
+int timing_read_class(Timing &t, int kclass, double *total_ms, int64_t *launches, double *flops,
+                      double *bytes) {
   if (kclass < 0) return KC_COUNT;
-  PPO_REQUIRE(kclass < KC_COUNT, "ppo_ctx_timing_read: class %d out of range", kclass);
-  Timing &t = ctx->tim;
+  PPO_REQUIRE(kclass < KC_COUNT, "timing read: class %d out of range", kclass);
   if (int rc = timing_fold(t)) return rc;
   if (total_ms) *total_ms = t.ms[kclass];
   if (launches) *launches = t.n[kclass];
@@ -1818,15 +1814,12 @@ extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, i
   return 0;
 }
 
-extern "C" int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name, int *kclass,
-                                     double *total_ms, int64_t *launches, double *flops,
-                                     double *bytes) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_kernel: null ctx");
-  Timing &t = ctx->tim;
+int timing_read_kernel(Timing &t, int index, const char **name, int *kclass, double *total_ms,
+                       int64_t *launches, double *flops, double *bytes) {
   if (int rc = timing_fold(t)) return rc;
   const int count = static_cast<int>(t.per_kernel.size());
   if (index < 0) return count;
-  PPO_REQUIRE(index < count, "ppo_ctx_timing_kernel: index %d out of range [0, %d)", index, count);
+  PPO_REQUIRE(index < count, "timing read: kernel index %d out of range [0, %d)", index, count);
   const KernelTotals &k = t.per_kernel[index];
   if (name) *name = k.name;
   if (kclass) *kclass = k.cls;
@@ -1835,6 +1828,25 @@ extern "C" int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name,
   if (flops) *flops = k.fl;
   if (bytes) *bytes = k.by;
   return 0;
+}
+}  // namespace ppo
+
+extern "C" int ppo_ctx_timing(ppo_ctx *ctx, int enable, int capacity) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing: null ctx");
+  return timing_enable(ctx->tim, enable, capacity);
+}
+
+extern "C" int ppo_ctx_timing_read(ppo_ctx *ctx, int kclass, double *total_ms, int64_t *launches,
+                                   double *flops, double *bytes) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_read: null ctx");
+  return timing_read_class(ctx->tim, kclass, total_ms, launches, flops, bytes);
+}
+
+extern "C" int ppo_ctx_timing_kernel(ppo_ctx *ctx, int index, const char **name, int *kclass,
+                                     double *total_ms, int64_t *launches, double *flops,
+                                     double *bytes) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_timing_kernel: null ctx");
+  return timing_read_kernel(ctx->tim, index, name, kclass, total_ms, launches, flops, bytes);
 }
 
 extern "C" const char *ppo_kernel_class_name(int kclass) {

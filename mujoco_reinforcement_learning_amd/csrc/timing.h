@@ -29,6 +29,7 @@ enum {
   KC_ENV,    // synthetic VecEnv step + Philox normals (bench harness)
   KC_FUSED,  // persistent fused minibatch forward + loss + backward (bf16)
   KC_LSTM,   // BiLSTM cell steps and elementwise glue (bilstm.hip)
+  KC_CONV,   // implicit-GEMM convolutions of the pixel encoder (cnn_engine.hip)
   KC_COUNT
 };
 
@@ -64,6 +65,14 @@ extern Timing *g_free_tim;
 const char *intern_name(const char *fmt, ...);
 
 inline bool tim_active() { return g_tim != nullptr; }
+
+// Shared bodies of the per-context timing entry points (ppo_ctx_timing / ppo_cnn_timing, ...):
+// enable (re)allocates `capacity` event pairs and clears the totals; read folds pending records.
+int timing_enable(Timing &t, int enable, int capacity);
+int timing_read_class(Timing &t, int kclass, double *total_ms, int64_t *launches, double *flops,
+                      double *bytes);
+int timing_read_kernel(Timing &t, int index, const char **name, int *kclass, double *total_ms,
+                       int64_t *launches, double *flops, double *bytes);
 
 struct FreeTimingScope {
   FreeTimingScope() { g_tim = (g_free_tim && g_free_tim->on) ? g_free_tim : nullptr; }

@@ -1,0 +1,294 @@
+"""GPU: the pixel-observation actor-critic (BASELINE.json configs[4]: dm_control cheetah-run,
+84x84x3 frames) against its CPU oracle (oracle/cnn_ref.py).
+
+Parity is unpinned by the reference (it has no pixel / CNN path); the oracle
+restates the engine's declared model with torch-CPU Conv2d / Linear modules.  Bars:
+  * synthetic pixel env: frames, rewards and terminations bit-exact;
+  * init: bit-exact (same modules, same RNG order);
+  * f32 (exact-f32 MFMA convolutions): encoder features, mean, value within rtol 1e-5;
+    minibatch gradients within 2e-5 of each tensor's max; a full PPO iteration with every
+    optimizer step at the north_star parameter bar (tests/parity_util.py stepwise_parity);
+  * bf16: against the oracle with every conv / linear operand rounded to bf16
+    (cnn_ref.use_bf16): outputs within 2e-3 of their scale; gradients within 3x the emulation's
+    own noise floor (the same emulation with f32 vs f64 accumulation), see the test;
+  * the full-size workload (1024 envs, T=128, B=16384, bf16) for one epoch: GAE of the engine's
+    own rollout bit-exact, finite outputs, moving and bit-reproducible parameters.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cnn_ref as C
+from oracle import ppo_ref as R
+from parity_util import (capture_engine_grads, capture_oracle_grads, compare_step_grads,
+                         own_gae, record_oracle_steps, replay_rows, stepwise_parity)
+
+pytestmark = pytest.mark.gpu
+
+FRAME_BYTES = 84 * 84 * 3
+
+
+def _run(n, t=8, b=64, hidden=(64, 64), precision="f32", epochs=2, rng="torch", seed=0, **kw):
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    return make_run(num_envs=n, horizon=t, obs_dim=FRAME_BYTES, act_dim=6, hidden=hidden,
+                    batch_size=b, epochs=epochs, rng=rng, seed=seed, precision=precision,
+                    feature_extractor="CNN", **kw)
+
+
+def _pair(gpu, n, b, hidden=(64, 64), precision="f32", seed=0, **kw):
+    from mujoco_reinforcement_learning_amd.agent import make_agent
+    run = _run(n, b=b, hidden=hidden, precision=precision, seed=seed, **kw)
+    torch.manual_seed(seed)
+    agent = make_agent(run, device=gpu, max_rows=max(n, b))
+    cfg = R.RefConfig(num_envs=n, horizon=run.environment_config.maximum_timesteps, act_dim=6,
+                      actor_hidden=tuple(hidden), critic_hidden=tuple(hidden), batch_size=b,
+                      epochs=run.training_config.epochs_per_iteration)
+    torch.manual_seed(seed)
+    ref = C.RefCNNAgent(cfg)
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref)), "init differs"
+    return run, agent, ref, cfg
+
+
+def _frames(n, seed=3, t=5):
+    g = np.random.default_rng(seed)
+    a = g.standard_normal((n, 6)).astype(np.float32)
+    return torch.from_numpy(C.synthetic_frames(seed, t, n, a)).contiguous()
+
+
+def test_pixel_env_bit_exact(gpu):
+    from mujoco_reinforcement_learning_amd.cnn import synthetic_pixel_step
+    n, t = 37, 6
+    g = torch.Generator().manual_seed(2)
+    base_r = torch.rand(t, n, generator=g) * 2 - 1
+    base_term = torch.rand(t, n, generator=g) < 0.2
+    act = torch.randn(n, 6, generator=g) * 3
+    out = torch.empty(n, FRAME_BYTES, dtype=torch.uint8, device=gpu)
+    synthetic_pixel_step(11, 0, None, out)
+    assert torch.equal(out.cpu().view(n, 84, 84, 3), torch.from_numpy(C.synthetic_frames(11, 0, n)))
+    rew = torch.empty(n, dtype=torch.float64, device=gpu)
+    term = torch.empty(n, dtype=torch.bool, device=gpu)
+    synthetic_pixel_step(11, 4, act.to(gpu), out, base_r.to(gpu), base_term.to(gpu), rew, term)
+    env = C.RefPixelEnv(11, base_r, base_term, 6)
+    env.reset()
+    env.t = 3
+    env.step(act)
+    assert torch.equal(out.cpu().view(n, 84, 84, 3), env.frame)
+    assert torch.equal(rew.cpu(), env.reward)
+    assert torch.equal(term.cpu(), env.terminated)
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_forward_matches_oracle(gpu, precision):
+    n = 48
+    run, agent, ref, cfg = _pair(gpu, n, n, hidden=(256, 256), precision=precision)
+    frames = _frames(n)
+    if precision == "bf16":
+        C.use_bf16(ref)
+    fa = torch.empty(n, 3136, device=gpu)
+    fc = torch.empty(n, 3136, device=gpu)
+    mean = torch.empty(n, 6, device=gpu)
+    value = torch.empty(n, device=gpu)
+    agent.engine.forward(frames.view(n, -1).to(gpu), mean=mean, value=value, feat_actor=fa,
+                         feat_critic=fc)
+    with torch.no_grad():
+        ra, rc = C.features(ref, frames)
+        m_ref, _ = ref.networks["actor"](frames)
+        v_ref = ref.networks["critic"](frames)[:, 0]
+    for name, got, exp in (("actor features", fa, ra), ("critic features", fc, rc),
+                           ("mean", mean, m_ref), ("value", value, v_ref)):
+        got = got.cpu()
+        err = float((got - exp).abs().max()) / (float(exp.abs().max()) + 1e-12)
+        print(f"{precision} {name}: max err {err:.3e} of scale")
+        if precision == "f32":
+            torch.testing.assert_close(got, exp, rtol=1e-5, atol=1e-5 * float(exp.abs().max()),
+                                       msg=name)
+        else:
+            assert err <= 2e-3, (name, err)
+
+
+def test_policy_step_sampling(gpu):
+    n = 40
+    run, agent, ref, cfg = _pair(gpu, n, n)
+    frames = _frames(n, seed=5).view(n, -1).to(gpu)
+    eps = torch.randn(n, 6, generator=torch.Generator().manual_seed(4))
+    action, mean = torch.empty(n, 6, device=gpu), torch.empty(n, 6, device=gpu)
+    logp, value = torch.empty(n, device=gpu), torch.empty(n, device=gpu)
+    agent.engine.policy_step(frames, eps=eps.to(gpu), action=action, logp=logp, value=value,
+                             mean=mean)
+    std = agent.networks["actor"].actor_logstd.detach().exp().cpu()
+    assert torch.equal(action.cpu(), eps * std + mean.cpu())  # fl(fl(eps*std)+mean)
+    lp = torch.distributions.Normal(mean.cpu(), std).log_prob(action.cpu()).sum(1)
+    torch.testing.assert_close(logp.cpu(), lp, rtol=1e-6, atol=1e-5)
+
+
+def _oracle_minibatch(cfg, seed, bf16, dtype, frames, actions, old_logp, adv, vt, rows):
+    """The minibatch loss of ppo.py:109-135 on the oracle nets and its gradient (parameters()
+    order); dtype float64 evaluates the same bf16-rounded operands with f64 accumulation."""
+    torch.manual_seed(seed)
+    ref = C.RefCNNAgent(cfg)
+    if bf16:
+        C.use_bf16(ref)
+    ref.networks.to(dtype)
+    saved = (C._pixels, R._bf)
+    C._pixels = lambda x: (x.float() / 255.0).to(dtype).permute(0, 3, 1, 2)
+    R._bf = lambda x: x.to(torch.bfloat16).to(x.dtype)
+    try:
+        idx = rows.long()
+        _, dist = ref.act(frames[idx], return_dist=True)
+        new_lp = dist.log_prob(actions[idx].to(dtype)).sum(dim=1)
+        v = ref.get_state_value(frames[idx])
+        lc = torch.nn.functional.huber_loss(v, vt[idx][:, None].to(dtype), reduction="mean")
+        ratio = (new_lp - old_logp[idx].to(dtype)).exp()[:, None]
+        a_ = adv[idx][:, None].to(dtype)
+        la = -torch.min(ratio * a_, torch.clamp(ratio, 0.9, 1.1) * a_).mean() \
+            - dist.entropy().mean() * 1e-4
+        ref.networks.zero_grad()
+        (la + lc).backward()
+    finally:
+        C._pixels, R._bf = saved
+    grads = [(n, p.grad.double().flatten()) for n, p in ref.networks.named_parameters()]
+    return grads, float(la), float(lc)
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_minibatch_grad_matches_oracle(gpu, precision):
+    """f32: every gradient within 2e-5 of its tensor's max.  bf16: the engine against the bf16
+    emulation, held to the emulation's own noise floor -- the same bf16-rounded minibatch
+    evaluated with f32 and with f64 accumulation already differs by 1-20 % of a tensor's max
+    here (bf16 rounding flips of intermediates, amplified through 6 layers and the ReLU kinks,
+    measured in the test): the engine must stay within 3x that spread (and 2e-3 absolute)."""
+    rows_total, b = 160, 96
+    run, agent, ref, cfg = _pair(gpu, rows_total, b, hidden=(256, 256), precision=precision, seed=4)
+    g = torch.Generator().manual_seed(10)
+    frames = _frames(rows_total, seed=9)
+    actions = torch.randn(rows_total, 6, generator=g) * 0.5
+    adv = torch.randn(rows_total, generator=g)
+    vt = torch.randn(rows_total, generator=g) * 2
+    with torch.no_grad():
+        m_ref, s_ref = ref.networks["actor"](frames)
+        lp = torch.distributions.Normal(m_ref, s_ref).log_prob(actions).sum(1)
+    old_logp = lp + torch.randn(rows_total, generator=g) * 0.2  # ratios on both sides of the clip
+    rows = torch.randperm(rows_total, generator=g)[:b].to(torch.int32)
+    grad = torch.empty(agent.engine.n_params, device=gpu)
+    loss = torch.empty(2, device=gpu)
+    agent.engine.minibatch_grad(frames.view(rows_total, -1).to(gpu), actions.to(gpu),
+                                old_logp.to(gpu), adv.to(gpu), vt.to(gpu), rows.to(gpu), b, grad,
+                                loss, 0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    bf16 = precision == "bf16"
+    args = (frames, actions, old_logp, adv, vt, rows)
+    ref_g, la, lc = _oracle_minibatch(cfg, 4, bf16, torch.float32, *args)
+    floor_g = _oracle_minibatch(cfg, 4, bf16, torch.float64, *args)[0] if bf16 else None
+    gd = agent.packed(grad).cpu().double()
+    worst, worst_l2, off = 0.0, 0.0, 0
+    for i, (name, r_) in enumerate(ref_g):
+        k = r_.numel()
+        a = gd[off:off + k]
+        scale = float(r_.abs().max()) + 1e-12
+        err = float((a - r_).abs().max()) / scale
+        l2 = float((a - r_).norm() / (r_.norm() + 1e-20))
+        if bf16:
+            f = floor_g[i][1]
+            f_err = float((r_ - f).abs().max()) / scale
+            f_l2 = float((r_ - f).norm() / (f.norm() + 1e-20))
+            bar, bar_l2 = max(3 * f_err, 2e-3), max(3 * f_l2, 2e-3)
+            print(f"bf16 {name}: err {err:.3e} of max, rel L2 {l2:.3e} (emulation f32 vs f64: "
+                  f"{f_err:.3e}, {f_l2:.3e})")
+        else:
+            bar, bar_l2 = 2e-5, 2e-5
+            print(f"f32 {name}: err {err:.3e} of max, rel L2 {l2:.3e}")
+        worst, worst_l2 = max(worst, err), max(worst_l2, l2)
+        assert err <= bar and l2 <= bar_l2, (name, err, l2, bar, bar_l2)
+        off += k
+    print(f"cnn minibatch grad {precision}: worst {worst:.3e} of max, rel L2 {worst_l2:.3e}")
+    lt = 1e-5 if precision == "f32" else 1e-3
+    assert abs(float(loss[1]) - lc) <= lt * (abs(lc) + 1e-2)
+    assert abs(float(loss[0]) - la) <= max(lt, 1e-4) * (abs(la) + 1e-2)
+
+
+def _algo(gpu, run, agent, streams, seed):
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.cnn import SyntheticPixelVecEnvHelper
+    helper = SyntheticPixelVecEnvHelper(streams, run, device=gpu, seed=seed)
+    return PPOEngine(helper, agent, log=lambda m: None)
+
+
+def test_iteration_matches_oracle_f32(gpu):
+    """One full PPO iteration (rollout of 8 steps x 16 envs, GAE, 2 epochs x 2 minibatches)
+    through the drop-in classes against the oracle loop on the same seeds, checked like the
+    Humanoid iteration (test_gpu_configs._iteration_case): rollout frames bit-exact and values
+    within 1e-5, GAE of the engine's rollout bit-exact, the first step's gradient within 1e-5 of
+    each tensor's max, the free-running update within 2*lr*steps and 1e-3 relative L2, and every
+    optimizer step restarted from the oracle's own state at the north_star bar
+    (parity_util.stepwise_parity)."""
+    from mujoco_reinforcement_learning_amd.environments import make_synthetic_streams
+    n, t, b, epochs = 16, 8, 64, 2
+    run, agent, ref, cfg = _pair(gpu, n, b, t=t)
+    streams = make_synthetic_streams(n, t, 1, seed=5, p_terminate=0.1)
+    algo = _algo(gpu, run, agent, streams, seed=7)
+    env = C.RefPixelEnv(7, streams["base_reward"], streams["base_terminated"], 6)
+    p0 = R.flat_params(ref).clone()
+    steps = record_oracle_steps(ref)
+    torch.manual_seed(1234)
+    mem = algo.rollout()
+    algo.calculate_advantages(mem)
+    torch.manual_seed(1234)
+    ref_mem = R.rollout(env, ref)
+    R.calculate_advantages(ref_mem, cfg)
+    assert torch.equal(mem["current_state"].cpu(), ref_mem["current_state"]), "frames differ"
+    for key in ("current_state_value", "next_state_value", "action", "action_log_prob",
+                "reward", "advantage"):
+        torch.testing.assert_close(mem[key].cpu().to(ref_mem[key].dtype), ref_mem[key],
+                                   rtol=1e-5, atol=1e-5, msg=key)
+    adv_own, _ = own_gae(mem, cfg)
+    assert torch.equal(mem["advantage"].cpu(), adv_own), "GAE on the engine's rollout"
+    g_eng, g_ref = capture_engine_grads(algo), capture_oracle_grads(ref)
+    torch.manual_seed(99)
+    algo.train(mem)
+    torch.manual_seed(99)
+    R.train(ref, ref_mem, 0)
+    torch.cuda.synchronize()
+    worst = compare_step_grads(g_eng, g_ref, ref, rel=1e-5, steps=1)
+    p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
+    lr = cfg.learning_rate
+    assert float((p_eng - p_ref).abs().max()) <= 2 * lr * len(g_ref)
+    worst_l2, off = 0.0, 0
+    for name, p in ref.networks.named_parameters():
+        k = p.numel()
+        du_e, du_r = p_eng[off:off + k] - p0[off:off + k], p_ref[off:off + k] - p0[off:off + k]
+        worst_l2 = max(worst_l2, float((du_e - du_r).norm() / (du_r.norm() + 1e-20)))
+        off += k
+    print(f"cnn iteration: first-step grad worst {worst:.3e} of max; free-running update rel L2 "
+          f"{worst_l2:.3e}")
+    assert worst_l2 <= 1e-3, worst_l2
+    rows = replay_rows(99, n, t, b, epochs, cfg.act_dim)
+    assert len(rows) == len(steps) == epochs * (n * t // b)
+    stepwise_parity(algo, agent, ref, cfg, ref_mem, steps, rows, label="cnn")
+
+
+def test_full_size_iteration_properties(gpu):
+    """BASELINE configs[4] at full size (1024 envs, T=128, B=16384, bf16, philox, hipGraphs),
+    one epoch, twice from the same seeds."""
+    from mujoco_reinforcement_learning_amd.agent import make_agent
+    from mujoco_reinforcement_learning_amd.environments import make_synthetic_streams
+    n, t, b = 1024, 128, 16384
+    outs = []
+    for _ in range(2):
+        run = _run(n, t=t, b=b, hidden=(256, 256), precision="bf16", epochs=1, rng="philox",
+                   seed=3)
+        torch.manual_seed(0)
+        agent = make_agent(run, device=gpu)
+        streams = make_synthetic_streams(n, t, 1, seed=2, p_terminate=0.01)
+        algo = _algo(gpu, run, agent, streams, seed=4)
+        p0 = agent.packed_params().clone()
+        for _ in range(2):  # eager warm-up iteration, then the captured graphs
+            algo.iterate(verbose=False)
+        torch.cuda.synchronize()
+        mem = algo.buffer
+        cfg = R.RefConfig(num_envs=n, horizon=t)
+        adv_own, _ = own_gae(mem, cfg)
+        assert torch.equal(mem["advantage"].cpu(), adv_own)
+        p1 = agent.packed_params()
+        assert bool(torch.isfinite(p1).all()) and not torch.equal(p0, p1)
+        assert all(np.isfinite(x) for x in algo.last_losses)
+        outs.append(p1.cpu())
+    assert torch.equal(outs[0], outs[1]), "not bit-reproducible"

@@ -244,9 +244,11 @@ def test_host_rollout_watchdog_measures_stalls_not_total_time(gpu, monkeypatch):
     which the pool can still be closed cleanly."""
     from mujoco_reinforcement_learning_amd._lib import EngineError
     import time
-    monkeypatch.setenv("PPO_HOST_ROLLOUT_STALL_MS", "400")
     algo, helper = _host_algo(gpu, 64, 16, 0.06)
     try:
+        algo.rollout()  # warm-up: the spawned workers' start-up is not a physics step
+        torch.cuda.synchronize()
+        monkeypatch.setenv("PPO_HOST_ROLLOUT_STALL_MS", "400")
         t0 = time.perf_counter()
         algo.rollout()
         torch.cuda.synchronize()
@@ -255,9 +257,13 @@ def test_host_rollout_watchdog_measures_stalls_not_total_time(gpu, monkeypatch):
         assert took > 0.4
         assert bool(torch.isfinite(algo.buffer.values).all())
     finally:
+        monkeypatch.delenv("PPO_HOST_ROLLOUT_STALL_MS")
         helper.close()
     algo, helper = _host_algo(gpu, 64, 4, 1.5)
     try:
+        algo.rollout()  # warm-up with the default limit (4 steps of 1.5 s)
+        torch.cuda.synchronize()
+        monkeypatch.setenv("PPO_HOST_ROLLOUT_STALL_MS", "400")
         with pytest.raises(EngineError, match="no group advanced"):
             algo.rollout()
     finally:
