@@ -30,6 +30,12 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 METRIC = "env-steps/sec (whole node) HalfCheetah-v4 4096 envs at 1/2/4/8 MI355X"
+# separate measurements (not the headline): their own metric strings
+METRICS = {"mlp": METRIC,
+           "lstm": "env-steps/sec main.py BiLSTM actor-critic (O=348, W=5, latent 256), 1024 envs, "
+                   "1x MI355X",
+           "cnn": "env-steps/sec dm_control cheetah-run pixels 84x84x3, 1024 envs, small CNN encoder "
+                  "(Nature-DQN), 1x MI355X"}
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
 PEAK_BF16_MFMA_TFLOPS = 2516.6  # MI355X_MICROARCH.md: bf16 dense (2.5 PF; sparsity excluded)
 PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec
@@ -38,11 +44,13 @@ PEAK_HBM_GBS = 8000.0           # MI355X HBM3E spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--model", choices=("mlp", "lstm"), default="mlp",
+    p.add_argument("--model", choices=("mlp", "lstm", "cnn"), default="mlp",
                    help="mlp: the north_star MLP actor-critic (the headline metric); lstm: the "
                         "reference PPOAgent's BiLSTM actor / critic on main.py's network (O=348, "
-                        "W=5, latent 256, [256,256,128,128], A=17) at N=1024, B=16384 unless "
-                        "overridden -- a separate measurement, not the headline line")
+                        "W=5, latent 256, [256,256,128,128], A=17) at N=1024, B=16384; cnn: "
+                        "BASELINE configs[4], 84x84x3 pixel frames, Nature-DQN encoder + 2x256 "
+                        "heads, A=6, N=1024, B=16384 (unless overridden) -- separate "
+                        "measurements, not the headline line")
     p.add_argument("--window", type=int, default=None)
     p.add_argument("--latent", type=int, default=256)
     p.add_argument("--steps", type=int, default=5)
@@ -88,6 +96,12 @@ def parse():
         args.no_timing = True  # per-kernel times for this leg come from rocprofv3
         args.no_legs = True
         args.cpu_baseline = False
+    if args.model == "cnn":
+        defaults = {"num_envs": 1024, "obs_dim": 84 * 84 * 3, "act_dim": 6, "batch": 16384}
+        for k, v in defaults.items():
+            if getattr(args, k) == p.get_default(k):
+                setattr(args, k, v)
+        args.no_legs = True
     if args.window is None:
         args.window = 1
     return args
@@ -104,7 +118,7 @@ def load_traffic(path):
 
 # gymnasium observation / action sizes of the BASELINE configs (SURVEY.md s8 notation)
 _ENV_NAMES = {(17, 6): "HalfCheetah-v4", (27, 8): "Ant-v4", (376, 17): "Humanoid-v4",
-              (348, 17): "main.py humanoid (O=348)"}
+              (348, 17): "main.py humanoid (O=348)", (84 * 84 * 3, 6): "cheetah-run pixels"}
 
 
 def roofline(name, c, traffic, force_hbm=False):
@@ -118,8 +132,8 @@ def roofline(name, c, traffic, force_hbm=False):
     peak_f = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     t_mfma = c["flops"] / (peak_f * 1e12)
     t_hbm = c["bytes"] / (PEAK_HBM_GBS * 1e9)
-    mfma = (c["class"].startswith("gemm") or c["class"] == "fused_update") and t_mfma >= t_hbm \
-        and not force_hbm
+    mfma = (c["class"].startswith("gemm") or c["class"] in ("fused_update", "conv")) and \
+        t_mfma >= t_hbm and not force_hbm
     if mfma:
         achieved, peak, unit = c["flops"] / launches / avg_s / 1e12, peak_f, "TFLOP/s"
     else:
@@ -210,6 +224,49 @@ def cpu_baseline(args, hidden):
             "seconds_per_iteration": t_iter}
 
 
+def cpu_baseline_cnn(args, hidden):
+    """The pixel oracle (oracle/cnn_ref.py) on the host cores: rollout_steps of the T-step
+    rollout, the full GAE and ONE minibatch of the E x M update, extrapolated to one iteration."""
+    from oracle import cnn_ref as C
+    from oracle import ppo_ref as R
+    threads = cpu_share()
+    torch.set_num_threads(threads)
+    _progress(f"cpu baseline (cnn) on {threads} threads ({cpu_model()})")
+    n, t, b = args.num_envs, args.horizon, args.batch
+    cfg = R.RefConfig(num_envs=n, horizon=t, act_dim=args.act_dim, actor_hidden=hidden,
+                      critic_hidden=hidden, batch_size=b, epochs=1)
+    g = torch.Generator().manual_seed(0)
+    env = C.RefPixelEnv(0, torch.rand(t, n, generator=g) * 2 - 1,
+                        torch.zeros(t, n, dtype=torch.bool), args.act_dim)
+    torch.manual_seed(0)
+    agent = C.RefCNNAgent(cfg)
+    k = min(args.cpu_rollout_steps, 4, t)
+    cfg.horizon = k
+    t0 = time.perf_counter()
+    mem = R.rollout(env, agent)
+    t_roll = (time.perf_counter() - t0) * (t / k)
+    cfg.horizon = t
+    reps = (t + k - 1) // k
+    full = {key: v.repeat(1, reps, *([1] * (v.dim() - 2)))[:, :t].contiguous()
+            for key, v in mem.items()}
+    t0 = time.perf_counter()
+    R.calculate_advantages(full, cfg)
+    t_gae = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    R.train(agent, full, 0, max_minibatches=1)
+    t_mb = time.perf_counter() - t0
+    steps = args.epochs * (n * t // b)
+    t_iter = t_roll + t_gae + t_mb * steps
+    _progress(f"cpu baseline (cnn): rollout {k} steps {t_roll * k / t:.2f} s, minibatch {t_mb:.2f} s")
+    return {"value": n * t / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "torch": torch.__version__,
+            "sample": (f"oracle/cnn_ref.py (torch-CPU Conv2d / Linear restatement; the reference has "
+                       f"no pixel path), {threads} threads: {k} of {t} rollout steps + full GAE + 1 of "
+                       f"{steps} minibatches of {b} at N={n}; extrapolated (rollout {t_roll:.2f}s, "
+                       f"gae {t_gae:.3f}s, minibatch {t_mb:.2f}s)"),
+            "seconds_per_iteration": t_iter}
+
+
 def build(args, precision, env_kind, dev, rank):
     """(run, agent, helper, algo) for one leg of the workload (BASELINE configs[1] shapes)."""
     from mujoco_reinforcement_learning_amd.agent import make_agent
@@ -223,10 +280,15 @@ def build(args, precision, env_kind, dev, rank):
                    window=args.window, hidden=hidden, batch_size=args.batch, epochs=args.epochs,
                    rng=args.rng, seed=rank, precision=precision,
                    rollout_graph=not args.no_graphs, train_graph=not args.no_graphs,
-                   feature_extractor="LSTM" if args.model == "lstm" else "MLP",
+                   feature_extractor={"lstm": "LSTM", "cnn": "CNN"}.get(args.model, "MLP"),
                    latent=args.latent)
     torch.manual_seed(0)  # identical initial parameters on every rank
     agent = make_agent(run, device=dev)
+    if args.model == "cnn":
+        from mujoco_reinforcement_learning_amd.cnn import SyntheticPixelVecEnvHelper
+        streams = make_synthetic_streams(n, t, 1, seed=1000 + rank, device=dev)
+        helper = SyntheticPixelVecEnvHelper(streams, run, device=dev, seed=1000 + rank)
+        return run, agent, helper, PPOEngine(helper, agent, log=lambda m: None)
     streams = make_synthetic_streams(n, t, args.obs_dim, seed=1000 + rank, device=dev)
     if env_kind == "host":
         from mujoco_reinforcement_learning_amd.environments import HostPhysicsVecEnvHelper
@@ -290,6 +352,8 @@ def main():
     # PPO_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the data-parallel path
     if os.environ.get("PPO_BENCH_ONE_DEVICE") == "1":
         local = 0
+        if world > 1:  # the in-launch fold needs its whole grid resident: not with N ranks per GPU
+            os.environ.setdefault("PPO_FUSED_FOLD", "0")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -323,7 +387,7 @@ def main():
         ec.rollout_graph, ec.train_graph = saved
 
     value = world * n * t * args.steps / elapsed
-    line = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+    line = {"metric": METRICS[args.model], "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",
@@ -332,6 +396,8 @@ def main():
                                     f"{args.obs_dim}, act {args.act_dim}, actor+critic "
                                     + (f"BiLSTM(latent {args.latent}, window {args.window}) + "
                                        if args.model == "lstm" else "")
+                                    + ("Nature-DQN CNN encoder (84x84x3 u8 frames -> 3136) + "
+                                       if args.model == "cnn" else "")
                                     + f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
                                     f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
@@ -363,7 +429,8 @@ def main():
             # s8(d)'s t_iter includes the per-step obs H2D and action D2H: the host-pool env
             line["pcie_inclusive_leg"] = leg(args, args.precision, "host", dev)
     if rank == 0 and world == 1 and args.cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, hidden)
+        line["cpu_baseline"] = (cpu_baseline_cnn(args, hidden) if args.model == "cnn"
+                                else cpu_baseline(args, hidden))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if hasattr(helper, "close"):

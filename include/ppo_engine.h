@@ -125,6 +125,18 @@ int ppo_pack_weights(ppo_ctx *ctx, void *stream);
  * a hipGraph replays with fresh noise after the host bumps the counter.  NULL restores plain
  * `offset`.  (No reference counterpart: the reference draws from the host generator.) */
 int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
+
+/* The fused bf16 update's in-launch slab fold (default off; PPO_FUSED_FOLD=1 or enable=1 turns
+ * it on): the partial-gradient slabs are folded -- and on ppo_update_step_staged, Adam, the
+ * weight images and the next minibatch's gather run -- inside the fused kernel behind a bounded,
+ * self-re-arming grid barrier, instead of in a separate reduce / tail launch.  Used only when the
+ * (G, 2) grid is resident (one workgroup per CU).  enable < 0 queries.  Results are bitwise those
+ * of the separate launches (same reduction order).  Off by default because it measured slower:
+ * the fold adds 29 us to the fused launch against an 18 us standalone tail. */
+int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable);
+/* Host check (synchronises): PPO_EHIP if a fold's grid barrier timed out since the last check
+ * (its step's gradients are wrong), with the message in ppo_last_error(). */
+int ppo_ctx_check_device_errors(ppo_ctx *ctx);
 /* GEMM precision of every fc-layer GEMM the ctx launches (rollout forward, update forward,
  * dgrad, wgrad): PPO_PREC_F32 (default; parity with the f32 reference) or PPO_PREC_BF16 (bf16
  * operands on v_mfma_f32_32x32x16_bf16, f32 accumulation, f32 activations / params / Adam in
@@ -190,6 +202,16 @@ int ppo_ctx_fused_active(const ppo_ctx *ctx);
 int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                       const float *old_logp_d, const float *adv_d, const float *vtarget_d,
                       int64_t n_rows, void *stream);
+/* ppo_gae (same arguments and outputs, ppo.py:70-80) and ppo_stage_records over its n*t rows in
+ * ONE pass: each row's record is written as soon as its advantage / value target leave the scan.
+ * Valid when nothing rewrites adv / vtarget between the two (ppo.py:81-88 advantage
+ * normalisation off); adv_d / vtarget_d / records are byte-identical to the two calls. */
+int ppo_gae_stage_records(ppo_ctx *ctx, const float *value_d, const float *next_value_d,
+                          const void *reward_d, int reward_is_f64, const uint8_t *done_d,
+                          const uint8_t *terminated_d, int force_last_done, int n, int t,
+                          double gamma, double lmbda, float *adv_d, float *vtarget_d,
+                          const float *states_d, const float *actions_d, const float *old_logp_d,
+                          void *stream);
 int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b, const int32_t *count_d,
                               float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                               float inv_ba, float *grad_d, float *loss_d, int flags,

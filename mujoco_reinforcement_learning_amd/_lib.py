@@ -124,6 +124,8 @@ _SIGNATURES = {
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
     "ppo_ctx_set_rng_counter": (c_int, [c_void_p, c_void_p]),
+    "ppo_ctx_fused_fold": (c_int, [c_void_p, c_int]),
+    "ppo_ctx_check_device_errors": (c_int, [c_void_p]),
     "ppo_ctx_set_precision": (c_int, [c_void_p, c_int]),
     "ppo_ctx_timing": (c_int, [c_void_p, c_int, c_int]),
     "ppo_ctx_timing_read": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64),
@@ -147,6 +149,9 @@ _SIGNATURES = {
     "ppo_host_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
     "ppo_stage_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_void_p]),
+    "ppo_gae_stage_records": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_int, c_int, c_int, c_double, c_double, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_minibatch_grad_staged": (c_int, [c_void_p, c_void_p, c_int, c_void_p, ctypes.c_float,
                                           ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                           ctypes.c_float, c_void_p, c_void_p, c_int, c_void_p]),

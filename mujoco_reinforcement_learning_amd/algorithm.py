@@ -296,6 +296,18 @@ class PPOEngine:
             buf.reward_work.copy_(buf.reward)
             E.normalize_rows(buf.reward_work, run.ppo_config.advantage_scaler)
             rewards = buf.reward_work
+        eng = getattr(self.agent, "engine", None)
+        buf.records_staged = False
+        if (not run.ppo_config.normalize_advantage and getattr(eng, "fused", False)
+                and hasattr(eng, "gae_stage_records")):
+            # fused bf16 path: the scan also writes the 128 B row records the epochs gather
+            # (byte-identical to gae + stage_records; train() then skips its staging pass)
+            eng.gae_stage_records(buf.values[:t_len], buf.values[1:], rewards, buf.terminated,
+                                  run.ppo_config.gamma, run.ppo_config.lmbda, buf.advantage,
+                                  buf.value_target, buf.states, buf.actions, buf.logp,
+                                  force_last_done=True)
+            buf.records_staged = True
+            return
         E.gae(buf.values[:t_len], buf.values[1:], rewards, buf.terminated, run.ppo_config.gamma,
               run.ppo_config.lmbda, buf.advantage, buf.value_target, force_last_done=True)
         if run.ppo_config.normalize_advantage:
@@ -343,8 +355,9 @@ class PPOEngine:
         self._tg_sched.copy_(sched, non_blocking=True)
 
         staged = eng.fused
-        if staged:
+        if staged and not getattr(buf, "records_staged", False):
             eng.stage_records(buf.states, buf.actions, buf.logp, buf.advantage, buf.value_target)
+        buf.records_staged = False
 
         def rows_of(k):
             e, i = divmod(k, batches)
@@ -358,19 +371,15 @@ class PPOEngine:
                     sched = self._tg_sched[k]
                     nxt = rows_of(k + 1) if k + 1 < steps else None
                     if staged and self.dp.active:
+                        # fused gradient (folded to the flat gradient) -> all-reduce -> ONE tail
+                        # launch: Adam + weight images + the next minibatch's row gather
                         eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
                                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
                                                   weights_current=k > 0, rows_gathered=k > 0)
-                        # the next minibatch's row gather depends on the row indices only: it
-                        # runs on the compute stream while the gradient all-reduce is in flight
-                        work = self.dp.allreduce_grad_async(agent.flat_grad)
-                        if nxt is not None:
-                            eng.gather_staged_rows(nxt)
-                        if work is not None:
-                            work.wait()
+                        self.dp.allreduce_grad(agent.flat_grad)
                         eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
                                       one_minus_beta1=1 - beta1, beta2=beta2,
-                                      one_minus_beta2=1 - beta2, eps=eps)
+                                      one_minus_beta2=1 - beta2, eps=eps, next_rows=nxt)
                         continue
                     if staged:
                         eng.update_step_staged(
@@ -444,8 +453,11 @@ class PPOEngine:
                         scheduler.step()
                 return out
         staged = eng.fused
-        if staged:  # one 128 B record per stored row: the minibatch gathers read one line a row
+        # one 128 B record per stored row: the minibatch gathers read one line a row (staged
+        # already when calculate_advantages ran the fused scan)
+        if staged and not getattr(buf, "records_staged", False):
             eng.stage_records(states, buf.actions, buf.logp, buf.advantage, buf.value_target)
+        buf.records_staged = False
         current = False  # bf16 weight images refreshed by the last optimizer step
         for epoch in range(epochs):
             if self._rng() == "torch":
@@ -545,6 +557,8 @@ class PPOEngine:
         t0 = time.perf_counter()
         memory, loss_buf = self._iterate()
         self._finish_logging(loss_buf)
+        if hasattr(self.agent.engine, "check_device_errors"):
+            self.agent.engine.check_device_errors()  # after the loss readback's synchronisation
         self.last_mean_reward = float(memory.reward.mean())
         run = self.run
         if verbose:

@@ -31,35 +31,6 @@ struct FusedNet {
   int64_t off_w0, off_b0, off_w1, off_b1, off_wh, off_bh;  // flat offsets (b: -1 = none)
 };
 
-struct FusedArgs {
-  FusedNet net[2];             // 0 actor, 1 critic
-  const float *logstd;
-  int64_t off_logstd;
-  // minibatch staged by fused_prep_kernel (rows >= count are zero)
-  __bf16 *xb;                  // (b, 32) bf16 states
-  float *srow;                 // (b, 16) f32 actions[A], old_logp, adv, vtarget
-  // prep sources: time-major storage arrays gathered through rows
-  const float *states, *actions, *old_logp, *adv, *vtarget;
-  const int32_t *rows;
-  const int32_t *rows_n;       // device row count (exact data parallel), nullable -> b
-  // staged records (fused_records_launch): when set, the prep gather copies one 128 B record
-  // per row instead of reading the five storage arrays
-  const uint4 *rec;
-  int64_t n_rec;
-  bool pack_w;                 // prep also refreshes the bf16 weight images from the masters
-  int b, din, act_dim, act, hidden;
-  float omv, clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
-  float *slabs;                // (G, slab_stride) partial gradients in the flat layout
-  int64_t slab_stride;
-  float *loss_part;            // (G, 2): actor / critic loss-term sums per workgroup
-  int G;                       // workgroups per net
-  uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
-};
-
-// Gather the minibatch (bf16 states + row scalars) and, with q.pack_w, refresh the bf16 weight
-// images.
-int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
-
 // One 128 B record per stored row: bf16 state[32] (columns >= din zero) | f32 actions[A],
 // old_logp, adv, vtarget, zeros -- the per-row image the prep gather copies.
 constexpr int kRecordBytes = 2 * kFusedKX + 4 * kFusedSP;
@@ -67,6 +38,22 @@ static_assert(kRecordBytes == 128, "one record per 128 B line");
 int fused_records_launch(uint4 *rec, const float *states, const float *actions,
                          const float *old_logp, const float *adv, const float *vtarget,
                          int64_t n_rows, int din, int act_dim, const TimRec &trec, hipStream_t st);
+
+// GAE + value target (gae_pipe.h) with the records staged in the same pass (gae_records_kernel):
+// rows t*n + env of the (t_len, n) time-major arrays.
+struct GaeRecordArgs {
+  const float *value, *next_value;
+  const void *reward;  // f32 or f64 (reward_f64)
+  const uint8_t *done, *term;
+  int force_last, n, t_len;
+  float gamma_f, lg_f;
+  float *adv, *vtarget;
+  const float *states, *actions, *old_logp;
+  uint4 *rec;
+  int din, act_dim;
+};
+int gae_records_launch(const GaeRecordArgs &g, bool reward_f64, const TimRec &rec,
+                       hipStream_t st);
 
 // Adam over the flat parameters of both nets (adam_elem) that also writes the updated values
 // into the fused kernels' bf16 weight images, so the next minibatch needs no weight refresh.
@@ -99,9 +86,53 @@ struct TailArgs {
   bool reduce;  // false: no slab reduction, Adam on the gradient already in a.g (data parallel)
 };
 int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st);
+
+struct FusedArgs {
+  FusedNet net[2];             // 0 actor, 1 critic
+  const float *logstd;
+  int64_t off_logstd;
+  // minibatch staged by fused_prep_kernel (rows >= count are zero)
+  __bf16 *xb;                  // (b, 32) bf16 states
+  float *srow;                 // (b, 16) f32 actions[A], old_logp, adv, vtarget
+  // prep sources: time-major storage arrays gathered through rows
+  const float *states, *actions, *old_logp, *adv, *vtarget;
+  const int32_t *rows;
+  const int32_t *rows_n;       // device row count (exact data parallel), nullable -> b
+  // staged records (fused_records_launch): when set, the prep gather copies one 128 B record
+  // per row instead of reading the five storage arrays
+  const uint4 *rec;
+  int64_t n_rec;
+  bool pack_w;                 // prep also refreshes the bf16 weight images from the masters
+  int b, din, act_dim, act, hidden;
+  float omv, clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
+  float *slabs;                // (G, slab_stride) partial gradients in the flat layout
+  int64_t slab_stride;
+  float *loss_part;            // (G, 2): actor / critic loss-term sums per workgroup
+  int G;                       // workgroups per net
+  uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
+  // In-launch fold of the partial-gradient slabs (fold > 0; every workgroup must be resident,
+  // fused_fold_ok): after its slab is written, each workgroup publishes it (agent-scope
+  // release), arrives on *sync (zeroed before the launch) and waits -- bounded -- for all the
+  // others; then the workgroups fold the slabs in red's fixed order, workgroup w taking the
+  // parameter blocks w, w + 2G, ... (the step_tail_kernel arithmetic, so results are bitwise
+  // those of the separate launch).  fold = 1: the flat gradient (data parallel: the all-reduce
+  // follows); fold = 2: also Adam + the bf16 weight images and the next minibatch's gather
+  // (tail).  A barrier that times out sets *fold_err and skips the fold.
+  int fold;
+  uint32_t *sync;
+  int *fold_err;
+  ReduceArgs red;
+  TailArgs tail;
+};
+// Gather the minibatch (bf16 states + row scalars) and, with q.pack_w, refresh the bf16 weight
+// images.
+int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.
 int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).
 bool fused_width_ok(int hidden);
+// True when a (G, 2) grid of the fused kernel for this activation / action width is fully
+// resident on the device (one workgroup per CU), i.e. the in-launch fold can wait on it.
+bool fused_fold_ok(int act, int act_dim, int G);
 
 }  // namespace ppo

@@ -667,7 +667,7 @@ static int run_rowwise(const GemmBatch &gb, int nprob, int rows, int max_n, hipS
   return launch_gemm<1, 1, 1, 4, A_MK, BMODE, EPI>(gb, nprob, rows, max_n, st);
 }
 
-static int run_partial(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+[[maybe_unused]] static int run_partial(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
   if (max_m <= 32) return launch_gemm<1, 1, 1, 4, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
   if (max_n <= 32) return launch_gemm<1, 1, 4, 1, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);
   return launch_big<2, 2, 2, 2, A_KM, B_KN, EPI_PARTIAL>(gb, nprob, max_m, max_n, st);

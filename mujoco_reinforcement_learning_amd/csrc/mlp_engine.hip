@@ -662,6 +662,10 @@ struct ppo_ctx {
   int64_t frec_cap, frec_rows;
   uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
   int fstamp_on, fstamp_g;
+  uint32_t *fsync;              // the in-launch fold's arrival counter (zeroed per launch)
+  int *ffold_err;               // set by a fold whose grid barrier timed out
+  int fold_on;                  // ppo_ctx_fused_fold (default: PPO_FUSED_FOLD, 0)
+  int fold_g;                   // G the residency check last passed for (0: none)
   ppo::Timing tim;
 };
 
@@ -875,6 +879,26 @@ static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, floa
   return r;
 }
 
+// The in-launch fold (FusedArgs::fold) is used when enabled and the (G, 2) grid is resident
+// (one workgroup per CU); the residency check runs once per G.
+static bool fold_usable(ppo_ctx *ctx, int G) {
+  if (!ctx->fold_on || !ctx->fsync) return false;
+  if (ctx->fold_g == G) return true;
+  if (!fused_fold_ok(ctx->cfg.activation, ctx->cfg.act_dim, G)) return false;
+  ctx->fold_g = G;
+  return true;
+}
+
+static int fold_prepare(ppo_ctx *ctx, FusedArgs &q, int mode, const ReduceArgs &r,
+                        hipStream_t st) {
+  q.fold = mode;
+  q.sync = ctx->fsync;
+  q.fold_err = ctx->ffold_err;
+  q.red = r;
+  (void)st;  // the barrier re-arms itself (fused_fold): nothing to reset per launch
+  return 0;
+}
+
 static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                                 const float *old_logp_d, const float *adv_d,
                                 const float *vtarget_d, const int32_t *rows_d, int b,
@@ -890,8 +914,13 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
     p.b = gathered ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
   }
-  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
+  if (fold_usable(ctx, q.G)) {  // the slab fold inside the fused launch: no reduce launch
+    FusedArgs f = q;
+    if (int rc = fold_prepare(ctx, f, 1, r, st)) return rc;
+    return fused_forward_backward(ctx, f, st);
+  }
+  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const int64_t P = ctx->total_params;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(q.G) * P,
                   4.0 * (static_cast<double>(q.G) + 1) * P},
@@ -1088,6 +1117,18 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       ctx->fslabs = reinterpret_cast<float *>(c);
       c += static_cast<int64_t>(kFusedMaxWG) * off * 4;
       ctx->floss = reinterpret_cast<float *>(c);
+      c += kFusedMaxWG * 2 * 4;
+      ctx->fsync = reinterpret_cast<uint32_t *>(c);  // [0] arrivals, [32] generation
+      ctx->ffold_err = reinterpret_cast<int *>(c + 64);
+      e = hipMemset(c, 0, 256);
+      if (e != hipSuccess) {
+        (void)hipFree(arena);
+        (void)hipFree(fa);
+        delete ctx;
+        set_error("ppo_ctx_create: hipMemset failed: %s", hipGetErrorString(e));
+        return PPO_EHIP;
+      }
+      ctx->fold_on = env_knob("PPO_FUSED_FOLD", 0);
     }
   }
   *out = ctx;
@@ -1220,6 +1261,29 @@ extern "C" int ppo_ctx_fused_active(const ppo_ctx *ctx) {
   return (ctx && fused_active(ctx)) ? 1 : 0;
 }
 
+// The ctx's record buffer grown to n_rows (outside a graph capture: the first call per size).
+static int ensure_records(ppo_ctx *ctx, int64_t n_rows, hipStream_t st, const char *who) {
+  if (n_rows > ctx->frec_cap) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    PPO_REQUIRE(hipStreamIsCapturing(st, &cap) == hipSuccess &&
+                    cap == hipStreamCaptureStatusNone,
+                "%s: first call for %lld rows inside a graph capture", who,
+                static_cast<long long>(n_rows));
+    (void)hipStreamSynchronize(st);
+    if (ctx->frec) (void)hipFree(ctx->frec);
+    ctx->frec = nullptr;
+    ctx->frec_cap = 0;
+    void *p = nullptr;
+    const hipError_t e = hipMalloc(&p, static_cast<size_t>(n_rows) * kRecordBytes);
+    PPO_REQUIRE(e == hipSuccess, "%s: hipMalloc(%lld records): %s", who,
+                static_cast<long long>(n_rows), hipGetErrorString(e));
+    ctx->frec = static_cast<uint4 *>(p);
+    ctx->frec_cap = n_rows;
+  }
+  ctx->frec_rows = n_rows;
+  return 0;
+}
+
 extern "C" int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                                  const float *old_logp_d, const float *adv_d,
                                  const float *vtarget_d, int64_t n_rows, void *stream) {
@@ -1229,30 +1293,67 @@ extern "C" int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const floa
   PPO_REQUIRE(states_d && actions_d && old_logp_d && adv_d && vtarget_d && n_rows > 0,
               "ppo_stage_records: null buffer or n_rows <= 0");
   hipStream_t st = as_stream(stream);
-  if (n_rows > ctx->frec_cap) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    PPO_REQUIRE(hipStreamIsCapturing(st, &cap) == hipSuccess &&
-                    cap == hipStreamCaptureStatusNone,
-                "ppo_stage_records: first call for %lld rows inside a graph capture",
-                static_cast<long long>(n_rows));
-    (void)hipStreamSynchronize(st);
-    if (ctx->frec) (void)hipFree(ctx->frec);
-    ctx->frec = nullptr;
-    ctx->frec_cap = 0;
-    void *p = nullptr;
-    const hipError_t e = hipMalloc(&p, static_cast<size_t>(n_rows) * kRecordBytes);
-    PPO_REQUIRE(e == hipSuccess, "ppo_stage_records: hipMalloc(%lld records): %s",
-                static_cast<long long>(n_rows), hipGetErrorString(e));
-    ctx->frec = static_cast<uint4 *>(p);
-    ctx->frec_cap = n_rows;
-  }
-  ctx->frec_rows = n_rows;
+  if (int rc = ensure_records(ctx, n_rows, st, "ppo_stage_records")) return rc;
   TimingScope timing_scope(ctx);
   const int din = ctx->cfg.obs_dim * ctx->cfg.window, A = ctx->cfg.act_dim;
   const TimRec rec{KC_GATHER, "fused_records_kernel", 0.0,
                    static_cast<double>(n_rows) * (4.0 * (din + A + 3) + kRecordBytes)};
   return fused_records_launch(ctx->frec, states_d, actions_d, old_logp_d, adv_d, vtarget_d,
                               n_rows, din, A, rec, st);
+}
+
+extern "C" int ppo_gae_stage_records(ppo_ctx *ctx, const float *value_d,
+                                     const float *next_value_d, const void *reward_d,
+                                     int reward_is_f64, const uint8_t *done_d,
+                                     const uint8_t *terminated_d, int force_last_done, int n,
+                                     int t, double gamma, double lmbda, float *adv_d,
+                                     float *vtarget_d, const float *states_d,
+                                     const float *actions_d, const float *old_logp_d,
+                                     void *stream) {
+  if (int rc = check_ctx(ctx)) return rc;
+  PPO_REQUIRE(fused_active(ctx), "ppo_gae_stage_records: needs the fused bf16 path "
+                                 "(ppo_ctx_fused_active)");
+  PPO_REQUIRE(value_d && next_value_d && reward_d && terminated_d && adv_d && vtarget_d &&
+                  states_d && actions_d && old_logp_d,
+              "ppo_gae_stage_records: null buffer");
+  PPO_REQUIRE(n > 0 && t > 0, "ppo_gae_stage_records: bad shape n=%d t=%d", n, t);
+  const int64_t n_rows = static_cast<int64_t>(n) * t;
+  if (t > 16 * 16) {  // beyond the pipelined scan: the two passes
+    if (int rc = ppo_gae(value_d, next_value_d, reward_d, reward_is_f64, done_d, terminated_d,
+                         force_last_done, n, t, gamma, lmbda, adv_d, vtarget_d, stream))
+      return rc;
+    return ppo_stage_records(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, n_rows,
+                             stream);
+  }
+  hipStream_t st = as_stream(stream);
+  if (int rc = ensure_records(ctx, n_rows, st, "ppo_gae_stage_records")) return rc;
+  TimingScope timing_scope(ctx);
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window, A = ctx->cfg.act_dim;
+  GaeRecordArgs g{};
+  g.value = value_d;
+  g.next_value = next_value_d;
+  g.reward = reward_d;
+  g.done = done_d;
+  g.term = terminated_d;
+  g.force_last = force_last_done;
+  g.n = n;
+  g.t_len = t;
+  g.gamma_f = static_cast<float>(gamma);
+  g.lg_f = static_cast<float>(lmbda * gamma);
+  g.adv = adv_d;
+  g.vtarget = vtarget_d;
+  g.states = states_d;
+  g.actions = actions_d;
+  g.old_logp = old_logp_d;
+  g.rec = ctx->frec;
+  g.din = din;
+  g.act_dim = A;
+  // algorithmic bytes: the GAE's (V, V', reward, terminated [+ done] in; adv, vtarget out) plus
+  // the record pass's (state, actions, old_logp in; the 128 B record out)
+  const double per_row = 4 + 4 + (reward_is_f64 ? 8 : 4) + 1 + (done_d ? 1 : 0) + 4 + 4 +
+                         4.0 * (din + A + 1) + kRecordBytes;
+  const TimRec rec{KC_GAE, "gae_records_kernel", 0.0, static_cast<double>(n_rows) * per_row};
+  return gae_records_launch(g, reward_is_f64 != 0, rec, st);
 }
 
 extern "C" int ppo_minibatch_grad_staged(ppo_ctx *ctx, const int32_t *rows_d, int b,
@@ -1366,7 +1467,6 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
     p.b = gathered ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
   }
-  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   // tail: slab reduction + Adam + weight images, and the next minibatch's row gather
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
   TailArgs t{};
@@ -1379,6 +1479,12 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.srow = ctx->fsrow;
   t.b = next_b;
   t.reduce = true;
+  if (fold_usable(ctx, q.G)) {  // the whole optimizer step in ONE launch
+    if (int rc = fold_prepare(ctx, q, 2, r, st)) return rc;
+    q.tail = t;
+    return fused_forward_backward(ctx, q, st);
+  }
+  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
                    4.0 * (q.G + 1.0) * P + 24.0 * P + 2.0 * 2.0 * H * (q.din + 2.0 * H) +
@@ -1737,6 +1843,29 @@ extern "C" int ppo_ctx_set_precision(ppo_ctx *ctx, int prec) {
   PPO_REQUIRE(prec == PPO_PREC_F32 || prec == PPO_PREC_BF16,
               "ppo_ctx_set_precision: unknown precision %d", prec);
   ctx->prec = prec;
+  return 0;
+}
+
+extern "C" int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_fold: null ctx");
+  if (enable < 0) return ctx->fold_on && ctx->fsync ? 1 : 0;
+  ctx->fold_on = enable != 0;
+  return 0;
+}
+
+extern "C" int ppo_ctx_check_device_errors(ppo_ctx *ctx) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_check_device_errors: null ctx");
+  if (!ctx->ffold_err) return 0;
+  int err = 0;
+  PPO_HIP_TRY(hipMemcpy(&err, ctx->ffold_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    // a timed-out barrier leaves the arrival count mid-generation: re-arm it with the flag
+    PPO_HIP_TRY(hipMemset(ctx->fsync, 0, 256));
+    set_error("fused update: the in-launch slab fold's grid barrier timed out (workgroups not "
+              "co-resident); the gradients of that step are wrong -- disable it with "
+              "ppo_ctx_fused_fold(ctx, 0) / PPO_FUSED_FOLD=0 (the default)");
+    return PPO_EHIP;
+  }
   return 0;
 }
 

@@ -45,113 +45,155 @@ constexpr int kRedGroups = 32;
 constexpr int kRedChunks = 16;
 constexpr int kRedThreads = kRedGroups * kRedChunks;
 constexpr int kRedParams = 4 * kRedGroups;  // parameters per block
-__device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t block) {
-  __shared__ float4 part[kRedChunks][kRedGroups];
-  __shared__ float lred[2][kRedThreads];
-  __shared__ ReduceSeg sseg[kMaxSegs];
+// LDS scratch of one block reduction: part [kRedChunks][kRedGroups], lred [2][kRedThreads],
+// sseg [kMaxSegs] (the standalone kernels declare it; the fused kernel's in-launch fold lends
+// its own LDS, free once the compute phase is over).
+struct RedScratch {
+  float4 *part;
+  float *lred;
+  ReduceSeg *sseg;
+};
+constexpr int kRedScratchBytes =
+    (kRedChunks * kRedGroups) * 16 + 2 * kRedThreads * 4 + kMaxSegs * static_cast<int>(sizeof(ReduceSeg));
+__device__ __forceinline__ RedScratch red_scratch(char *lds) {
+  return RedScratch{reinterpret_cast<float4 *>(lds),
+                    reinterpret_cast<float *>(lds + kRedChunks * kRedGroups * 16),
+                    reinterpret_cast<ReduceSeg *>(lds + kRedChunks * kRedGroups * 16 + 2 * kRedThreads * 4)};
+}
+
+// The segment holding parameter i: the last one with dst <= i (dst ascending).
+__device__ __forceinline__ int seg_find(const ReduceSeg *sseg, int nseg, int64_t i) {
+  int s = 0, hi = nseg - 1;
+  while (s < hi) {
+    const int mid = (s + hi + 1) >> 1;
+    if (sseg[mid].dst <= i) s = mid;
+    else hi = mid - 1;
+  }
+  return s;
+}
+
+// Chunk `chunk`'s share (splits [k0, k1)) of parameters i..i+3: the one summation order every
+// slab reduction uses.  The aligned path keeps two interleaved partial sums (even / odd split)
+// so 8 independent loads stay in flight per thread; the association is fixed, so the result is
+// deterministic run to run.  The unaligned path (tail of a tensor, logstd partials, 1-wide
+// biases) takes 8 strided partial sums per element; padding stays zero.
+__device__ __forceinline__ float4 slab_item_sum(const ReduceArgs &q, const ReduceSeg *sseg,
+                                                int64_t i, int chunk) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i >= q.total) return acc;
+  const ReduceSeg &g = sseg[seg_find(sseg, q.nseg, i)];
+  const int64_t off = i - g.dst;
+  const int k0 = (g.nsplit * chunk) / kRedChunks, k1 = (g.nsplit * (chunk + 1)) / kRedChunks;
+  if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
+    const float *src = g.src + off;
+    float4 acc1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = k0;
+#pragma unroll 4
+    for (; k + 1 < k1; k += 2) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+      const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+      acc1.x += u.x;
+      acc1.y += u.y;
+      acc1.z += u.z;
+      acc1.w += u.w;
+    }
+    if (k < k1) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    acc = make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
+  } else if (off >= 0) {
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (off + e >= g.len) continue;
+      const float *src = g.src + off + e;
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int k = k0;
+      for (; k + 7 < k1; k += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += src[static_cast<int64_t>(k + j) * g.stride];
+      }
+      for (; k < k1; ++k) s[0] += src[static_cast<int64_t>(k) * g.stride];
+      a4[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    }
+    acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
+  }
+  return acc;
+}
+
+// The chunks of one float4 group combined in chunk order (part[c * stride + grp]).
+__device__ __forceinline__ float4 chunk_combine(const float4 *part, int stride, int grp) {
+  float4 out = part[grp];
+#pragma unroll
+  for (int c = 1; c < kRedChunks; ++c) {
+    const float4 b = part[c * stride + grp];
+    out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
+  }
+  return out;
+}
+
+// The minibatch loss scalars from the per-split partials (fixed-shape tree over kRedThreads
+// threads; every thread of the block must call it).
+__device__ __forceinline__ void reduce_loss_block(const ReduceArgs &q, float *lred_flat) {
+  float (*lred)[kRedThreads] = reinterpret_cast<float (*)[kRedThreads]>(lred_flat);
+  const int tid = threadIdx.x;
+  float la = 0.f, lc = 0.f;
+  for (int k = tid; k < q.loss_splits; k += kRedThreads) {
+    la += q.loss_part[2 * k];
+    lc += q.loss_part[2 * k + 1];
+  }
+  lred[0][tid] = la;
+  lred[1][tid] = lc;
+  __syncthreads();
+  for (int w = kRedThreads / 2; w > 0; w >>= 1) {
+    if (tid < w) {
+      lred[0][tid] += lred[0][tid + w];
+      lred[1][tid] += lred[1][tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    float h = 0.f;
+    if (q.logstd) {
+      for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
+      h = h / static_cast<float>(q.act_dim);
+    }
+    q.loss_out[0] = -(lred[0][0] * q.inv_b) - h * q.ent_coef;
+    q.loss_out[1] = lred[1][0] * q.inv_b;
+  }
+}
+
+__device__ __forceinline__ float4 reduce_slab_block_s(const ReduceArgs &q, int64_t block,
+                                                      RedScratch sc) {
   const int tid = threadIdx.x, grp = tid % kRedGroups, chunk = tid / kRedGroups;
   const int64_t i = block * kRedParams + 4 * grp;
   // The segment table, staged once per block: a per-lane lookup straight from the kernel
   // arguments compiled to a chain of dependent loads (one round trip per probe and per field).
-  if (tid < q.nseg) sseg[tid] = q.seg[tid];
+  if (tid < q.nseg) sc.sseg[tid] = q.seg[tid];
   __syncthreads();
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < q.total) {
-    int s = 0, hi = q.nseg - 1;  // the last segment with dst <= i (dst ascending)
-    while (s < hi) {
-      const int mid = (s + hi + 1) >> 1;
-      if (sseg[mid].dst <= i) s = mid;
-      else hi = mid - 1;
-    }
-    const ReduceSeg &g = sseg[s];
-    const int64_t off = i - g.dst;
-    const int k0 = (g.nsplit * chunk) / kRedChunks, k1 = (g.nsplit * (chunk + 1)) / kRedChunks;
-    // Two interleaved partial sums (even / odd split) keep 8 independent loads in flight per
-    // thread; the association is fixed, so the result is still deterministic run to run.
-    if (off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
-        reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
-      const float *src = g.src + off;
-      float4 acc1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      int k = k0;
-#pragma unroll 4
-      for (; k + 1 < k1; k += 2) {
-        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
-        const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-        acc1.x += u.x;
-        acc1.y += u.y;
-        acc1.z += u.z;
-        acc1.w += u.w;
-      }
-      if (k < k1) {
-        const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-      }
-      acc = make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
-    } else if (off >= 0) {  // tail of a tensor / unaligned source (logstd partials, 1-wide
-                            // biases); padding stays zero.  8 strided partial sums per element.
-      float a4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (off + e >= g.len) continue;
-        const float *src = g.src + off + e;
-        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int k = k0;
-        for (; k + 7 < k1; k += 8) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += src[static_cast<int64_t>(k + j) * g.stride];
-        }
-        for (; k < k1; ++k) s[0] += src[static_cast<int64_t>(k) * g.stride];
-        a4[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-      }
-      acc = make_float4(a4[0], a4[1], a4[2], a4[3]);
-    }
-  }
-  part[chunk][grp] = acc;
+  sc.part[chunk * kRedGroups + grp] = slab_item_sum(q, sc.sseg, i, chunk);
   __syncthreads();
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
   if (chunk == 0 && i < q.total) {
-    out = part[0][grp];
-#pragma unroll
-    for (int c = 1; c < kRedChunks; ++c) {
-      const float4 b = part[c][grp];
-      out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
-    }
+    out = chunk_combine(sc.part, kRedGroups, grp);
     *reinterpret_cast<float4 *>(q.grad + i) = out;
   }
-  if (block == 0 && q.loss_out) {
-    float la = 0.f, lc = 0.f;
-    for (int k = tid; k < q.loss_splits; k += kRedThreads) {
-      la += q.loss_part[2 * k];
-      lc += q.loss_part[2 * k + 1];
-    }
-    lred[0][tid] = la;
-    lred[1][tid] = lc;
-    __syncthreads();
-    for (int w = kRedThreads / 2; w > 0; w >>= 1) {
-      if (tid < w) {
-        lred[0][tid] += lred[0][tid + w];
-        lred[1][tid] += lred[1][tid + w];
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      float h = 0.f;
-      if (q.logstd) {
-        for (int a = 0; a < q.act_dim; ++a) h += kEntropyConst + logf(expf(q.logstd[a]));
-        h = h / static_cast<float>(q.act_dim);
-      }
-      q.loss_out[0] = -(lred[0][0] * q.inv_b) - h * q.ent_coef;
-      q.loss_out[1] = lred[1][0] * q.inv_b;
-    }
-  }
+  if (block == 0 && q.loss_out) reduce_loss_block(q, sc.lred);
   return out;
+}
+
+__device__ __forceinline__ float4 reduce_slab_block(const ReduceArgs &q, int64_t block) {
+  __shared__ __attribute__((aligned(16))) char scratch[kRedScratchBytes];
+  return reduce_slab_block_s(q, block, red_scratch(scratch));
 }
 
 }  // namespace ppo

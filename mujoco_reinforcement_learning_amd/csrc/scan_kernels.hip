@@ -12,6 +12,7 @@
 
 #include "adam_elem.h"
 #include "common.h"
+#include "gae_pipe.h"
 #include "timing.h"
 
 namespace ppo {
@@ -182,14 +183,7 @@ __global__ __launch_bounds__(256) void gae_lds_kernel(const float *__restrict__ 
   }
 }
 
-// Pipelined variant (the default for T <= 16*KMAX): a block of EB*16 threads owns EB envs and
-// walks the horizon backwards in chunks of TC = 16 time rows, thread (tt, c) holding slot k =
-// time row T-1-(16k+tt) of env c.  Every load of every slot is issued up front (chunk 0 first, so
-// chunk 0 lands first chip-wide); then per chunk: delta and the f64 discount go to LDS, ONE
-// barrier, the EB chain lanes run the chunk's 16 dependent steps while every thread stores the
-// previous chunk's adv / vtarget (the chain that produced them finished before the barrier).  The
-// chain starts when the first chunk has landed instead of after the whole tile, and the stores
-// drain under the chain.  Same operations as gae_kernel: bit-identical.
+// Pipelined variant (the default for T <= 16*KMAX): gae_pipe.h's body with no extra outputs.
 template <typename RT, int EB, int KMAX>
 __global__ __launch_bounds__(EB * 16) void gae_pipe_kernel(const float *__restrict__ value,
                                                            const float *__restrict__ next_value,
@@ -200,71 +194,9 @@ __global__ __launch_bounds__(EB * 16) void gae_pipe_kernel(const float *__restri
                                                            float gamma_f, float lg_f,
                                                            float *__restrict__ adv,
                                                            float *__restrict__ vtarget) {
-  constexpr int TC = 16;
-  __shared__ RT s_d[2][TC][EB];     // delta
-  __shared__ RT s_q[2][TC][EB];     // (RT) disc
-  __shared__ float s_o[2][TC][EB];  // f32 advantage
-  const int tid = threadIdx.x, c = tid % EB, tt = tid / EB;
-  const int env = blockIdx.x * EB + c;
-  float lv[KMAX], lvn[KMAX];
-  RT lr[KMAX];
-  uint8_t ltm[KMAX], ldn[KMAX];
-  // unconditional loads from clamped (valid) addresses: no branches or register merges between
-  // them, so every load of every slot is in flight before the first use
-  const int envc = env < n ? env : n - 1;
-  const uint8_t *const dsrc = done ? done : term;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    const int t = t_len - 1 - (TC * k + tt);
-    const int64_t idx = static_cast<int64_t>(t >= 0 ? t : 0) * n + envc;
-    lv[k] = value[idx];
-    lvn[k] = next_value[idx];
-    lr[k] = reward[idx];
-    ltm[k] = term[idx];
-    ldn[k] = dsrc[idx];
-  }
-  RT prev = 0;
-  // a fixed KMAX chunks (no data-dependent control flow, so no load is sunk into a branch);
-  // rows t < 0 (T < 16 KMAX) carry delta = disc = 0 and come after t = 0 in the chain
-#pragma unroll
-  for (int k = 0; k <= KMAX; ++k) {
-    const int buf = k & 1;
-    if (k < KMAX) {
-      const int t = t_len - 1 - (TC * k + tt);
-      const float g_nt = gamma_f * (ltm[k] ? 0.f : 1.f);
-      const float gv = g_nt * lvn[k];
-      const RT delta = (lr[k] + static_cast<RT>(gv)) - static_cast<RT>(lv[k]);
-      const bool is_done = ldn[k] != 0 || (force_last && t == t_len - 1);
-      const RT q = static_cast<RT>(lg_f * (is_done ? 0.f : 1.f));
-      const bool ok = t >= 0 && env < n;
-      s_d[buf][tt][c] = ok ? delta : static_cast<RT>(0);
-      s_q[buf][tt][c] = ok ? q : static_cast<RT>(0);
-    }
-    __syncthreads();
-    if (k < KMAX && tid < EB) {  // the chain: rows of this chunk in descending time
-      RT d[TC], qq[TC];
-#pragma unroll
-      for (int j = 0; j < TC; ++j) {
-        d[j] = s_d[buf][j][tid];
-        qq[j] = s_q[buf][j][tid];
-      }
-#pragma unroll
-      for (int j = 0; j < TC; ++j) {
-        prev = d[j] + prev * qq[j];
-        s_o[buf][j][tid] = static_cast<float>(prev);
-      }
-    }
-    if (k > 0) {  // chunk k-1: its chain ran before this iteration's barrier
-      const int kp = k - 1;
-      const int t = t_len - 1 - (TC * kp + tt);
-      if (t >= 0 && env < n) {
-        const int64_t idx = static_cast<int64_t>(t) * n + env;
-        const float a = s_o[buf ^ 1][tt][c];
-        adv[idx] = a;
-        vtarget[idx] = a + lv[kp];  // value_target = advantage + state_value (f32)
-      }
-    }
-  }
+  GaeNoEmit em;
+  gae_pipe_body<RT, EB, KMAX>(value, next_value, reward, done, term, force_last, n, t_len, gamma_f,
+                              lg_f, adv, vtarget, em);
 }
 
 // ============================================================================================

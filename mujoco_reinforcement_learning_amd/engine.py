@@ -208,6 +208,18 @@ class Engine:
         check(self.lib.ppo_ctx_set_rng_counter(self._ctx, ptr(counter)))
         self._rng_counter = counter  # keep the buffer alive while the ctx may read it
 
+    def fused_fold(self, enable: Optional[bool] = None) -> bool:
+        """The fused update's in-launch slab fold (ppo_ctx_fused_fold): set it with enable,
+        return whether it is on."""
+        if enable is not None:
+            check(self.lib.ppo_ctx_fused_fold(self._ctx, int(bool(enable))))
+        return bool(self.lib.ppo_ctx_fused_fold(self._ctx, -1))
+
+    def check_device_errors(self) -> None:
+        """Raise EngineError if a device-side failure was flagged since the last check (the
+        fold's grid barrier timing out).  Synchronises the host."""
+        check(self.lib.ppo_ctx_check_device_errors(self._ctx))
+
     # ---- measurement ---------------------------------------------------------------------
     def timing(self, enable: bool, capacity: int = 65536) -> None:
         """Record a HIP event pair around every kernel this context launches (live roofline)."""
@@ -293,6 +305,24 @@ class Engine:
                                          ptr(adv), ptr(vtarget), int(n_rows),
                                          _stream(self.device)))
 
+    def gae_stage_records(self, value, next_value, reward, terminated, gamma: float, lmbda: float,
+                          adv, vtarget, states, actions, old_logp, done=None,
+                          force_last_done: bool = True) -> None:
+        """gae(...) and stage_records(states, actions, old_logp, adv, vtarget) in one pass
+        (ppo_gae_stage_records); only valid when adv / vtarget are not normalised in between."""
+        t, n = value.shape[0], value.shape[1]
+        _gae_check(value, next_value, reward, terminated, adv, vtarget, done)
+        for name, x, width in (("states", states, self.obs_dim * self.window),
+                               ("actions", actions, self.act_dim), ("old_logp", old_logp, 1)):
+            _need(x, name, torch.float32, None, self.device)
+            if x.numel() < t * n * width:  # states may carry the extra slot T
+                raise RuntimeError(f"{name}: {x.numel()} elements for {t * n} rows x {width}")
+        check(self.lib.ppo_gae_stage_records(
+            self._ctx, ptr(value), ptr(next_value), ptr(reward), int(reward.dtype == torch.float64),
+            ptr(done), ptr(terminated), int(force_last_done), n, t, float(gamma), float(lmbda),
+            ptr(adv), ptr(vtarget), ptr(states), ptr(actions), ptr(old_logp),
+            _stream(self.device)))
+
     def minibatch_grad_staged(self, rows, b: int, grad, loss, clip_lo: float, clip_hi: float,
                               entropy_coef: float, inv_b: float, inv_ba: float,
                               count: Optional[torch.Tensor] = None,
@@ -376,10 +406,7 @@ class Engine:
 # ==============================================================================================
 # Context-free kernels
 # ==============================================================================================
-def gae(value, next_value, reward, terminated, gamma: float, lmbda: float, adv, vtarget,
-        done=None, force_last_done: bool = True) -> None:
-    """A7/A8 on time-major (T, N) arrays (torchrl GAE semantics, f64 carry)."""
-    lib = _lib.load()
+def _gae_check(value, next_value, reward, terminated, adv, vtarget, done) -> None:
     t, n = value.shape[0], value.shape[1]
     dev = value.device
     _need(value, "value", torch.float32, (t, n))
@@ -394,6 +421,15 @@ def gae(value, next_value, reward, terminated, gamma: float, lmbda: float, adv, 
         _need(done, "done", None, (t, n), dev)
     _need(adv, "adv", torch.float32, (t, n), dev)
     _need(vtarget, "vtarget", torch.float32, (t, n), dev)
+
+
+def gae(value, next_value, reward, terminated, gamma: float, lmbda: float, adv, vtarget,
+        done=None, force_last_done: bool = True) -> None:
+    """A7/A8 on time-major (T, N) arrays (torchrl GAE semantics, f64 carry)."""
+    lib = _lib.load()
+    t, n = value.shape[0], value.shape[1]
+    dev = value.device
+    _gae_check(value, next_value, reward, terminated, adv, vtarget, done)
     check(lib.ppo_gae(ptr(value), ptr(next_value), ptr(reward), int(reward.dtype == torch.float64),
                       ptr(done), ptr(terminated), int(force_last_done), n, t, float(gamma),
                       float(lmbda), ptr(adv), ptr(vtarget), _stream(dev)))

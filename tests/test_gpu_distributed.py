@@ -113,7 +113,8 @@ def _local_worker(rank, world, port, q):
     torch.cuda.synchronize()
     kernels = sorted(agent.engine.timing_kernels())
     agent.engine.timing(False)
-    q.put((rank, agent.packed_params().cpu(), kernels, algo.last_losses))
+    q.put((rank, agent.packed_params().cpu(), (kernels, agent.engine.fused_fold()),
+           algo.last_losses))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -138,8 +139,10 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu):
     # replicas bit-identical (same all-reduced gradient, same Adam), and they moved
     assert torch.equal(got[0][0], got[1][0])
     assert all(abs(x) < 1e6 for x in got[0][2])
-    kernels = got[0][1]
+    kernels, fold = got[0][1]
+    # the data-parallel optimizer step: the fused kernel (slabs folded to the flat gradient in
+    # the same launch, or by reduce_slabs_kernel without the in-launch fold), the all-reduce,
+    # then ONE tail launch: Adam + weight images + the next minibatch's gather
     assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
-    assert "adam_pack_kernel" in kernels, kernels           # Adam + weight images
-    assert "fused_prep_kernel" in kernels, kernels          # next gather, under the all-reduce
-    assert "reduce_slabs_kernel" in kernels, kernels         # grad folded before the all-reduce
+    assert "step_tail_kernel" in kernels, kernels
+    assert ("reduce_slabs_kernel" in kernels) == (not fold), (fold, kernels)

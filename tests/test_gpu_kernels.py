@@ -523,6 +523,59 @@ def test_fused_kernels_bitwise_deterministic(gpu):
         assert torch.equal(gr, grads[0]), int((gr != grads[0]).sum())
 
 
+@pytest.mark.parametrize("n,t,f64_reward,with_done", [(512, 16, True, False),
+                                                      (100, 37, False, True),
+                                                      (96, 200, True, True),
+                                                      (40, 300, True, False)])
+def test_gae_stage_records_matches_two_pass(gpu, n, t, f64_reward, with_done):
+    """ppo_gae_stage_records (the GAE scan with the record pass fused in) == ppo_gae followed by
+    ppo_stage_records, byte for byte: adv / vtarget compared directly, the records through
+    ppo_minibatch_grad_staged over minibatches covering every row (a record that differed in any
+    field would move the gradient).  Ragged N (not a multiple of the 16-env block), T not a
+    multiple of the 16-row chunk, the 16-chunk variant (T = 200) and the two-pass fallback
+    (T > 256); terminations mid-trajectory."""
+    from mujoco_reinforcement_learning_amd import engine as E
+    b = 2048
+    run, eng, ref, cfg = _agents(gpu, 13, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    assert e.fused
+    g = torch.Generator().manual_seed(5)
+    values = torch.randn(t + 1, n, generator=g).to(gpu)
+    rdt = torch.float64 if f64_reward else torch.float32
+    reward = torch.randn(t, n, generator=g, dtype=rdt).to(gpu)
+    term = (torch.rand(t, n, generator=g) < 0.03).to(gpu)
+    done = (term.cpu() | (torch.rand(t, n, generator=g) < 0.02)).to(gpu) if with_done else None
+    states = torch.randn(t + 1, n, 17, generator=g).to(gpu)
+    actions = torch.randn(t, n, 6, generator=g).to(gpu)
+    old_lp = torch.randn(t, n, generator=g).to(gpu) - 5
+    adv0, vt0 = torch.empty(t, n, device=gpu), torch.empty(t, n, device=gpu)
+    adv1, vt1 = torch.full((t, n), float("nan"), device=gpu), torch.full((t, n), float("nan"), device=gpu)
+    E.gae(values[:t], values[1:], reward, term, 0.99, 0.95, adv0, vt0, done=done)
+    e.pack_weights()
+    args = (0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    perm = torch.randperm(n * t, generator=g).to(torch.int32).to(gpu)
+    chunks = [perm[i:i + b] for i in range(0, n * t, b)]
+
+    def grads():
+        out = []
+        for rows in chunks:
+            gr, lo = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+            e.minibatch_grad_staged(rows, rows.numel(), gr, lo, *args)
+            out.append(torch.cat([gr, lo]))
+        return out
+
+    e.stage_records(states, actions, old_lp, adv0, vt0)
+    ref_grads = grads()
+    e.gae_stage_records(values[:t], values[1:], reward, term, 0.99, 0.95, adv1, vt1, states,
+                        actions, old_lp, done=done)
+    got = grads()
+    torch.cuda.synchronize()
+    assert torch.equal(adv0, adv1) and torch.equal(vt0, vt1)
+    for a, c in zip(ref_grads, got):
+        assert torch.equal(a, c), int((a != c).sum())
+
+
 @pytest.mark.parametrize("with_count", [False, True])
 def test_staged_records_and_adam_pack_match_unstaged(gpu, with_count):
     """ppo_stage_records + ppo_minibatch_grad_staged give the gradient and losses of

@@ -11,6 +11,10 @@
 #   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
 #   phases    fused-update phase stamps (tools/fused_phases.py)
 #   micro     tools/micro_fused.py timing of the fused update kernel alone
+#   fold      the bench line with PPO_FUSED_FOLD=1 (in-launch slab fold) -> bench_${TAG}_fold.json
+#   cnn       bench.py --model cnn (pixel cheetah-run) -> bench_${TAG}_cnn.json
+#   cnntrace  rocprofv3 --kernel-trace --stats over the CNN bench
+#   dp2       2-rank data-parallel rehearsal on the one GPU (gloo) -> bench_${TAG}_dp2.json
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
@@ -83,6 +87,25 @@ for S in $STEPS; do
         -- python3 bench.py --model lstm --steps 1 --warmup 1 $LSTM_ARGS > gpurun_out/rp_${TAG}_lstm.json \
         2> gpurun_out/rp_${TAG}_lstm.log || fail lstmtrace gpurun_out/rp_${TAG}_lstm.log
       head -12 $(find gpurun_out/rp_${TAG}_lstm -name "*kernel_stats.csv") ;;
+    fold)
+      PPO_FUSED_FOLD=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs > gpurun_out/bench_${TAG}_fold.json \
+        2> gpurun_out/bench_${TAG}_fold.err || fail fold gpurun_out/bench_${TAG}_fold.err
+      cat gpurun_out/bench_${TAG}_fold.json ;;
+    cnn)
+      timeout -k 10 600 python bench.py --model cnn $CNN_ARGS > gpurun_out/bench_${TAG}_cnn.json \
+        2> gpurun_out/bench_${TAG}_cnn.err || fail cnn gpurun_out/bench_${TAG}_cnn.err
+      cat gpurun_out/bench_${TAG}_cnn.json ;;
+    cnntrace)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_${TAG}_cnn -o cnn --output-format csv \
+        -- python3 bench.py --model cnn --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/rp_${TAG}_cnn.json \
+        2> gpurun_out/rp_${TAG}_cnn.log || fail cnntrace gpurun_out/rp_${TAG}_cnn.log
+      head -16 $(find gpurun_out/rp_${TAG}_cnn -name "*kernel_stats.csv") ;;
+    dp2)
+      PPO_BENCH_BACKEND=gloo PPO_BENCH_ONE_DEVICE=1 timeout -k 10 600 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+        --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_${TAG}_dp2.json \
+        2> gpurun_out/bench_${TAG}_dp2.err || fail dp2 gpurun_out/bench_${TAG}_dp2.err
+      cat gpurun_out/bench_${TAG}_dp2.json ;;
     micro)
       timeout -k 10 200 python tools/micro_fused.py 20 > gpurun_out/micro_${TAG}.txt 2>&1 || fail micro gpurun_out/micro_${TAG}.txt
       cat gpurun_out/micro_${TAG}.txt ;;
