@@ -405,7 +405,10 @@ def main():
                        "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
                                else f"host pool ({args.env_workers} worker processes, page-locked "
                                     "device-mapped shared memory, ppo_host_rollout)"),
-                       "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)"}}
+                       "parallelism": (f"dp{world} (env-sharded, RCCL grad all-reduce)"
+                                       if os.environ.get("PPO_DP_REHEARSE") != "1" or world > 1
+                                       else "dp1 rehearsal (the data-parallel step sequence, "
+                                            "no peer: PPO_DP_REHEARSE=1)")}}
     if kernels:
         traffic = load_traffic(args.traffic)
         name, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])

@@ -215,7 +215,8 @@ __device__ __forceinline__ int rs16_feature(int lane) {
 
 __device__ __forceinline__ int reg_feature(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
-// acc[t] += W[32w + r][:] . img[32t + r][:] over k = 0..H-1 for row tiles t = 0, 1.  A operand
+// acc[t] += W[32w + r][:] . img[32t + r][:] over k = 0..H-1 for row tiles t < NTILE (2: the
+// update kernel's 64-row chunks; 1: the rollout step's 32-row workgroups).  A operand
 // = the L2-resident bf16 weight image in FRAGMENT-MAJOR order (w_frag below: the 64 lanes' 16-B
 // fragments of one (k-step, wave) are one contiguous 1 KB block, so a ring load is 8 full cache
 // lines instead of 32 partial row pieces), B operand = 16-B row reads of the LDS activation image.
@@ -244,9 +245,9 @@ __device__ __forceinline__ void wring_prime(const __bf16 *wfrag, bf16x8 (&ring)[
 #pragma unroll
   for (int s = 0; s < PD; ++s) ring[s] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * s);
 }
-template <int H>
+template <int H, int NTILE>
 __device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, int r, int h,
-                                         bf16x8 (&ring)[PD + 1], f32x16 (&acc)[2]) {
+                                         bf16x8 (&ring)[PD + 1], f32x16 (&acc)[NTILE]) {
   constexpr int KS = H / 16;
   static_assert(KS % (PD + 1) == 0, "ring period must divide the k-steps");
   const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
@@ -262,7 +263,7 @@ __device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, i
       ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * (s + PD));
       const char *p = rowp + 16 * ((2 * s + h) ^ swz);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
+      for (int t = 0; t < NTILE; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
     }
   }
   // ... and the last period peeled: only its first k-step still prefetches (step KS-1), so no
@@ -276,7 +277,7 @@ __device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, i
       ring[(u + PD) % (PD + 1)] = *reinterpret_cast<const bf16x8 *>(wfrag + static_cast<int64_t>(16 * H) * (s + PD));
     const char *p = rowp + 16 * ((2 * s + h) ^ swz);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
+    for (int t = 0; t < NTILE; ++t) acc[t] = mfma(af, lds_b128(p + t * 32 * (2 * H)), acc[t]);
   }
   mfma_drain(acc);
 }

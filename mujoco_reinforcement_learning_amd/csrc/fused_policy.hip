@@ -3,10 +3,11 @@
 // 53-58, 61-92), actor and critic forward (network_block_creator.py:74-86, linear/actor.py:
 // 25-30, critic.py:22-25), Normal sampling and log-prob (ppo_agent.py:27-43, ppo.py:22-26).
 //
-// grid = (ceil(N / 64), nets): blockIdx.y is the net (0 actor, 1 critic), one workgroup = 64
-// envs of one net, 8 waves, wave w owning hidden features 32w..32w+31 -- the same LDS images,
-// weight ring and MFMA maps as the fused update kernel (fused_common.h), so a rollout step and
-// the update's forward compute identical bf16-operand products.  The head width is compile-time
+// grid = (ceil(N / RP), nets): blockIdx.y is the net (0 actor, 1 critic), one workgroup = RP = 32
+// envs of one net (256 workgroups at N = 4096: every CU busy), 8 waves, wave w owning hidden
+// features 32w..32w+31 -- the same LDS images, weight ring and MFMA maps as the fused update
+// kernel (fused_common.h) on one 32-row tile instead of two, so a rollout step and the update's
+// forward compute identical bf16-operand products.  The head width is compile-time
 // (actor: act_dim padded to 2/4/6/8 with zero head rows; critic: 1).
 //
 // Window length 1 (every MLP config): the pushed window is the new observation itself, so both
@@ -17,26 +18,29 @@
 
 #include "fused_common.h"
 #include "fused_policy.h"
+#include "row_stats.h"
 
 namespace ppo {
 
 using namespace fu;
 
 constexpr int kPolicyXsPitch = 33;  // f64 observation staging pitch (doubles)
+constexpr int RP = 32;              // envs per workgroup (one 32-row MFMA tile)
+constexpr int NTP = RP / 32;        // row tiles per workgroup
 
 template <int H>
 struct PolicyLds {
   static constexpr int PITCH = 2 * H;
-  static constexpr int X = 0;                                   // bf16 [64][32]
-  static constexpr int A1 = X + R * 64;                         // bf16 [64][H]
-  static constexpr int A2 = A1 + R * PITCH;                     // bf16 [64][H]
-  static constexpr int WH = A2 + R * PITCH;                     // bf16 head image [16][H + 8]
+  static constexpr int X = 0;                                   // bf16 [RP][32]
+  static constexpr int A1 = X + RP * 64;                        // bf16 [RP][H]
+  static constexpr int A2 = A1 + RP * PITCH;                    // bf16 [RP][H]
+  static constexpr int WH = A2 + RP * PITCH;                    // bf16 head image [16][H + 8]
   static constexpr int BIAS = WH + HeadImg<H>::BYTES;           // f32 b0[H], b1[H]
   static constexpr int HS = BIAS + 2 * H * 4;                   // f32 head bias[8], logstd[8]
-  static constexpr int XD = HS + 16 * 4;                        // f64 [64][33] raw observations
-  static constexpr int ST = XD + R * kPolicyXsPitch * 8;        // f64 [64][16][2] slice mean, std
-  static constexpr int EPS = ST + R * 16 * 2 * 8;               // f32 [64][8] sampling noise
-  static constexpr int SMAP = EPS + R * 8 * 4;                  // int [32] slice of feature f (-1: none)
+  static constexpr int XD = HS + 16 * 4;                        // f64 [RP][33] raw observations
+  static constexpr int ST = XD + RP * kPolicyXsPitch * 8;       // f64 [RP][16][2] slice mean, std
+  static constexpr int EPS = ST + RP * 16 * 2 * 8;              // f32 [RP][8] sampling noise
+  static constexpr int SMAP = EPS + RP * 8 * 4;                 // int [32] slice of feature f (-1: none)
   static constexpr int TOTAL = SMAP + kFusedKX * 4;
   static_assert(TOTAL <= 163840, "LDS budget");
 };
@@ -65,10 +69,10 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int row0 = blockIdx.x * R;
+  const int row0 = blockIdx.x * RP;
   const int A = q.act_dim;
   const int O = q.obs_dim;
-  const int nrow = min(R, q.n - row0);
+  const int nrow = min(RP, q.n - row0);
   // the window / state writer: the actor's workgroups, or the critic's on a value-only call
   const bool writer = ACTOR || !q.do_actor;
 
@@ -94,7 +98,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     eraw = gptr(q.eps ? q.eps : fb)[q.eps ? eidx_c : 0];
   }
   const double *const xsrc = q.obs_d ? q.obs_d : q.window_d;  // W = 1: the window is the obs
-  constexpr int XE = R * kFusedKX / NT;                          // 4 elements per thread
+  constexpr int XE = RP * kFusedKX / NT;                         // 2 elements per thread
   double xv[XE];
 #pragma unroll
   for (int k = 0; k < XE; ++k) {
@@ -132,7 +136,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   bias[tid] = (wu < NW / 2 ? N.b0 != nullptr : N.b1 != nullptr) ? braw : 0.f;
   if (tid < 16)
     hs[tid] = (tid < 8 ? (tid < nh_real && N.bh != nullptr) : (ACTOR && tid - 8 < A)) ? hraw : 0.f;
-  if constexpr (ACTOR) eps_s[tid] = q.eps ? ((ea < A && erow < nrow) ? eraw : 0.f) : epsv;
+  if (ACTOR && tid < RP * 8) eps_s[tid] = q.eps ? ((ea < A && erow < nrow) ? eraw : 0.f) : epsv;
   if (tid < kFusedKX) {  // feature -> slice map (the edges are uniform: scalar loads)
     int sl_of = -1;
     for (int sl = 0; sl < q.tab.count; ++sl)
@@ -149,36 +153,18 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   }
   __syncthreads();
   PSTAMP(2);
-  // ---- per-(row, slice) mean and std: wave 0, lane = row, the A1 kernels' f64 loops (same
-  //      order, bit-identical) ----
-  if (q.normalize && tid < R) {
+  // ---- per-(row, slice) mean and std: wave 0, lane = row, row_stats.h (the layered A1
+  //      kernel's arithmetic, bit-identical) ----
+  if (q.normalize && tid < RP) {
     double x[kFusedKX];  // the row in registers: the slice loops below are unrolled over f
 #pragma unroll
     for (int f = 0; f < kFusedKX; ++f) x[f] = xd[tid * kPolicyXsPitch + f];
     for (int sl = 0; sl < q.tab.count; ++sl) {
       const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
-      const int cnt = hi - lo;
-      if (cnt <= 0) continue;
-      // The sums add +0.0 for features outside [lo, hi): exact, since each sum starts at +0.0
-      // and so is never -0.0 (x + +0.0 == x for every other x).  The select sits on the operand,
-      // off the dependent chain, and there are no branches (uniform branches per feature cost
-      // more than the extra adds: measured).
-      double sum = 0.0;
-#pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) sum += (f >= lo && f < hi) ? x[f] : 0.0;
-      const double mean = sum / cnt;
-      double csum = 0.0;
-#pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) csum += (f >= lo && f < hi) ? x[f] - mean : 0.0;
-      const double cmean = csum / cnt;
-      double ss = 0.0;
-#pragma unroll
-      for (int f = 0; f < kFusedKX; ++f) {
-        const double d = (x[f] - mean) - cmean;
-        ss += (f >= lo && f < hi) ? d * d : 0.0;
-      }
-      double sd = sqrt(ss / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
-      if (sd == 0.0) sd = 1.0;
+      if (hi - lo <= 0) continue;
+      // row_stats.h: the layered A1 kernel's exact arithmetic (pairwise trees, depth 5)
+      const SliceStats ss = slice_stats32(x, lo, hi);
+      const double mean = ss.mean, sd = ss.sd;
       st[(tid * 16 + sl) * 2] = mean;
       st[(tid * 16 + sl) * 2 + 1] = sd;
     }
@@ -188,8 +174,9 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   // ---- standardised states: thread -> (row, feature pair); bf16 X image and the f32 state
   //      (writer workgroups) ----
 #pragma unroll
-  for (int k = 0; k < R * 16 / NT; ++k) {
+  for (int k = 0; k < (RP * 16 + NT - 1) / NT; ++k) {
     const int idx = tid + NT * k, xr = idx >> 4, c2 = (idx & 15) * 2;
+    if (RP * 16 % NT != 0 && idx >= RP * 16) break;
     float y[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -210,16 +197,16 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   bf16x8 ring[PD + 1];
   wring_prime<H>(w_frag_base<H>(N.w1b, w, lane), ring);
   {
-    f32x16 acc[2];
+    f32x16 acc[NTP];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NTP; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 af = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NTP; ++t)
         acc[t] = mfma(af, lds_b128(ximg + x_off(32 * t + r, 2 * s + h)), acc[t]);
     }
     mfma_drain(acc);
@@ -228,7 +215,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       const int f0 = 32 * w + 8 * g + 4 * h;
       const float4 bv = *reinterpret_cast<const float4 *>(bias + f0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < NTP; ++t) {
         const float y0 = act_forward(acc[t][4 * g] + bv.x, ACT);
         const float y1 = act_forward(acc[t][4 * g + 1] + bv.y, ACT);
         const float y2 = act_forward(acc[t][4 * g + 2] + bv.z, ACT);
@@ -243,9 +230,9 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 
   // ---- L1: a2 = act(W1 a1 + b1) -> A2 image (bf16: the head's operand) ----
   {
-    f32x16 a2[2];
+    f32x16 a2[NTP];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NTP; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
@@ -255,7 +242,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       const int f0 = 32 * w + 8 * g + 4 * h;
       const float4 bv = *reinterpret_cast<const float4 *>(bias + H + f0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NTP; ++t)
         *reinterpret_cast<uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h) =
             make_uint2(pack2(act_forward(a2[t][4 * g] + bv.x, ACT), act_forward(a2[t][4 * g + 1] + bv.y, ACT)),
                        pack2(act_forward(a2[t][4 * g + 2] + bv.z, ACT), act_forward(a2[t][4 * g + 3] + bv.w, ACT)));
@@ -266,16 +253,20 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
 
   // ---- heads: z = a2 . W_h^T on the 16x16x32 MFMA (the update kernel's bf16 products); waves w
   //      and w + 4 form the same 16-row tile and split its rows: lane -> head n = lane & 15, rows
-  //      16 (w & 3) + 4 (lane >> 4) + 2 (w >> 2) + {0, 1} ----
+  //      16 (w & 3) + 4 (lane >> 4) + 2 (w >> 2) + {0, 1}; RP / 16 tiles, so waves with
+  //      (w & 3) >= RP / 16 only take part in the exchange barrier ----
   {
     const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
+    const bool head_wave = tile < RP / 16;
     // K split between the wave pair (the update kernel's head order): half 0 sums k-steps
     // 0..H/64-1, half 1 the rest; partners swap their kept rows through the free A1 region
     f32x4 zacc = {0.f, 0.f, 0.f, 0.f};
+    if (head_wave) {
 #pragma unroll
-    for (int s = half * (H / 64); s < (half + 1) * (H / 64); ++s)
-      zacc = mfma16(lds_b128(a2img + img_off(16 * tile + n, 4 * s + qg, L::PITCH)),
-                    lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
+      for (int s = half * (H / 64); s < (half + 1) * (H / 64); ++s)
+        zacc = mfma16(lds_b128(a2img + img_off(16 * tile + n, 4 * s + qg, L::PITCH)),
+                      lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg)), zacc);
+    }
     asm volatile("s_nop 15" : "+v"(zacc));
     float *const xch = reinterpret_cast<float *>(a1img);  // [8 waves][64 lanes][2]
     *reinterpret_cast<float2 *>(xch + 2 * (w * 64 + lane)) =
@@ -283,7 +274,8 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     __syncthreads();
     const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
     const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
-    if constexpr (ACTOR) {
+    if (!head_wave) {
+    } else if constexpr (ACTOR) {
       const bool act_lane = n < A;
       const float sd = act_lane ? expf(hs[8 + n]) : 1.f;
       const float lsd = act_lane ? logf(sd) : 0.f;
@@ -345,7 +337,7 @@ int policy_fused_launch(const PolicyFusedArgs &q, const TimRec &rec, hipStream_t
   PPO_REQUIRE(q.window == 1 && q.obs_dim <= kFusedKX, "fused policy: needs W = 1, O <= %d",
               kFusedKX);
   PPO_REQUIRE(q.do_actor || q.do_critic, "fused policy: nothing requested");
-  const dim3 grid(ceil_div(q.n, R), (q.do_actor && q.do_critic) ? 2 : 1);
+  const dim3 grid(ceil_div(q.n, RP), (q.do_actor && q.do_critic) ? 2 : 1);
   auto go = [&](auto kernel) { launch_k(rec, kernel, grid, dim3(NT), 0, st, q); };
   const int na = q.act_dim <= 2 ? 2 : q.act_dim <= 4 ? 4 : q.act_dim <= 6 ? 6 : 8;
   if (q.stamps) {  // diagnostic build: ReLU, padded head width 6 (HalfCheetah) only

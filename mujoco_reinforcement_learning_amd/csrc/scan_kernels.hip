@@ -13,6 +13,7 @@
 #include "adam_elem.h"
 #include "common.h"
 #include "gae_pipe.h"
+#include "row_stats.h"
 #include "timing.h"
 
 namespace ppo {
@@ -259,7 +260,9 @@ struct SliceTable {
 };
 
 // One thread per (env, window slot): standardise each feature slice in f64 (mean, unbiased std,
-// std==0 -> 1), cast to f32, write permuted (N, W, O).  running_gym_sequential_vectorized.py:61-92.
+// std==0 -> 1; row_stats.h, the fused rollout step's exact arithmetic), cast to f32, write
+// permuted (N, W, O).  running_gym_sequential_vectorized.py:61-92.  O <= 32 (wider rows take
+// obs_normalize_wide_kernel).
 __global__ void obs_normalize_kernel(const double *__restrict__ window, float *__restrict__ state,
                                      int n, int o, int w, SliceTable tab, int normalize) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // (env, slot)
@@ -272,25 +275,16 @@ __global__ void obs_normalize_kernel(const double *__restrict__ window, float *_
     for (int f = 0; f < o; ++f) dst[f] = static_cast<float>(src[static_cast<int64_t>(f) * w]);
     return;
   }
+  double x[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) x[f] = f < o ? src[static_cast<int64_t>(f < o ? f : 0) * w] : 0.0;
   for (int s = 0; s < tab.count; ++s) {
     const int lo = tab.edge[s], hi = tab.edge[s + 1];
-    const int cnt = hi - lo;
-    if (cnt <= 0) continue;
-    double sum = 0.0;
-    for (int f = lo; f < hi; ++f) sum += src[static_cast<int64_t>(f) * w];
-    const double mean = sum / cnt;
-    double csum = 0.0;
-    for (int f = lo; f < hi; ++f) csum += src[static_cast<int64_t>(f) * w] - mean;
-    const double cmean = csum / cnt;
-    double ss = 0.0;
-    for (int f = lo; f < hi; ++f) {
-      const double d = (src[static_cast<int64_t>(f) * w] - mean) - cmean;
-      ss += d * d;
-    }
-    double sd = sqrt(ss / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
-    if (sd == 0.0) sd = 1.0;
-    for (int f = lo; f < hi; ++f)
-      dst[f] = static_cast<float>((src[static_cast<int64_t>(f) * w] - mean) / sd);
+    if (hi - lo <= 0) continue;
+    const SliceStats st = slice_stats32(x, lo, hi);
+#pragma unroll
+    for (int f = 0; f < 32; ++f)
+      if (f >= lo && f < hi) dst[f] = static_cast<float>((x[f] - st.mean) / st.sd);
   }
 }
 
@@ -740,7 +734,7 @@ extern "C" int ppo_obs_normalize(const double *window_d, float *state_d, int n, 
   }
   const int64_t total = static_cast<int64_t>(n) * w;
   FreeTimingScope timing_scope;
-  if (o > 32)
+  if (o > 32)  // obs_normalize_kernel holds a row in 32 registers
     launch_k(TimRec{KC_OBS, "obs_normalize_wide_kernel", 0.0, 12.0 * total * o},
              obs_normalize_wide_kernel, dim3(ceil_div(total * 64, 256)), dim3(256), 0,
              as_stream(stream), window_d, state_d, n, o, w, tab, normalize);

@@ -43,10 +43,15 @@ class DataParallel:
             self.rank = torch.distributed.get_rank(process_group)
         else:
             self.world, self.rank = 1, 0
+        # PPO_DP_REHEARSE=1: one rank runs the data-parallel step sequence (eager launches, the
+        # gradient folded to HBM, the separate Adam / gather tail) with a no-op exchange -- the
+        # DP kernel cost measured without a second process contending for the GPU
+        import os
+        self.rehearse = self.world == 1 and os.environ.get("PPO_DP_REHEARSE") == "1"
 
     @property
     def active(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.rehearse
 
     def allreduce_grad(self, flat_grad: torch.Tensor) -> None:
         """SUM of the flat gradient over ranks, in place, ordered on the current stream."""

@@ -15,6 +15,8 @@
 #   cnn       bench.py --model cnn (pixel cheetah-run) -> bench_${TAG}_cnn.json
 #   cnntrace  rocprofv3 --kernel-trace --stats over the CNN bench
 #   dp2       2-rank data-parallel rehearsal on the one GPU (gloo) -> bench_${TAG}_dp2.json
+#   hum       Humanoid configs[3] shard (1024 envs, O=376, A=17, 3x512) -> bench_${TAG}_hum.json
+#   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1; fold off and on)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
@@ -106,6 +108,18 @@ for S in $STEPS; do
         --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_${TAG}_dp2.json \
         2> gpurun_out/bench_${TAG}_dp2.err || fail dp2 gpurun_out/bench_${TAG}_dp2.err
       cat gpurun_out/bench_${TAG}_dp2.json ;;
+    dp1)
+      PPO_DP_REHEARSE=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs > gpurun_out/bench_${TAG}_dp1.json \
+        2> gpurun_out/bench_${TAG}_dp1.err || fail dp1 gpurun_out/bench_${TAG}_dp1.err
+      PPO_DP_REHEARSE=1 PPO_FUSED_FOLD=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs \
+        > gpurun_out/bench_${TAG}_dp1fold.json 2> gpurun_out/bench_${TAG}_dp1fold.err \
+        || fail dp1fold gpurun_out/bench_${TAG}_dp1fold.err
+      cat gpurun_out/bench_${TAG}_dp1.json gpurun_out/bench_${TAG}_dp1fold.json ;;
+    hum)
+      timeout -k 10 500 python bench.py --num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 \
+        --steps 3 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
+        2> gpurun_out/bench_${TAG}_hum.err || fail hum gpurun_out/bench_${TAG}_hum.err
+      cat gpurun_out/bench_${TAG}_hum.json ;;
     micro)
       timeout -k 10 200 python tools/micro_fused.py 20 > gpurun_out/micro_${TAG}.txt 2>&1 || fail micro gpurun_out/micro_${TAG}.txt
       cat gpurun_out/micro_${TAG}.txt ;;
