@@ -116,9 +116,10 @@ int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d, const u
                     int all_reset, const int32_t *bounds, int n_bounds, int normalize,
                     float *state_d, int n, const float *eps_d, uint64_t seed, uint64_t offset,
                     float *action_d, float *logp_d, float *value_d, float *mean_d, void *stream);
-/* Refresh the bf16 weight images the fused kernels read from the bound f32 parameters; call after
- * the parameters change outside ppo_minibatch_grad (Adam steps, loads) and before
- * ppo_observe_act.  No-op unless the fused bf16 path is active. */
+/* Refresh the bf16 weight images the fused kernels (or the wide bf16-resident layered path,
+ * csrc/wide_path.h) read from the bound f32 parameters; call after the parameters change outside
+ * ppo_minibatch_grad (Adam steps, loads) and before ppo_observe_act.  No-op unless a bf16 path
+ * with weight images is active (ppo_policy_step refreshes the wide path's images itself). */
 int ppo_pack_weights(ppo_ctx *ctx, void *stream);
 /* Philox sampling in ppo_policy_step uses offset + *counter_d when counter_d (a device uint64)
  * is set, read when the kernel runs rather than when it is launched: a rollout captured once in
@@ -492,6 +493,23 @@ int ppo_synthetic_pixel_step(uint32_t seed, int t, const float *action_d, int n,
                              int c, int a, uint8_t *frames_out_d, const float *base_reward_d,
                              const uint8_t *base_term_d, double *reward_out_d,
                              uint8_t *term_out_d, void *stream);
+
+/* ---- wide layered path (bf16-resident activations; csrc/wide_gemm.h) ----------------------------
+ * One bf16 MFMA GEMM of the wide path on caller buffers (kernel-level parity tests and tuning).
+ * The products of network_block_creator.py:74-86 (Linear layers) and their autograd backward
+ * (ppo.py:109-135 loss.backward()), on bf16 operands with f32 accumulation:
+ *   kind 0 FWD    C[m][n] bf16 = act(sum_k A[m][k] B[n][k] + bias[n])   (rows >= *count_d: 0)
+ *   kind 1 DGRAD  C[m][n] bf16 = act'(aux[m][n]) * sum_k A[m][k] B[n][k] (aux: the layer output,
+ *                 bf16, C may alias it); colsum_d (nullable) [ceil(m / tile)][n] f32 column sums
+ *                 of C before rounding, one row per row tile
+ *   kind 2 F32    C[m][n] f32 = sum_k A[m][k] B[n][k]
+ *   kind 3 WGRAD  C[split][m][n] f32 = sum over the split's rows k of A[k][m] B[k][n] (split-K
+ *                 over *count_d (or k) rows, `splits` slabs of m*ldc floats)
+ * A, B bf16; NT kinds need k % 64 == 0 and operand rows readable up to the padded extents
+ * (round_up(m or n, tile) rows of k elements); act = PPO_ACT_*. */
+int ppo_wide_gemm(int kind, int m, int n, int k, const void *a_d, int64_t lda, const void *b_d,
+                  int64_t ldb, void *c_d, int64_t ldc, const float *bias_d, const void *aux_d,
+                  float *colsum_d, int act, int splits, const int32_t *count_d, void *stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip",
            "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip",
-           "csrc/cnn_engine.hip", "csrc/gemm_ops.hip"]
+           "csrc/cnn_engine.hip", "csrc/gemm_ops.hip", "csrc/wide_gemm.hip",
+           "csrc/wide_engine.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 
@@ -33,6 +34,19 @@ def build_host_env(verbose: bool = True) -> str:
     return out
 
 
+def _object_deps(obj: str, headers: list) -> list:
+    """The headers an object was compiled from (its -MMD file), or every header if unknown."""
+    dep = obj + ".d"
+    if not os.path.exists(dep):
+        return headers
+    with open(dep) as f:
+        words = f.read().replace("\\\n", " ").split()
+    files = [w for w in words if not w.endswith(":") and w.endswith(".h")]
+    if any(not os.path.exists(f) for f in files):
+        return headers
+    return files
+
+
 def build_library(verbose: bool = True) -> str:
     build_host_env(verbose)
     out = os.path.join(HERE, "libppo_engine.so")
@@ -49,9 +63,10 @@ def build_library(verbose: bool = True) -> str:
         os.makedirs(os.path.dirname(obj), exist_ok=True)
         objs.append(obj)
         if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d)
-                                       for d in [src] + headers):
+                                       for d in [src] + _object_deps(obj, headers)):
             continue  # object up to date (per-source incremental rebuild)
-        cmd = [hipcc, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", "-o", obj, src]
+        cmd = [hipcc, *FLAGS, "-I", os.path.join(ROOT, "include"), "-MMD", "-MF", obj + ".d",
+               "-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, cwd=HERE)))

@@ -197,6 +197,10 @@ _SIGNATURES = {
     "ppo_cnn_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
                                       POINTER(c_double), POINTER(c_int64), POINTER(c_double),
                                       POINTER(c_double)]),
+    # wide layered path (wide_gemm.hip)
+    "ppo_wide_gemm": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64,
+                              c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                              c_void_p, c_void_p]),
     "ppo_synthetic_pixel_step": (c_int, [ctypes.c_uint32, c_int, c_void_p, c_int, c_int, c_int,
                                          c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p]),

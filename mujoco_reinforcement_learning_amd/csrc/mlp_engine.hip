@@ -28,12 +28,14 @@
 #include <vector>
 
 #include "common.h"
+#include "ctx.h"
 #include "fused_policy.h"
 #include "fused_update.h"
 #include "gemm.h"
 #include "gemm_ops.h"
 #include "reduce_slabs.h"
 #include "timing.h"
+#include "wide_path.h"
 
 namespace ppo {
 
@@ -590,21 +592,6 @@ __global__ __launch_bounds__(kRedThreads) void reduce_slabs_kernel(ReduceArgs q)
 // ============================================================================================
 // Context
 // ============================================================================================
-struct LayerDesc {
-  int in, out;
-  int64_t w_off, b_off;  // flat offsets (b_off < 0: no bias)
-};
-
-struct NetDesc {
-  int n_hidden;
-  LayerDesc layer[PPO_MAX_LAYERS + 1];  // hidden layers then the head
-  int64_t begin, count;
-  int64_t logstd_off;                   // actor only
-  float *h[PPO_MAX_LAYERS];             // workspace: hidden outputs (max_rows, width)
-  float *g;                             // workspace: dH_L
-  float *dz;                            // workspace: head pre-activation grads (max_rows, out)
-};
-
 // ============================================================================================
 // Per-launch timing (timing.h): event pairs on each dispatch packet while enabled (bench.py's
 // live roofline), read back after the timed region.
@@ -634,40 +621,6 @@ const char *intern_name(const char *fmt, ...) {
 
 }  // namespace ppo
 
-struct ppo_ctx {
-  ppo_net_cfg cfg;
-  int device;
-  ppo::NetDesc net[2];
-  int64_t total_params;
-  float *params;
-  float *slabs;          // (kSlabSplits, total_params)
-  float *head_part;      // logstd partials (kHeadSplits, A) + loss partials (kHeadSplits, 2)
-  float *head_w_part;    // fused head dW/db partials (kHeadSplits, hw_stride), UpdateHeadArgs
-  const uint64_t *rng_counter;  // device Philox offset base (nullable), read at kernel run time
-  int prec;                     // GEMM precision (ppo_ctx_set_precision), PPO_PREC_F32 default
-  int hw_stride, hw_off_ba, hw_off_wc, hw_off_bc;
-  float *xg;             // gathered minibatch states (max_rows, ldx)
-  int ldx;               // round_up(W*O, 4)
-  void *arena;
-  // persistent fused update (bf16, two equal hidden layers; fused_update.hip)
-  bool fused_ok;                // network shapes the fused kernel supports
-  int fused_hidden;
-  __bf16 *fw[2][3];             // per net: bf16 W0 image (H, 32), W1 (H, H), W1^T (H, H)
-  __bf16 *fxb;                  // (max_rows, 32) staged bf16 states
-  float *fsrow;                 // (max_rows, 16) staged row scalars
-  float *fslabs;                // (kFusedMaxWG, total_params) partial gradients
-  float *floss;                 // (kFusedMaxWG, 2) loss-term partials
-  void *farena;
-  uint4 *frec;                  // (frec_cap, 128 B) staged records (ppo_stage_records)
-  int64_t frec_cap, frec_rows;
-  uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
-  int fstamp_on, fstamp_g;
-  uint32_t *fsync;              // the in-launch fold's arrival counter (zeroed per launch)
-  int *ffold_err;               // set by a fold whose grid barrier timed out
-  int fold_on;                  // ppo_ctx_fused_fold (default: PPO_FUSED_FOLD, 0)
-  int fold_g;                   // G the residency check last passed for (0: none)
-  ppo::Timing tim;
-};
 
 namespace ppo {
 
@@ -1149,6 +1102,7 @@ extern "C" int ppo_ctx_destroy(ppo_ctx *ctx) {
   if (ctx->farena) (void)hipFree(ctx->farena);
   if (ctx->fstamps) (void)hipFree(ctx->fstamps);
   if (ctx->frec) (void)hipFree(ctx->frec);
+  wide_free(ctx);
   delete ctx;
   return 0;
 }
@@ -1192,6 +1146,9 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
               ctx->cfg.max_rows);
   hipStream_t st = as_stream(stream);
   TimingScope timing_scope(ctx);
+  if (wide_active(ctx))
+    return wide_policy_step(ctx, state_d, n, eps_d, seed, offset, action_d, logp_d, value_d,
+                            mean_d, true, st);
   const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
   if (!use[0] && !use[1]) return 0;
   if (int rc = forward_hidden(ctx, use, state_d, nullptr, n, nullptr, st,
@@ -1243,6 +1200,10 @@ extern "C" int ppo_policy_step(ppo_ctx *ctx, const float *state_d, int n, const 
 
 extern "C" int ppo_pack_weights(ppo_ctx *ctx, void *stream) {
   if (int rc = check_ctx(ctx)) return rc;
+  if (wide_active(ctx)) {
+    TimingScope timing_scope(ctx);
+    return wide_pack(ctx, as_stream(stream));
+  }
   if (!fused_active(ctx)) return 0;  // the layered path reads the f32 masters directly
   TimingScope timing_scope(ctx);
   FusedArgs q{};
@@ -1519,6 +1480,11 @@ extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs
     }
     if (int rc = ppo_obs_normalize(window_d, state_d, n, o, w, bounds, n_bounds, normalize, stream))
       return rc;
+    if (wide_active(ctx)) {  // the weight images are current (ppo_pack_weights before the rollout)
+      TimingScope timing_scope(ctx);
+      return wide_policy_step(ctx, state_d, n, eps_d, seed, offset, action_d, logp_d, value_d,
+                              mean_d, false, as_stream(stream));
+    }
     return ppo_policy_step(ctx, state_d, n, eps_d, seed, offset, action_d, logp_d, value_d,
                            mean_d, stream);
   }
@@ -1584,6 +1550,10 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
     return fused_minibatch_grad(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d, b,
                                 count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
                                 loss_d, st);
+  if (wide_active(ctx))
+    return wide_minibatch_grad(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d, b,
+                               count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, grad_d,
+                               loss_d, st);
   const bool both[2] = {true, true};
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
   const int A = ctx->cfg.act_dim;
@@ -1843,6 +1813,8 @@ extern "C" int ppo_ctx_set_precision(ppo_ctx *ctx, int prec) {
   PPO_REQUIRE(prec == PPO_PREC_F32 || prec == PPO_PREC_BF16,
               "ppo_ctx_set_precision: unknown precision %d", prec);
   ctx->prec = prec;
+  if (prec == PPO_PREC_BF16)  // the wide path's workspace, for the shapes it covers
+    if (int rc = wide_alloc(ctx)) return rc;
   return 0;
 }
 

@@ -1,0 +1,724 @@
+// The wide layered path (wide_path.h): bf16-resident rollout forward and minibatch
+// forward + loss + backward for ReLU actor-critics the fused kernels do not cover (Humanoid-v4:
+// O=376, 3x512, A=17 -- BASELINE configs[3]).
+//
+// Per optimizer step (ppo.py:108-135 for one minibatch, both nets in every launch):
+//   pack     bf16 weight images W [out][in] and W^T [in][out] from the f32 masters (zero padded)
+//   gather   x[j] = bf16(states[rows[j]])                         (A5 row gather + operand rounding)
+//   FWD      h_l = relu(h_{l-1} W_l^T + b_l)                       (wide_gemm.h NT, bf16 out)
+//   F32      z = h_{L-1} W_L^T                                      (head pre-activations)
+//   loss     tanh / Normal log-prob / clipped surrogate / Huber / entropy per row (A11-A13),
+//            dz (bf16), per-block partials of the logstd and head-bias gradients and the losses
+//   WGRAD    slab[s] = dz^T h_{L-1}, then per hidden layer dZ_l^T h_{l-1} (split-K over rows)
+//   DGRAD    dZ_{l-1} = (dZ_l W_l) * relu'(h_{l-1}), written over h_{l-1}, + bias column sums
+//   reduce   fixed-order sums of the slabs / partials into the flat gradient + loss scalars
+// The same formulas as update_head_kernel / policy_head_kernel (mlp_engine.hip) on the bf16
+// emulation's operands: every product's operands rounded to bf16, f32 accumulation, biases,
+// losses and activation derivatives in f32 (the derivative of ReLU from the bf16 output: the
+// sign of a value survives RNE rounding, so it is the f32 output's).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <new>
+
+#include "common.h"
+#include "reduce_slabs.h"
+#include "timing.h"
+#include "wide_gemm.h"
+#include "wide_ops.h"
+#include "wide_path.h"
+
+namespace ppo {
+
+using wide::WideBatch;
+using wide::WideProblem;
+
+static inline int64_t rup(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+constexpr int kWideSplits = 16;      // WGRAD split-K slabs of the hidden layers
+constexpr int kWideHeadSplits = 64;  // ... of the heads (few output tiles)
+static const int g_wide_enabled = [] {
+  const char *v = getenv("PPO_WIDE");
+  return v ? atoi(v) : 1;
+}();
+
+bool wide_shapes_ok(const ppo_ctx *ctx) {
+  if (!g_wide_enabled || ctx->fused_ok) return false;
+  if (ctx->cfg.activation != PPO_ACT_RELU || ctx->cfg.act_dim > 32) return false;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    for (int l = 0; l < nd.n_hidden; ++l)
+      if (nd.layer[l].out % 8 != 0) return false;
+  }
+  return true;
+}
+
+bool wide_active(const ppo_ctx *ctx) {
+  return ctx->wide != nullptr && ctx->prec == PPO_PREC_BF16 && wide_shapes_ok(ctx);
+}
+
+int wide_alloc(ppo_ctx *ctx) {
+  if (ctx->wide || !wide_shapes_ok(ctx)) return 0;
+  WideWork *w = new (std::nothrow) WideWork();
+  PPO_REQUIRE(w != nullptr, "wide_alloc: out of host memory");
+  const int64_t R = rup(ctx->cfg.max_rows, 256);
+  w->rpad = static_cast<int>(R);
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  w->ldx = static_cast<int>(rup(din, 64));
+  const int blocks = static_cast<int>(R / kWideLossRows);
+  // carve-out in bytes; every buffer 256-B aligned, 1 KB of slack after each (tile reads past a
+  // row end stay inside the allocation)
+  int64_t bytes = 0;
+  auto take = [&](int64_t b) {
+    const int64_t o = bytes;
+    bytes += rup(b, 256) + 1024;
+    return o;
+  };
+  struct Off {
+    int64_t h[PPO_MAX_LAYERS], w[PPO_MAX_LAYERS + 1], wt[PPO_MAX_LAYERS + 1], cs[PPO_MAX_LAYERS];
+    int64_t dz, z;
+  } off[2];
+  const int64_t ox = take(R * w->ldx * 2);
+  int64_t img0 = -1, img_bytes = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    WideNetWork &wn = w->net[z];
+    for (int l = 0; l < nd.n_hidden; ++l) {
+      wn.ldh[l] = static_cast<int>(rup(nd.layer[l].out, 64));
+      off[z].h[l] = take(R * wn.ldh[l] * 2);
+      off[z].cs[l] = take((R / 64) * nd.layer[l].out * 4);
+    }
+    off[z].dz = take(R * 64 * 2);
+    off[z].z = take(R * 32 * 4);
+  }
+  // weight images last and contiguous, so the pack kernel zero-fills them as one range
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    WideNetWork &wn = w->net[z];
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      wn.ldw[l] = static_cast<int>(rup(L.in, 64));
+      wn.ldwt[l] = static_cast<int>(rup(L.out, 64));
+      const int64_t a = rup(rup(L.out, 128) * wn.ldw[l] * 2, 256);
+      const int64_t b = rup(rup(L.in, 128) * wn.ldwt[l] * 2, 256);
+      off[z].w[l] = bytes;
+      bytes += a;
+      off[z].wt[l] = bytes;
+      bytes += b;
+      if (img0 < 0) img0 = off[z].w[l];
+      img_bytes = bytes - img0;
+    }
+  }
+  bytes += 1024;
+  const int64_t opart = take(static_cast<int64_t>(blocks) * kWidePart * 4);
+  const int64_t oloss = take(static_cast<int64_t>(blocks) * 2 * 4);
+  void *arena = nullptr;
+  hipError_t e = hipMalloc(&arena, bytes);
+  if (e != hipSuccess) {
+    delete w;
+    set_error("wide_alloc: hipMalloc(%lld bytes) failed: %s", static_cast<long long>(bytes),
+              hipGetErrorString(e));
+    return PPO_EHIP;
+  }
+  e = hipMemset(arena, 0, bytes);  // pad rows / columns of every operand stay zero
+  if (e != hipSuccess) {
+    (void)hipFree(arena);
+    delete w;
+    set_error("wide_alloc: hipMemset failed: %s", hipGetErrorString(e));
+    return PPO_EHIP;
+  }
+  char *base = static_cast<char *>(arena);
+  w->arena = arena;
+  w->x = reinterpret_cast<__bf16 *>(base + ox);
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    WideNetWork &wn = w->net[z];
+    for (int l = 0; l < nd.n_hidden; ++l) {
+      wn.h[l] = reinterpret_cast<__bf16 *>(base + off[z].h[l]);
+      wn.colsum[l] = reinterpret_cast<float *>(base + off[z].cs[l]);
+    }
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      wn.w[l] = reinterpret_cast<__bf16 *>(base + off[z].w[l]);
+      wn.wt[l] = reinterpret_cast<__bf16 *>(base + off[z].wt[l]);
+    }
+    wn.dz = reinterpret_cast<__bf16 *>(base + off[z].dz);
+    wn.z = reinterpret_cast<float *>(base + off[z].z);
+  }
+  w->part = reinterpret_cast<float *>(base + opart);
+  w->loss_part = reinterpret_cast<float *>(base + oloss);
+  w->img_elems = img_bytes / 2;
+  ctx->wide = w;
+  return 0;
+}
+
+void wide_free(ppo_ctx *ctx) {
+  if (!ctx->wide) return;
+  if (ctx->wide->arena) (void)hipFree(ctx->wide->arena);
+  delete ctx->wide;
+  ctx->wide = nullptr;
+}
+
+// ============================================================================================
+// Weight images: dst[r][c] = bf16(W[r][c]) (or W^T), zero outside the tensor; 8 elements per
+// thread, one 16-B store.
+// ============================================================================================
+constexpr int kMaxImages = 2 * 2 * (PPO_MAX_LAYERS + 1);
+struct ImageDesc {
+  const float *w;   // [out][in] f32 master
+  __bf16 *dst;
+  int out, in;      // tensor shape
+  int rows, cols;   // image shape (cols % 8 == 0)
+  int transposed;   // dst = W^T
+  int blocks;       // first block of this image (prefix over images)
+};
+struct PackArgs {
+  ImageDesc img[kMaxImages];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q) {
+  int i = 0;
+  while (i + 1 < q.n && q.img[i + 1].blocks <= static_cast<int>(blockIdx.x)) ++i;
+  const ImageDesc d = q.img[i];
+  const int64_t e = (static_cast<int64_t>(blockIdx.x - d.blocks) * 256 + threadIdx.x) * 8;
+  if (e >= static_cast<int64_t>(d.rows) * d.cols) return;
+  const int r = static_cast<int>(e / d.cols), c0 = static_cast<int>(e % d.cols);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const int o = d.transposed ? c : r, in = d.transposed ? r : c;
+    v[j] = (o < d.out && in < d.in) ? d.w[static_cast<int64_t>(o) * d.in + in] : 0.f;
+  }
+  *reinterpret_cast<uint4 *>(d.dst + e) =
+      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
+                 wide::pack2(v[6], v[7]));
+}
+
+int wide_pack(ppo_ctx *ctx, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  PackArgs q{};
+  int blocks = 0;
+  double elems = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    const WideNetWork &wn = W.net[z];
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      for (int t = 0; t < 2; ++t) {
+        ImageDesc &d = q.img[q.n++];
+        d.w = ctx->params + L.w_off;
+        d.out = L.out;
+        d.in = L.in;
+        d.transposed = t;
+        d.dst = t ? wn.wt[l] : wn.w[l];
+        d.rows = static_cast<int>(t ? rup(L.in, 128) : rup(L.out, 128));
+        d.cols = t ? wn.ldwt[l] : wn.ldw[l];
+        d.blocks = blocks;
+        blocks += ceil_div(static_cast<int64_t>(d.rows) * d.cols, 256 * 8);
+        elems += static_cast<double>(d.out) * d.in;
+      }
+    }
+  }
+  launch_k(TimRec{KC_GATHER, "wide_pack_kernel", 0.0, elems * (4.0 + 2.0)}, wide_pack_kernel,
+           dim3(blocks), dim3(256), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// ============================================================================================
+// Row staging: x[j][0:ldx] = bf16(states[rows ? rows[j] : j][0:din]) for j < count, zero rows
+// for count <= j < rows_pad (the padding contract of wide_gemm.h).
+// ============================================================================================
+__global__ __launch_bounds__(256) void wide_gather_kernel(const float *__restrict__ states,
+                                                          const int32_t *__restrict__ rows,
+                                                          const int32_t *__restrict__ rows_n,
+                                                          int n, int rows_pad, int din, int ldx,
+                                                          __bf16 *__restrict__ x) {
+  const int count = rows_n ? *rows_n : n;
+  const int per_row = ldx / 8;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= static_cast<int64_t>(rows_pad) * per_row) return;
+  const int j = static_cast<int>(i / per_row), c0 = static_cast<int>(i % per_row) * 8;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (j < count) {
+    const float *src = states + static_cast<int64_t>(rows ? rows[j] : j) * din;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (c0 + e < din) v[e] = src[c0 + e];
+  }
+  *reinterpret_cast<uint4 *>(x + static_cast<int64_t>(j) * ldx + c0) =
+      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
+                 wide::pack2(v[6], v[7]));
+}
+
+static int stage_rows(ppo_ctx *ctx, const float *states, const int32_t *rows,
+                      const int32_t *count_d, int n, int rows_pad, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
+  const int64_t items = static_cast<int64_t>(rows_pad) * (W.ldx / 8);
+  launch_k(TimRec{KC_GATHER, "wide_gather_kernel", 0.0,
+                  static_cast<double>(n) * din * 4.0 + static_cast<double>(rows_pad) * W.ldx * 2.0},
+           wide_gather_kernel, dim3(ceil_div(items, 256)), dim3(256), 0, st, states, rows,
+           count_d, n, rows_pad, din, W.ldx, W.x);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// ============================================================================================
+// Forward through the hidden layers and the head pre-activations (both nets per launch)
+// ============================================================================================
+static int forward(ppo_ctx *ctx, const bool use[2], int rows_pad, const int32_t *count_d,
+                   hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  const int max_l = std::max(use[0] ? ctx->net[0].n_hidden : 0, use[1] ? ctx->net[1].n_hidden : 0);
+  for (int l = 0; l < max_l; ++l) {
+    WideBatch wb{};
+    wb.rows_n = count_d;
+    wb.act = ctx->cfg.activation;
+    int np = 0, max_n = 0;
+    for (int z = 0; z < 2; ++z) {
+      const NetDesc &nd = ctx->net[z];
+      if (!use[z] || l >= nd.n_hidden) continue;
+      const LayerDesc &L = nd.layer[l];
+      const WideNetWork &wn = W.net[z];
+      WideProblem &P = wb.p[np++];
+      P.a = l == 0 ? W.x : wn.h[l - 1];
+      P.lda = l == 0 ? W.ldx : wn.ldh[l - 1];
+      P.b = wn.w[l];
+      P.ldb = wn.ldw[l];
+      P.c = wn.h[l];
+      P.ldc = wn.ldh[l];
+      P.bias = L.b_off >= 0 ? ctx->params + L.b_off : nullptr;
+      P.m = rows_pad;
+      P.n = L.out;
+      P.k = wn.ldw[l];
+      max_n = std::max(max_n, L.out);
+    }
+    if (np)
+      if (int rc = wide::run(wide::WK_FWD, wb, np, rows_pad, max_n, 0, st)) return rc;
+  }
+  WideBatch wb{};
+  wb.rows_n = count_d;
+  int np = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    if (!use[z]) continue;
+    const int L = nd.n_hidden;
+    const WideNetWork &wn = W.net[z];
+    WideProblem &P = wb.p[np++];
+    P.a = wn.h[L - 1];
+    P.lda = wn.ldh[L - 1];
+    P.b = wn.w[L];
+    P.ldb = wn.ldw[L];
+    P.c = wn.z;
+    P.ldc = 32;
+    P.m = rows_pad;
+    P.n = 32;
+    P.k = wn.ldw[L];
+  }
+  return wide::run(wide::WK_F32, wb, np, rows_pad, 32, 0, st);
+}
+
+// ============================================================================================
+// Rollout head: sampling + log-prob + value from the head pre-activations (policy_head_kernel's
+// formulas, ppo_agent.py:27-43 and ppo.py:23-26): one thread per row, actions in order.
+// ============================================================================================
+struct WidePolicyArgs {
+  const float *za, *zc;  // [rows][32] head pre-activations (nullable per net)
+  int n, act_dim;
+  const float *ba, *logstd, *bc;
+  float omv;
+  const float *eps;
+  uint64_t seed, offset;
+  const uint64_t *offset_base;
+  float *action, *logp, *value, *mean;
+};
+
+// 32 lanes per row (A <= 32): lane a samples action a; the row's log-prob is summed in action
+// order by the row's first lane (the sequential order of policy_head_kernel).
+__global__ __launch_bounds__(256) void wide_policy_head_kernel(WidePolicyArgs q) {
+  const int lane = threadIdx.x & 63, a = lane & 31;
+  const int j = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool row_ok = j < q.n;  // uniform per 32-lane half; both halves take every shuffle
+  if (q.za) {
+    float lp = 0.f;
+    if (row_ok && a < q.act_dim) {
+      const float zr = q.za[static_cast<int64_t>(j) * 32 + a];
+      const float z = q.ba ? zr + q.ba[a] : zr;
+      const float mu = q.omv * tanhf(z);
+      const float sd = expf(q.logstd[a]);
+      const int64_t idx = static_cast<int64_t>(j) * q.act_dim + a;
+      const uint64_t base = q.offset + (q.offset_base ? *q.offset_base : 0);
+      const float e = q.eps ? q.eps[idx] : philox_normal_at(q.seed, base + idx);
+      const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
+      if (q.action) q.action[idx] = x;
+      if (q.mean) q.mean[idx] = mu;
+      const float d = x - mu;
+      const float var = sd * sd;
+      lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+    }
+    float s = 0.f;
+    for (int k = 0; k < q.act_dim; ++k) s += __shfl(lp, (lane & 32) + k, 64);
+    if (row_ok && a == 0 && q.logp) q.logp[j] = s;
+  }
+  if (row_ok && a == 0 && q.zc && q.value) {
+    const float v = q.zc[static_cast<int64_t>(j) * 32];
+    q.value[j] = q.bc ? v + q.bc[0] : v;
+  }
+}
+
+int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
+                     uint64_t offset, float *action_d, float *logp_d, float *value_d,
+                     float *mean_d, bool pack, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
+  if (!use[0] && !use[1]) return 0;
+  const int rows_pad = static_cast<int>(rup(n, 64));
+  if (pack)
+    if (int rc = wide_pack(ctx, st)) return rc;
+  if (int rc = stage_rows(ctx, state_d, nullptr, nullptr, n, rows_pad, st)) return rc;
+  if (int rc = forward(ctx, use, rows_pad, nullptr, st)) return rc;
+  const NetDesc &A = ctx->net[0], &C = ctx->net[1];
+  WidePolicyArgs q{};
+  q.n = n;
+  q.act_dim = ctx->cfg.act_dim;
+  q.omv = ctx->cfg.output_max_value;
+  if (use[0]) {
+    const LayerDesc &hl = A.layer[A.n_hidden];
+    q.za = W.net[0].z;
+    q.ba = hl.b_off >= 0 ? ctx->params + hl.b_off : nullptr;
+    q.logstd = ctx->params + A.logstd_off;
+  }
+  if (use[1]) {
+    q.zc = W.net[1].z;
+    q.bc = ctx->params + C.layer[C.n_hidden].b_off;
+  }
+  q.eps = eps_d;
+  q.seed = seed;
+  q.offset = offset;
+  q.offset_base = ctx->rng_counter;
+  q.action = action_d;
+  q.logp = logp_d;
+  q.value = value_d;
+  q.mean = mean_d;
+  const int na = q.act_dim;
+  launch_k(TimRec{KC_POLICY_HEAD, "wide_policy_head_kernel", 0.0,
+                  4.0 * n * (32.0 * (use[0] + use[1]) + (eps_d ? na : 0) + (action_d ? na : 0) +
+                             (mean_d ? na : 0) + 2.0)},
+           wide_policy_head_kernel, dim3(ceil_div(n, 8)), dim3(256), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// ============================================================================================
+// Minibatch loss heads (update_head_kernel's formulas, ppo.py:109-135): one thread per row.
+// dz rows (bf16, 64 columns, zero past the head width and for rows >= count), and per block the
+// fixed-order sums of d loss / d logstd, the head-bias gradients (the f32 dz before rounding) and
+// the two loss terms.
+// ============================================================================================
+struct WideLossArgs {
+  const float *za, *zc;
+  __bf16 *dza, *dzc;
+  int act_dim;
+  const float *ba, *logstd, *bc;
+  float omv;
+  const int32_t *rows;
+  const int32_t *rows_n;
+  int b;
+  const float *actions, *old_logp, *adv, *vtarget;
+  float clip_lo, clip_hi, ent_coef, inv_b, inv_ba;
+  float *part, *loss_part;
+};
+
+// Block partials: per action a, the wave's butterfly sums of d loss / d logstd_a and of dz_a go
+// to LDS, then waves 0..3 are added in order; the same for the critic bias gradient and the two
+// loss terms.  The per-action values are recomputed in a second pass (tanh again) rather than
+// kept in per-lane arrays.
+__device__ __forceinline__ float wave_bfly(float s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  return s;
+}
+
+__global__ __launch_bounds__(kWideLossRows) void wide_loss_kernel(WideLossArgs q) {
+  constexpr int NWV = kWideLossRows / 64;
+  __shared__ float red[NWV][kWidePart];
+  __shared__ float lred[NWV][2];
+  __shared__ float s_sd[32], s_logsd[32], s_var[32], s_b[32];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int A = q.act_dim;
+  if (tid < 32) {
+    const float sd = tid < A ? expf(q.logstd[tid]) : 1.f;
+    s_sd[tid] = sd;
+    s_logsd[tid] = logf(sd);
+    s_var[tid] = sd * sd;
+    s_b[tid] = (q.ba && tid < A) ? q.ba[tid] : 0.f;
+  }
+  __syncthreads();
+  const int count = q.rows_n ? *q.rows_n : q.b;
+  const int j = blockIdx.x * kWideLossRows + tid;
+  const bool valid = j < count;
+  const int64_t sr = valid ? q.rows[j] : 0;
+  const float *zr = q.za + static_cast<int64_t>(j) * 32;
+  const float *xr = q.actions + sr * A;
+  const bool has_b = q.ba != nullptr;
+  float logp = 0.f;
+  for (int a = 0; a < A; ++a) {
+    const float z = has_b ? zr[a] + s_b[a] : zr[a];
+    const float mu = q.omv * tanhf(z);
+    const float x = valid ? xr[a] : mu;
+    const float d = x - mu;
+    logp += ((-(d * d)) / (2.f * s_var[a]) - s_logsd[a]) - kLogSqrt2Pi;
+  }
+  const float old_lp = valid ? q.old_logp[sr] : logp;
+  const float adv = valid ? q.adv[sr] : 0.f;
+  const float ratio = expf(logp - old_lp);
+  const float s1 = ratio * adv;
+  const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+  const float s2 = cl * adv;
+  const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+  const float g = -q.inv_b;
+  const float g1 = (s1 < s2) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+  const float g2 = (s2 < s1) ? g : (s1 == s2 ? g * 0.5f : 0.f);
+  const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+  const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+  const float dlogp = valid ? dratio * ratio : 0.f;
+  uint32_t *dzrow = reinterpret_cast<uint32_t *>(q.dza + static_cast<int64_t>(j) * 64);
+  for (int a0 = 0; a0 < A; a0 += 2) {
+    float dzp[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int a = a0 + h;
+      float dz = 0.f, ls = 0.f;
+      if (a < A) {
+        const float z = has_b ? zr[a] + s_b[a] : zr[a];
+        const float y = tanhf(z);
+        const float mu = q.omv * y;
+        const float x = valid ? xr[a] : mu;
+        const float d = x - mu;
+        const float dmu = dlogp * (d / s_var[a]);
+        dz = valid ? (dmu * q.omv) * (1.f - y * y) : 0.f;
+        ls = valid ? dlogp * ((d * d) / s_var[a] - 1.f) - q.ent_coef * q.inv_ba : 0.f;
+        const float sl = wave_bfly(ls), sz = wave_bfly(dz);
+        if (lane == 0) {
+          red[wid][a] = sl;
+          red[wid][32 + a] = sz;
+        }
+      }
+      dzp[h] = dz;
+    }
+    dzrow[a0 >> 1] = wide::pack2(dzp[0], dzp[1]);  // columns >= A stay zero (never written)
+  }
+  // critic
+  const float zc0 = q.zc[static_cast<int64_t>(j) * 32];
+  const float v = q.bc ? zc0 + q.bc[0] : zc0;
+  const float vt = valid ? q.vtarget[sr] : v;
+  const float diff = v - vt;
+  const float ad = fabsf(diff);
+  const float dv = valid ? q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff)) : 0.f;
+  reinterpret_cast<uint32_t *>(q.dzc + static_cast<int64_t>(j) * 64)[0] = wide::pack2(dv, 0.f);
+  const float sdv = wave_bfly(dv);
+  const float sla = wave_bfly(valid ? mn : 0.f);
+  const float slc = wave_bfly(valid ? ((ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f)) : 0.f);
+  if (lane == 0) {
+    red[wid][64] = sdv;
+    lred[wid][0] = sla;
+    lred[wid][1] = slc;
+  }
+  __syncthreads();
+  float *part = q.part + static_cast<int64_t>(blockIdx.x) * kWidePart;
+  if (tid < 65 && (tid >= 64 || (tid & 31) < A)) {
+    float s = red[0][tid];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) s += red[w][tid];
+    part[tid] = s;
+  } else if (tid == 65 || tid == 66) {
+    const int k = tid - 65;
+    float s = lred[0][k];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) s += lred[w][k];
+    q.loss_part[2 * blockIdx.x + k] = s;
+  }
+}
+
+__global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q) {
+  (void)reduce_slab_block(q, blockIdx.x);
+}
+
+int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                        const float *old_logp_d, const float *adv_d, const float *vtarget_d,
+                        const int32_t *rows_d, int b, const int32_t *count_d, float clip_lo,
+                        float clip_hi, float entropy_coef, float inv_b, float inv_ba,
+                        float *grad_d, float *loss_d, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  const int rows_pad = static_cast<int>(rup(b, 64));
+  const int64_t P = ctx->total_params;
+  const int A = ctx->cfg.act_dim;
+  NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
+  if (int rc = wide_pack(ctx, st)) return rc;
+  if (int rc = stage_rows(ctx, states_d, rows_d, count_d, b, rows_pad, st)) return rc;
+  const bool both[2] = {true, true};
+  if (int rc = forward(ctx, both, rows_pad, count_d, st)) return rc;
+
+  // ---- loss heads -----------------------------------------------------------------------------
+  const int blocks = ceil_div(rows_pad, kWideLossRows);
+  {
+    WideLossArgs q{};
+    q.za = W.net[0].z;
+    q.zc = W.net[1].z;
+    q.dza = W.net[0].dz;
+    q.dzc = W.net[1].dz;
+    q.act_dim = A;
+    const LayerDesc &HA = NA.layer[NA.n_hidden], &HC = NC.layer[NC.n_hidden];
+    q.ba = HA.b_off >= 0 ? ctx->params + HA.b_off : nullptr;
+    q.logstd = ctx->params + NA.logstd_off;
+    q.bc = ctx->params + HC.b_off;
+    q.omv = ctx->cfg.output_max_value;
+    q.rows = rows_d;
+    q.rows_n = count_d;
+    q.b = b;
+    q.actions = actions_d;
+    q.old_logp = old_logp_d;
+    q.adv = adv_d;
+    q.vtarget = vtarget_d;
+    q.clip_lo = clip_lo;
+    q.clip_hi = clip_hi;
+    q.ent_coef = entropy_coef;
+    q.inv_b = inv_b;
+    q.inv_ba = inv_ba;
+    q.part = W.part;
+    q.loss_part = W.loss_part;
+    launch_k(TimRec{KC_UPDATE_HEAD, "wide_loss_kernel", 0.0,
+                    static_cast<double>(b) * (4.0 * 64 + 4.0 * A + 16.0 + 256.0)},
+             wide_loss_kernel, dim3(blocks), dim3(kWideLossRows), 0, st, q);
+    PPO_LAUNCHED();
+  }
+
+  // ---- backward, deepest layer first: WGRAD of layer l (needs its input), then DGRAD into it --
+  int colsum_rows[2][PPO_MAX_LAYERS] = {};
+  int splits_of[2][PPO_MAX_LAYERS + 1] = {};
+  const int depth = std::max(NA.n_hidden, NC.n_hidden);
+  for (int s = 0; s <= depth; ++s) {
+    // weight gradient of layer l = n_hidden - s
+    WideBatch wg{};
+    wg.rows_n = count_d;
+    int np = 0, max_m = 0, max_n = 0;
+    for (int z = 0; z < 2; ++z) {
+      const NetDesc &nd = ctx->net[z];
+      const int l = nd.n_hidden - s;
+      if (l < 0) continue;
+      const LayerDesc &L = nd.layer[l];
+      const WideNetWork &wn = W.net[z];
+      WideProblem &Q = wg.p[np++];
+      Q.a = l == nd.n_hidden ? wn.dz : wn.h[l];
+      Q.lda = l == nd.n_hidden ? 64 : wn.ldh[l];
+      Q.b = l == 0 ? W.x : wn.h[l - 1];
+      Q.ldb = l == 0 ? W.ldx : wn.ldh[l - 1];
+      Q.c = ctx->slabs + L.w_off;
+      Q.ldc = L.in;
+      Q.m = L.out;
+      Q.n = L.in;
+      Q.k = rows_pad;
+      Q.slab_stride = P;
+      max_m = std::max(max_m, L.out);
+      max_n = std::max(max_n, L.in);
+    }
+    if (np) {
+      wg.splits = s == 0 ? kWideHeadSplits : kWideSplits;
+      for (int z = 0; z < 2; ++z)
+        if (ctx->net[z].n_hidden - s >= 0) splits_of[z][ctx->net[z].n_hidden - s] = wg.splits;
+      if (int rc = wide::run(wide::WK_WGRAD, wg, np, max_m, max_n, b, st)) return rc;
+    }
+    // input gradient of layer l into h[l-1] (l >= 1)
+    WideBatch dg{};
+    dg.rows_n = count_d;
+    dg.act = ctx->cfg.activation;
+    np = 0;
+    max_n = 0;
+    for (int z = 0; z < 2; ++z) {
+      const NetDesc &nd = ctx->net[z];
+      const int l = nd.n_hidden - s;
+      if (l < 1) continue;
+      const LayerDesc &L = nd.layer[l];
+      const WideNetWork &wn = W.net[z];
+      WideProblem &Q = dg.p[np++];
+      Q.a = l == nd.n_hidden ? wn.dz : wn.h[l];
+      Q.lda = l == nd.n_hidden ? 64 : wn.ldh[l];
+      Q.b = wn.wt[l];
+      Q.ldb = wn.ldwt[l];
+      Q.c = wn.h[l - 1];
+      Q.aux = wn.h[l - 1];
+      Q.ldc = wn.ldh[l - 1];
+      Q.colsum = nd.layer[l - 1].b_off >= 0 ? wn.colsum[l - 1] : nullptr;
+      Q.n_colsum = L.in;
+      Q.m = rows_pad;
+      Q.n = L.in;
+      Q.k = wn.ldwt[l];
+      max_n = std::max(max_n, L.in);
+    }
+    if (np) {
+      const int tile = wide::row_tile(wide::WK_DGRAD, rows_pad, max_n);
+      for (int z = 0; z < 2; ++z) {
+        const int l = ctx->net[z].n_hidden - s;
+        if (l >= 1) colsum_rows[z][l - 1] = ceil_div(rows_pad, tile);
+      }
+      if (int rc = wide::run(wide::WK_DGRAD, dg, np, rows_pad, max_n, 0, st)) return rc;
+    }
+  }
+
+  // ---- fixed-order reduction into the flat gradient + loss scalars ----------------------------
+  ReduceArgs r{};
+  int ns = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    if (z == 0) {
+      ReduceSeg &g = r.seg[ns++];
+      g.dst = nd.logstd_off;
+      g.len = A;
+      g.src = W.part;
+      g.stride = kWidePart;
+      g.nsplit = blocks;
+    }
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      ReduceSeg &g = r.seg[ns++];
+      g.dst = L.w_off;
+      g.len = static_cast<int64_t>(L.out) * L.in;
+      g.src = ctx->slabs + L.w_off;
+      g.stride = P;
+      g.nsplit = splits_of[z][l];
+      if (L.b_off >= 0) {
+        ReduceSeg &gb = r.seg[ns++];
+        gb.dst = L.b_off;
+        gb.len = L.out;
+        if (l < nd.n_hidden) {
+          gb.src = W.net[z].colsum[l];
+          gb.stride = L.out;
+          gb.nsplit = colsum_rows[z][l];
+        } else {
+          gb.src = W.part + (z == 0 ? 32 : 64);
+          gb.stride = kWidePart;
+          gb.nsplit = blocks;
+        }
+      }
+    }
+  }
+  r.nseg = ns;
+  r.total = P;
+  r.grad = grad_d;
+  r.loss_part = W.loss_part;
+  r.loss_splits = blocks;
+  r.inv_b = inv_b;
+  r.logstd = ctx->params + NA.logstd_off;
+  r.act_dim = A;
+  r.ent_coef = entropy_coef;
+  r.loss_out = loss_d;
+  double slab_floats = 0;
+  for (int i = 0; i < ns; ++i) slab_floats += static_cast<double>(r.seg[i].nsplit) * r.seg[i].len;
+  launch_k(TimRec{KC_REDUCE, "wide_reduce_kernel", slab_floats, 4.0 * (slab_floats + P)},
+           wide_reduce_kernel, dim3(ceil_div(P, kRedParams)), dim3(kRedThreads), 0, st, r);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+}  // namespace ppo

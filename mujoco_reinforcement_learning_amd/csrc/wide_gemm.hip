@@ -1,0 +1,123 @@
+// The single instantiation of the wide-path GEMM templates (wide_gemm.h) and their launch helper,
+// plus ppo_wide_gemm: the same launches on caller buffers (kernel-level parity tests, tuning).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "wide_gemm.h"
+#include "wide_ops.h"
+
+namespace ppo {
+namespace wide {
+
+template <int TM, int TN, int WM, int WN, int KIND, int NS>
+static int launch_cfg(const WideBatch &wb, int nprob, int max_m, int max_n, int kflops,
+                      hipStream_t st) {
+  using C = WideCfg<TM, TN, WM, WN, KIND, NS>;
+  const int tiles = ceil_div(max_m, C::BM) * ceil_div(max_n, C::BN);
+  const dim3 grid(tiles, KIND == WK_WGRAD ? wb.splits : 1, nprob);
+  TimRec rec{KIND == WK_FWD || KIND == WK_F32 ? KC_GEMM_FWD
+                                              : (KIND == WK_DGRAD ? KC_GEMM_DGRAD : KC_GEMM_WGRAD),
+             nullptr, 0.0, 0.0};
+  if (tim_active()) {
+    rec.name = intern_name("wide_gemm_kernel<%d, %d, %d, %d, %d, %d>", TM, TN, WM, WN, KIND, NS);
+    for (int i = 0; i < nprob; ++i) {  // algorithmic: bf16 A + B read once, C written once
+      const WideProblem &p = wb.p[i];
+      const double k = KIND == WK_WGRAD ? kflops : p.k;
+      rec.flops += 2.0 * p.m * p.n * k;
+      rec.bytes += 2.0 * (static_cast<double>(p.m) * k + static_cast<double>(p.n) * k) +
+                   static_cast<double>(p.m) * p.n *
+                       (KIND == WK_FWD ? 2.0 : KIND == WK_DGRAD ? 4.0 : 4.0 * (KIND == WK_WGRAD ? wb.splits : 1));
+    }
+  }
+  launch_k(rec, wide_gemm_kernel<TM, TN, WM, WN, KIND, NS>, grid, dim3(C::NT), 0, st, wb);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// Tile choice: 128 x 128 (4 waves of 64 x 64) for the minibatch GEMMs, 64 x 64 for rollout-sized
+// row counts (enough workgroups to cover the chip), 128 x 32 / 32 x 128 for the heads' narrow
+// products.  PPO_WIDE_CFG=<n> forces a tile / stage variant (tools/wide_bench.py sweeps).
+template <int KIND>
+static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kflops,
+                    hipStream_t st) {
+  const char *force = getenv("PPO_WIDE_CFG");
+  const int f = force ? atoi(force) : -1;
+  if (KIND == WK_WGRAD) {
+    if (max_m <= 32) return launch_cfg<1, 1, 1, 4, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    switch (f) {
+      case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+      case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
+      default: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    }
+  }
+  if (KIND == WK_F32 || (KIND == WK_FWD && max_n <= 32))
+    return launch_cfg<1, 1, 4, 1, KIND, 8>(wb, nprob, max_m, max_n, kflops, st);
+  if (max_m <= 4096) {
+    if (f == 5) return launch_cfg<1, 1, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
+    return launch_cfg<1, 1, 2, 2, KIND, 8>(wb, nprob, max_m, max_n, kflops, st);
+  }
+  switch (f) {
+    case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
+    default: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+  }
+}
+
+int run(int kind, const WideBatch &wb, int nprob, int max_m, int max_n, int kflops,
+        hipStream_t st) {
+  switch (kind) {
+    case WK_FWD: return run_kind<WK_FWD>(wb, nprob, max_m, max_n, kflops, st);
+    case WK_DGRAD: return run_kind<WK_DGRAD>(wb, nprob, max_m, max_n, kflops, st);
+    case WK_F32: return run_kind<WK_F32>(wb, nprob, max_m, max_n, kflops, st);
+    case WK_WGRAD: return run_kind<WK_WGRAD>(wb, nprob, max_m, max_n, kflops, st);
+    default:
+      set_error("wide gemm: unknown kind %d", kind);
+      return PPO_EINVAL;
+  }
+}
+
+int row_tile(int kind, int max_m, int max_n) {
+  if (kind == WK_F32 || (kind == WK_FWD && max_n <= 32)) return 128;
+  return max_m <= 4096 ? 64 : 128;
+}
+
+}  // namespace wide
+}  // namespace ppo
+
+using namespace ppo;
+
+extern "C" int ppo_wide_gemm(int kind, int m, int n, int k, const void *a_d, int64_t lda,
+                             const void *b_d, int64_t ldb, void *c_d, int64_t ldc,
+                             const float *bias_d, const void *aux_d, float *colsum_d, int act,
+                             int splits, const int32_t *count_d, void *stream) {
+  PPO_REQUIRE(kind >= wide::WK_FWD && kind <= wide::WK_WGRAD, "ppo_wide_gemm: kind %d", kind);
+  PPO_REQUIRE(a_d && b_d && c_d && m > 0 && n > 0 && k > 0, "ppo_wide_gemm: bad operands");
+  PPO_REQUIRE(kind == wide::WK_WGRAD || k % wide::kBK == 0,
+              "ppo_wide_gemm: NT reduction length %d must be a multiple of 64", k);
+  PPO_REQUIRE(kind == wide::WK_WGRAD || (n % 8 == 0 && ldc % 8 == 0),
+              "ppo_wide_gemm: NT outputs need n %% 8 == 0 and ldc %% 8 == 0");
+  PPO_REQUIRE(lda % 8 == 0 && ldb % 8 == 0, "ppo_wide_gemm: operand rows must be 16-B aligned");
+  PPO_REQUIRE(kind != wide::WK_DGRAD || aux_d, "ppo_wide_gemm: DGRAD needs aux");
+  wide::WideBatch wb{};
+  wide::WideProblem &p = wb.p[0];
+  p.a = static_cast<const __bf16 *>(a_d);
+  p.lda = lda;
+  p.b = static_cast<const __bf16 *>(b_d);
+  p.ldb = ldb;
+  p.c = c_d;
+  p.ldc = ldc;
+  p.bias = bias_d;
+  p.aux = static_cast<const __bf16 *>(aux_d);
+  p.colsum = colsum_d;
+  p.n_colsum = n;
+  p.m = m;
+  p.n = n;
+  p.k = k;
+  p.slab_stride = static_cast<int64_t>(m) * ldc;
+  wb.rows_n = count_d;
+  wb.act = act;
+  wb.splits = std::max(1, splits);
+  FreeTimingScope ts;
+  return wide::run(kind, wb, 1, m, n, k, as_stream(stream));
+}

@@ -1,0 +1,59 @@
+// The wide layered path: the MLP actor-critic's rollout forward and minibatch forward + loss +
+// backward with bf16-resident activations (PPO_PREC_BF16, ReLU nets the fused kernels do not
+// cover, e.g. Humanoid 3x512 with O=376 and A=17).  Kernels: wide_gemm.h (products),
+// wide_engine.hip (gather, heads, loss, weight images).  Entry points route here from
+// ppo_policy_step / ppo_minibatch_grad / ppo_pack_weights (mlp_engine.hip) when wide_active().
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ctx.h"
+
+namespace ppo {
+
+struct WideNetWork {
+  __bf16 *h[PPO_MAX_LAYERS];       // [rpad][ldh] hidden outputs; backward overwrites them with dZ
+  int ldh[PPO_MAX_LAYERS];         // round_up(width, 64), pad columns stay zero
+  __bf16 *w[PPO_MAX_LAYERS + 1];   // W image [round_up(out, 128)][round_up(in, 64)] (head: l = L)
+  __bf16 *wt[PPO_MAX_LAYERS + 1];  // W^T image [round_up(in, 128)][round_up(out, 64)]
+  int ldw[PPO_MAX_LAYERS + 1], ldwt[PPO_MAX_LAYERS + 1];
+  float *colsum[PPO_MAX_LAYERS];   // [rpad / 64][out] bias-gradient partials per DGRAD row tile
+  __bf16 *dz;                      // [rpad][64] head pre-activation gradients (bf16 operand)
+  float *z;                        // [rpad][32] head pre-activations (f32)
+};
+
+struct WideWork {
+  int rpad;                        // rows allocated: round_up(max_rows, 128)
+  __bf16 *x;                       // [rpad][ldx] bf16 states (gathered minibatch / rollout rows)
+  int ldx;                         // round_up(W*O, 64)
+  WideNetWork net[2];
+  float *part;                     // loss-kernel partials [blocks][kWidePart]
+  float *loss_part;                // [blocks][2]
+  int64_t img_elems;               // bf16 elements of all weight images (pack kernel extent)
+  void *arena;
+};
+
+constexpr int kWideLossRows = 256;  // rows per loss-kernel block
+constexpr int kWidePart = 96;       // per block: logstd grads [0,32), actor head bias [32,64),
+                                    // critic head bias [64]
+
+// shapes the wide path covers (precision is checked at use)
+bool wide_shapes_ok(const ppo_ctx *ctx);
+bool wide_active(const ppo_ctx *ctx);
+// allocate / free the workspace (outside graph capture)
+int wide_alloc(ppo_ctx *ctx);
+void wide_free(ppo_ctx *ctx);
+// refresh the bf16 weight images from the f32 master parameters
+int wide_pack(ppo_ctx *ctx, hipStream_t st);
+int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
+                     uint64_t offset, float *action_d, float *logp_d, float *value_d,
+                     float *mean_d, bool pack, hipStream_t st);  // pack: refresh the images first
+int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
+                        const float *old_logp_d, const float *adv_d, const float *vtarget_d,
+                        const int32_t *rows_d, int b, const int32_t *count_d, float clip_lo,
+                        float clip_hi, float entropy_coef, float inv_b, float inv_ba,
+                        float *grad_d, float *loss_d, hipStream_t st);
+
+}  // namespace ppo

@@ -276,3 +276,34 @@ def test_hip_forward_matches_reference_golden(gpu, name):
                                atol=1e-6)
     std = agent.networks["actor"].actor_logstd.detach().exp().cpu()
     assert torch.equal(std[None].expand(len(x), -1), torch.from_numpy(z[f"{name}/std"]))
+
+
+# --------------------------------------------- bf16 policy step on the wide path (Humanoid shapes)
+def test_policy_step_humanoid_bf16(gpu):
+    """The rollout step on the wide bf16-resident path (csrc/wide_engine.hip) against the bf16
+    emulation oracle (operands rounded to bf16, f32 accumulation): mean / value within 1e-2 of
+    their scale (bf16 rounding of 3 hidden layers' outputs, different summation order), the
+    action exactly fl(fl(eps*std)+mean) of the engine's own mean, log-prob from that action."""
+    shape, n = HUMANOID, 1024
+    obs, act = shape["obs"], shape["act"]
+    eng, ref = _agent_pair(gpu, 3, n, n, obs, act, shape["hidden"], precision="bf16")
+    R.use_bf16_gemms(ref)
+    g = torch.Generator().manual_seed(9)
+    state = torch.randn(n, 1, obs, generator=g)
+    eps = torch.randn(n, act, generator=g)
+    sd = state.reshape(n, -1).contiguous().to(gpu)
+    action, mean = torch.empty(n, act, device=gpu), torch.empty(n, act, device=gpu)
+    logp, value = torch.empty(n, device=gpu), torch.empty(n, device=gpu)
+    eng.engine.policy_step(sd, eps=eps.to(gpu), action=action, logp=logp, value=value, mean=mean)
+    with torch.no_grad():
+        m_ref, s_ref = ref.networks["actor"](state)
+        v_ref = ref.networks["critic"](state)[:, 0]
+    for got, want in ((mean.cpu(), m_ref), (value.cpu(), v_ref)):
+        err = float((got - want).abs().max()) / (float(want.abs().max()) + 1e-12)
+        l2 = float((got - want).norm() / (want.norm() + 1e-20))
+        print(f"bf16 policy step: max err {err:.3e} of scale, rel L2 {l2:.3e}")
+        assert err <= 1e-2 and l2 <= 5e-3
+    std = eng.networks["actor"].actor_logstd.detach().exp().cpu()
+    assert torch.equal(action.cpu(), eps * std + mean.cpu())
+    lp_ref = torch.distributions.Normal(mean.cpu(), std).log_prob(action.cpu()).sum(dim=1)
+    torch.testing.assert_close(logp.cpu(), lp_ref, rtol=1e-6, atol=1e-5)

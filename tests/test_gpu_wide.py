@@ -1,0 +1,143 @@
+"""GPU parity of the wide-path bf16 GEMMs (csrc/wide_gemm.h) against a float64 CPU product of the
+same bf16 operands.
+
+The wide path computes the layered MLP's products (network_block_creator.py:74-86 forward,
+ppo.py:109-135 backward) on bf16 operands with f32 accumulation; its outputs are bf16 (FWD, DGRAD)
+or f32 (F32, WGRAD slabs).  Bar: |got - ref| <= 2^-8 |ref| (one bf16 rounding of the output, for
+bf16 outputs) + 1e-5 * sum_k |a_k b_k| (f32 accumulation in a different order), elementwise; the
+DGRAD column sums and WGRAD split slabs to 1e-5 of the |.|-sums they add; rows at or past the
+device row count must be written as exact zeros.
+"""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FWD, DGRAD, F32, WGRAD = 0, 1, 2, 3
+
+
+def _gemm(kind, m, n, k, a, b, c, bias=None, aux=None, colsum=None, act=0, splits=1, count=None):
+    from mujoco_reinforcement_learning_amd import _lib
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+    _lib.check(lib.ppo_wide_gemm(kind, m, n, k, p(a), a.shape[-1], p(b), b.shape[-1], p(c),
+                                 c.shape[-1], p(bias), p(aux), p(colsum), act, splits, p(count),
+                                 st))
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _pad_rows(x, mult):
+    r = (x.shape[0] + mult - 1) // mult * mult
+    out = torch.zeros(r, x.shape[1], dtype=x.dtype)
+    out[: x.shape[0]] = x
+    return out
+
+
+@pytest.mark.parametrize("m,n,k,act", [(65536, 512, 512, 0), (1024, 512, 384, 0),
+                                       (640, 256, 64, 1), (4096, 512, 512, 0)])
+def test_wide_fwd(gpu, m, n, k, act):
+    g = torch.Generator().manual_seed(m + n + k)
+    a = _bf(torch.randn(m, k, generator=g))
+    w = _bf(torch.randn(n, k, generator=g) / k ** 0.5)
+    bias = torch.randn(n, generator=g) * 0.1
+    count = m - 37 if m > 1024 else m
+    ad = _pad_rows(a, 128).to(gpu)
+    c = torch.full((ad.shape[0], n), float("nan"), dtype=torch.bfloat16, device=gpu)
+    cnt = torch.tensor([count], dtype=torch.int32, device=gpu)
+    _gemm(FWD, m, n, k, ad, w.to(gpu), c, bias=bias.to(gpu), act=act, count=cnt)
+    torch.cuda.synchronize()
+    a64, w64 = a.double(), w.double()
+    z = a64 @ w64.t() + bias.double()
+    ref = torch.relu(z) if act == 0 else torch.tanh(z)
+    scale = a64.abs() @ w64.abs().t()
+    got = c[:m].float().cpu().double()
+    err = (got[:count] - ref[:count]).abs()
+    tol = 2.0 ** -8 * ref[:count].abs() + 1e-5 * scale[:count] + 1e-30
+    assert bool((err <= tol).all()), f"FWD max err {err.max():.3e}"
+    assert bool((got[count:] == 0).all()), "rows past the count must be zero"
+
+
+@pytest.mark.parametrize("m,n,k", [(65536, 512, 512), (1024, 384, 512), (4096, 512, 64)])
+def test_wide_dgrad(gpu, m, n, k):
+    g = torch.Generator().manual_seed(3 * m + n + k)
+    dy = _bf(torch.randn(m, k, generator=g))
+    wt = _bf(torch.randn(n, k, generator=g) / k ** 0.5)  # W^T image [in][out]
+    y = _bf(torch.relu(torch.randn(m, n, generator=g)))    # layer output (ReLU)
+    count = m - 100
+    tile = 64 if m <= 4096 else 128
+    tiles = (m + tile - 1) // tile
+    yd = _pad_rows(y, 128).to(gpu)
+    c = yd.clone()  # in place over the activations
+    colsum = torch.full((tiles, n), float("nan"), device=gpu)
+    cnt = torch.tensor([count], dtype=torch.int32, device=gpu)
+    _gemm(DGRAD, m, n, k, _pad_rows(dy, 128).to(gpu), wt.to(gpu), c, aux=yd, colsum=colsum,
+          act=0, count=cnt)
+    torch.cuda.synchronize()
+    d64 = (dy.double() @ wt.double().t()) * (y.double() > 0)
+    scale = dy.double().abs() @ wt.double().abs().t()
+    got = c[:m].float().cpu().double()
+    err = (got[:count] - d64[:count]).abs()
+    tol = 2.0 ** -8 * d64[:count].abs() + 1e-5 * scale[:count] + 1e-30
+    assert bool((err <= tol).all()), f"DGRAD max err {err.max():.3e}"
+    assert bool((got[count:] == 0).all())
+    cs = colsum.cpu().double()
+    assert not torch.isnan(cs).any()
+    ref_cs = d64[:count].sum(0)
+    assert torch.allclose(cs.sum(0), ref_cs, rtol=0, atol=1e-5 * float(scale[:count].sum(0).max()) + 1e-6)
+    # bitwise reproducible
+    c2 = yd.clone()
+    colsum2 = torch.empty_like(colsum)
+    _gemm(DGRAD, m, n, k, _pad_rows(dy, 128).to(gpu), wt.to(gpu), c2, aux=yd, colsum=colsum2,
+          act=0, count=cnt)
+    torch.cuda.synchronize()
+    assert torch.equal(c, c2) and torch.equal(colsum, colsum2)
+
+
+@pytest.mark.parametrize("m,n,k", [(65536, 32, 512), (1024, 32, 512)])
+def test_wide_f32(gpu, m, n, k):
+    g = torch.Generator().manual_seed(m + 5)
+    a = _bf(torch.randn(m, k, generator=g))
+    w = torch.zeros(n, k, dtype=torch.bfloat16)
+    w[:17] = _bf(torch.randn(17, k, generator=g) / k ** 0.5)
+    c = torch.empty(((m + 127) // 128) * 128, n, device=gpu)
+    _gemm(F32, m, n, k, _pad_rows(a, 128).to(gpu), w.to(gpu), c)
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().t()
+    scale = a.double().abs() @ w.double().abs().t()
+    err = (c[:m].cpu().double() - ref).abs()
+    assert bool((err <= 1e-5 * scale + 1e-30).all()), f"F32 max err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("m,n,rows,splits", [(512, 512, 65536, 16), (512, 376, 65536, 16),
+                                             (32, 512, 65536, 64), (512, 512, 1000, 4),
+                                             (17, 384, 4096, 8)])
+def test_wide_wgrad(gpu, m, n, rows, splits):
+    g = torch.Generator().manual_seed(m * 7 + n + rows)
+    ld_a = (m + 7) // 8 * 8
+    ld_a = max(ld_a, 32 if m <= 32 else 128)
+    ld_b = max((n + 7) // 8 * 8, 128 * ((n + 127) // 128))
+    dy = torch.zeros(rows, ld_a, dtype=torch.bfloat16)
+    dy[:, :m] = _bf(torch.randn(rows, m, generator=g))
+    x = torch.zeros(rows, ld_b, dtype=torch.bfloat16)
+    x[:, :n] = _bf(torch.randn(rows, n, generator=g))
+    count = rows - 3
+    dyd = _pad_rows(dy, 128)
+    dyd[count:] = 0  # the contract: rows past the count are zero
+    xd = _pad_rows(x, 128)
+    xd[count:] = 0
+    slab = torch.full((splits, m, n), float("nan"), device=gpu)
+    cnt = torch.tensor([count], dtype=torch.int32, device=gpu)
+    _gemm(WGRAD, m, n, rows, dyd.to(gpu), xd.to(gpu), slab, splits=splits, count=cnt)
+    torch.cuda.synchronize()
+    ref = dy[:count, :m].double().t() @ x[:count, :n].double()
+    scale = dy[:count, :m].double().abs().t() @ x[:count, :n].double().abs()
+    got = slab.cpu().double()
+    assert not torch.isnan(got).any()
+    err = (got.sum(0) - ref).abs()
+    assert bool((err <= 1e-5 * scale + 1e-30).all()), f"WGRAD max err {err.max():.3e}"

@@ -10,6 +10,7 @@
 #   traffic   FETCH_SIZE / WRITE_SIZE PMC passes over the bench -> traffic per launch
 #   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
 #   phases    fused-update phase stamps (tools/fused_phases.py)
+#   wbench    tools/wide_bench.py: the wide-path bf16 GEMMs at Humanoid shapes vs torch's matmul
 #   micro     tools/micro_fused.py timing of the fused update kernel alone
 #   fold      the bench line with PPO_FUSED_FOLD=1 (in-launch slab fold) -> bench_${TAG}_fold.json
 #   cnn       bench.py --model cnn (pixel cheetah-run) -> bench_${TAG}_cnn.json
@@ -120,6 +121,9 @@ for S in $STEPS; do
         --steps 3 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
         2> gpurun_out/bench_${TAG}_hum.err || fail hum gpurun_out/bench_${TAG}_hum.err
       cat gpurun_out/bench_${TAG}_hum.json ;;
+    wbench)
+      timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
+      cat gpurun_out/wbench_${TAG}.txt ;;
     micro)
       timeout -k 10 200 python tools/micro_fused.py 20 > gpurun_out/micro_${TAG}.txt 2>&1 || fail micro gpurun_out/micro_${TAG}.txt
       cat gpurun_out/micro_${TAG}.txt ;;
