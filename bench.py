@@ -388,7 +388,13 @@ def main():
         ec.rollout_graph, ec.train_graph = saved
 
     value = world * n * t * args.steps / elapsed
-    line = {"metric": METRICS[args.model], "value": value, "unit": "env-steps/s", "n_gpus": world,
+    metric = METRICS[args.model]
+    if args.model == "mlp" and (args.obs_dim, args.act_dim, hidden, n) != (17, 6, (256, 256), 4096):
+        # a non-headline MLP config (e.g. BASELINE configs[2] Ant, configs[3]'s Humanoid shard):
+        # its own metric string, never the HalfCheetah headline's
+        metric = (f"env-steps/sec {_ENV_NAMES.get((args.obs_dim, args.act_dim), 'custom')} "
+                  f"{n} envs/GPU, {'x'.join(map(str, hidden))} MLP, {world}x MI355X")
+    line = {"metric": metric, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",

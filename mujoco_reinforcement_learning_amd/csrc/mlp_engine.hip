@@ -1473,6 +1473,15 @@ extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs
                 "ppo_observe_act: bounds must be ascending within [0, O]");
     tab.edge[i] = bounds[i];
   }
+  if (!fused_active(ctx) && wide_active(ctx) && wide_observe_ok(ctx)) {
+    // wide path: window push + standardisation + bf16 operand rows in one launch, then the GEMMs
+    TimingScope timing_scope(ctx);
+    if (int rc = wide_observe(ctx, window_d, obs_d, reset_d, all_reset, tab, normalize, state_d, n,
+                              as_stream(stream)))
+      return rc;
+    return wide_policy_step(ctx, state_d, n, eps_d, seed, offset, action_d, logp_d, value_d,
+                            mean_d, false, as_stream(stream), true);
+  }
   if (!fused_active(ctx) || w > kPolicyMaxWindow) {  // layered: A1 kernels, then GEMM policy step
     if (obs_d) {
       int rc = ppo_obs_window_push(window_d, obs_d, 1, reset_d, all_reset, n, o, w, stream);

@@ -158,15 +158,18 @@ void wide_free(ppo_ctx *ctx) {
 }
 
 // ============================================================================================
-// Weight images: dst[r][c] = bf16(W[r][c]) (or W^T), zero outside the tensor; 8 elements per
-// thread, one 16-B store.
+// Weight images: dst[r][c] = bf16(W[r][c]) (or W^T), zero outside the tensor.  One 64 x 64 tile
+// of one image per block: the f32 master tile is read row-coalesced (64 consecutive `in` columns
+// per wave row) into LDS, then every thread writes 8 consecutive image columns as one 16-B store,
+// so the transposed images are written from the same coalesced reads as the plain ones.
 // ============================================================================================
 constexpr int kMaxImages = 2 * 2 * (PPO_MAX_LAYERS + 1);
+constexpr int kPackT = 64;
 struct ImageDesc {
   const float *w;   // [out][in] f32 master
   __bf16 *dst;
   int out, in;      // tensor shape
-  int rows, cols;   // image shape (cols % 8 == 0)
+  int rows, cols;   // image shape (multiples of 64)
   int transposed;   // dst = W^T
   int blocks;       // first block of this image (prefix over images)
 };
@@ -176,22 +179,35 @@ struct PackArgs {
 };
 
 __global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q) {
+  __shared__ float tile[kPackT][kPackT + 1];
   int i = 0;
   while (i + 1 < q.n && q.img[i + 1].blocks <= static_cast<int>(blockIdx.x)) ++i;
   const ImageDesc d = q.img[i];
-  const int64_t e = (static_cast<int64_t>(blockIdx.x - d.blocks) * 256 + threadIdx.x) * 8;
-  if (e >= static_cast<int64_t>(d.rows) * d.cols) return;
-  const int r = static_cast<int>(e / d.cols), c0 = static_cast<int>(e % d.cols);
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    const int o = d.transposed ? c : r, in = d.transposed ? r : c;
-    v[j] = (o < d.out && in < d.in) ? d.w[static_cast<int64_t>(o) * d.in + in] : 0.f;
+  const int t = static_cast<int>(blockIdx.x) - d.blocks;
+  const int tiles_c = d.cols / kPackT;
+  const int r0 = (t / tiles_c) * kPackT, c0 = (t % tiles_c) * kPackT;  // image tile origin
+  // master tile: rows o0.. (out), columns i0.. (in); image (r, c) = master (r, c) or (c, r)
+  const int o0 = d.transposed ? c0 : r0, i0 = d.transposed ? r0 : c0;
+  const int tid = threadIdx.x, li = tid & 63;
+#pragma unroll 4
+  for (int k = 0; k < kPackT / 4; ++k) {
+    const int lo = 4 * k + (tid >> 6);
+    const int o = o0 + lo, in = i0 + li;
+    const bool ok = o < d.out && in < d.in;
+    // clamped address, masked value: no load behind a branch
+    const float v = d.w[static_cast<int64_t>(ok ? o : 0) * d.in + (ok ? in : 0)];
+    if (d.transposed) tile[li][lo] = ok ? v : 0.f;  // tile[image row][image col]
+    else tile[lo][li] = ok ? v : 0.f;
   }
-  *reinterpret_cast<uint4 *>(d.dst + e) =
-      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
-                 wide::pack2(v[6], v[7]));
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int item = k * 256 + tid, lr = item >> 3, cg = item & 7;
+    const float *s = &tile[lr][8 * cg];
+    *reinterpret_cast<uint4 *>(d.dst + static_cast<int64_t>(r0 + lr) * d.cols + c0 + 8 * cg) =
+        make_uint4(wide::pack2(s[0], s[1]), wide::pack2(s[2], s[3]), wide::pack2(s[4], s[5]),
+                   wide::pack2(s[6], s[7]));
+  }
 }
 
 int wide_pack(ppo_ctx *ctx, hipStream_t st) {
@@ -214,7 +230,7 @@ int wide_pack(ppo_ctx *ctx, hipStream_t st) {
         d.rows = static_cast<int>(t ? rup(L.in, 128) : rup(L.out, 128));
         d.cols = t ? wn.ldwt[l] : wn.ldw[l];
         d.blocks = blocks;
-        blocks += ceil_div(static_cast<int64_t>(d.rows) * d.cols, 256 * 8);
+        blocks += (d.rows / kPackT) * (d.cols / kPackT);
         elems += static_cast<double>(d.out) * d.in;
       }
     }
@@ -239,12 +255,24 @@ __global__ __launch_bounds__(256) void wide_gather_kernel(const float *__restric
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= static_cast<int64_t>(rows_pad) * per_row) return;
   const int j = static_cast<int>(i / per_row), c0 = static_cast<int>(i % per_row) * 8;
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (j < count) {
-    const float *src = states + static_cast<int64_t>(rows ? rows[j] : j) * din;
+  const bool live = j < count;
+  const int64_t sr = rows ? rows[live ? j : 0] : j;
+  const float *src = states + (live ? sr : 0) * din;
+  float v[8];
+  if ((din & 3) == 0 && (reinterpret_cast<uintptr_t>(states) & 15) == 0) {
+    // two 16-B loads from clamped addresses (din % 4 == 0: a 4-group is wholly in or out)
+    const bool in0 = live && c0 < din, in1 = live && c0 + 4 < din;
+    const float4 x0 = *reinterpret_cast<const float4 *>(src + (in0 ? c0 : 0));
+    const float4 x1 = *reinterpret_cast<const float4 *>(src + (in1 ? c0 + 4 : 0));
+    v[0] = in0 ? x0.x : 0.f, v[1] = in0 ? x0.y : 0.f, v[2] = in0 ? x0.z : 0.f, v[3] = in0 ? x0.w : 0.f;
+    v[4] = in1 ? x1.x : 0.f, v[5] = in1 ? x1.y : 0.f, v[6] = in1 ? x1.z : 0.f, v[7] = in1 ? x1.w : 0.f;
+  } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (c0 + e < din) v[e] = src[c0 + e];
+    for (int e = 0; e < 8; ++e) {
+      const bool in = live && c0 + e < din;
+      const float u = src[in ? c0 + e : 0];
+      v[e] = in ? u : 0.f;
+    }
   }
   *reinterpret_cast<uint4 *>(x + static_cast<int64_t>(j) * ldx + c0) =
       make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
@@ -367,16 +395,161 @@ __global__ __launch_bounds__(256) void wide_policy_head_kernel(WidePolicyArgs q)
   }
 }
 
+// ============================================================================================
+// Rollout observation step of the wide path, one launch (A1): the window push (helper.py:51-64,
+// running_gym_sequential_vectorized.py:53-58), the per-(slot, slice) f64 standardisation
+// (running_gym_sequential_vectorized.py:61-92) and the bf16 GEMM operand row x[env] -- three
+// launches (ppo_obs_window_push, ppo_obs_normalize, the row staging) before.  One wave per env:
+// every global load of the row (new observation, kept window slots) is issued up front from
+// clamped addresses; the row is then standardised from an LDS copy in obs_normalize_wide_kernel's
+// exact summation order (lane-strided partials over the slice, fixed xor tree), so the state is
+// bitwise that kernel's.  Waves of rows in [n, rows_pad) write the zero operand rows of the
+// padding contract (wide_gemm.h).
+// ============================================================================================
+constexpr int kObsMaxK = 8;  // W*O <= 64 * kObsMaxK elements per row
+struct WideObserveArgs {
+  double *window;        // (N, O, W) f64, updated in place when obs != null
+  const double *obs;     // (N, O) f64 new observations, nullable (no push)
+  const uint8_t *reset;  // nullable
+  int all_reset;
+  int n, rows_pad, o, w;
+  PolicySlices tab;
+  int normalize;
+  float *state;          // (N, W*O) f32
+  __bf16 *x;             // [rows_pad][ldx] bf16
+  int ldx;
+};
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void wide_observe_kernel(WideObserveArgs q) {
+  __shared__ double rowbuf[4][64 * kObsMaxK];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int env = blockIdx.x * 4 + wv;  // wave-uniform
+  if (env >= q.rows_pad) return;
+  const int o = q.o, w = q.w, ow = o * w;
+  if (env >= q.n) {  // padding row: zero operand
+    for (int c = 8 * lane; c < q.ldx; c += 512)
+      *reinterpret_cast<uint4 *>(q.x + static_cast<int64_t>(env) * q.ldx + c) = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  double *win = rowbuf[wv];
+  double *const grow = q.window + static_cast<int64_t>(env) * ow;
+  // ---- every load of the row first: kept slots (element e + 1 of the old row) and the obs ----
+  double old[kObsMaxK], ob[kObsMaxK];
+  const bool push = q.obs != nullptr;
+  const bool full = q.all_reset || (q.reset && q.reset[env]);
+#pragma unroll
+  for (int k = 0; k < kObsMaxK; ++k) {
+    const int e = lane + 64 * k;            // element (f = e / w, slot = e % w)
+    const int f = e / w, slot = e - f * w;
+    const bool in = e < ow;
+    const bool keep = in && !(push && (full || slot == w - 1));
+    old[k] = grow[keep ? (push ? e + 1 : e) : 0];
+    ob[k] = push ? q.obs[static_cast<int64_t>(env) * o + (in ? f : 0)] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kObsMaxK; ++k) {
+    const int e = lane + 64 * k;
+    if (e < ow) {
+      const int f = e / w, slot = e - f * w;
+      const bool take_obs = push && (full || slot == w - 1);
+      const double v = take_obs ? ob[k] : old[k];
+      win[e] = v;
+      if (push) grow[e] = v;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS row is complete
+  __builtin_amdgcn_wave_barrier();
+  float *const srow = q.state + static_cast<int64_t>(env) * ow;
+  __bf16 *const xrow = q.x + static_cast<int64_t>(env) * q.ldx;
+  // state (N, W, O): slot-major; x is the same row as bf16, zero past W*O
+  for (int slot = 0; slot < w; ++slot) {
+    const double *src = win + slot;  // feature f at f * w
+    float *dst = srow + static_cast<int64_t>(slot) * o;
+    __bf16 *xd = xrow + slot * o;
+    if (!q.normalize) {
+      for (int f = lane; f < o; f += 64) {
+        const float v = static_cast<float>(src[f * w]);
+        dst[f] = v;
+        xd[f] = static_cast<__bf16>(v);
+      }
+      continue;
+    }
+    for (int sl = 0; sl < q.tab.count; ++sl) {
+      const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
+      const int cnt = hi - lo;
+      if (cnt <= 0) continue;
+      double sum = 0.0;
+      for (int f = lo + lane; f < hi; f += 64) sum += src[f * w];
+      const double mean = wave_sum64(sum) / cnt;
+      double csum = 0.0;
+      for (int f = lo + lane; f < hi; f += 64) csum += src[f * w] - mean;
+      const double cmean = wave_sum64(csum) / cnt;
+      double ss = 0.0;
+      for (int f = lo + lane; f < hi; f += 64) {
+        const double d = (src[f * w] - mean) - cmean;
+        ss += d * d;
+      }
+      double sd = sqrt(wave_sum64(ss) / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
+      if (sd == 0.0) sd = 1.0;
+      for (int f = lo + lane; f < hi; f += 64) {
+        const float v = static_cast<float>((src[f * w] - mean) / sd);
+        dst[f] = v;
+        xd[f] = static_cast<__bf16>(v);
+      }
+    }
+  }
+  for (int c = ow + lane; c < q.ldx; c += 64) xrow[c] = static_cast<__bf16>(0.f);
+}
+
+int wide_observe(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint8_t *reset_d,
+                 int all_reset, const PolicySlices &tab, int normalize, float *state_d, int n,
+                 hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  const int o = ctx->cfg.obs_dim, w = ctx->cfg.window;
+  PPO_REQUIRE(o * w <= 64 * kObsMaxK, "wide_observe: W*O = %d exceeds %d", o * w, 64 * kObsMaxK);
+  WideObserveArgs q{};
+  q.window = window_d;
+  q.obs = obs_d;
+  q.reset = reset_d;
+  q.all_reset = all_reset;
+  q.n = n;
+  q.rows_pad = static_cast<int>(rup(n, 64));
+  q.o = o;
+  q.w = w;
+  q.tab = tab;
+  q.normalize = normalize;
+  q.state = state_d;
+  q.x = W.x;
+  q.ldx = W.ldx;
+  const double by = static_cast<double>(n) * o * w * (8.0 * (obs_d ? 2 : 1) + 4.0 + 2.0) +
+                    (obs_d ? 8.0 * n * o : 0.0);
+  launch_k(TimRec{KC_OBS, "wide_observe_kernel", 0.0, by}, wide_observe_kernel,
+           dim3(ceil_div(q.rows_pad, 4)), dim3(256), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+bool wide_observe_ok(const ppo_ctx *ctx) {
+  return ctx->cfg.obs_dim * ctx->cfg.window <= 64 * kObsMaxK;
+}
+
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                      uint64_t offset, float *action_d, float *logp_d, float *value_d,
-                     float *mean_d, bool pack, hipStream_t st) {
+                     float *mean_d, bool pack, hipStream_t st, bool staged) {
   WideWork &W = *ctx->wide;
   const bool use[2] = {action_d || logp_d || mean_d, value_d != nullptr};
   if (!use[0] && !use[1]) return 0;
   const int rows_pad = static_cast<int>(rup(n, 64));
   if (pack)
     if (int rc = wide_pack(ctx, st)) return rc;
-  if (int rc = stage_rows(ctx, state_d, nullptr, nullptr, n, rows_pad, st)) return rc;
+  if (!staged)  // (wide_observe wrote x already)
+    if (int rc = stage_rows(ctx, state_d, nullptr, nullptr, n, rows_pad, st)) return rc;
   if (int rc = forward(ctx, use, rows_pad, nullptr, st)) return rc;
   const NetDesc &A = ctx->net[0], &C = ctx->net[1];
   WidePolicyArgs q{};

@@ -129,7 +129,8 @@ struct ColImage {
   static constexpr int NINST = BYTES / 1024;
   static constexpr int CHUNKS = R / 8;          // 16-B chunks per k-row
   static constexpr int ROWS_PER_INST = 1024 / (2 * R);
-  static_assert(R == 32 || R == 64 || R == 128, "TT tile width");
+  // R = 256 rows are 512 B: the same bank pattern mod 256 B as R = 128, so the same swizzle
+  static_assert(R == 32 || R == 64 || R == 128 || R == 256, "TT tile width");
   __device__ __forceinline__ static void fill(__bf16 *img, const __bf16 *src, int64_t ld, int k0,
                                               int wid, int lane) {
 #pragma unroll
@@ -165,6 +166,12 @@ __device__ __forceinline__ void xcd_map(int b, int tiles, int &id) {
   id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// LDS-DMA wave-instructions of one operand image (instantiates only the image kind in use)
+template <bool TT, int R, int NW>
+struct ImageInst { static constexpr int v = RowImage<R, NW>::NINST; };
+template <int R, int NW>
+struct ImageInst<true, R, NW> { static constexpr int v = ColImage<R, NW>::NINST; };
+
 template <int TM, int TN, int WM, int WN, int KIND, int NS>
 struct WideCfg {
   static constexpr int NW = WM * WN;
@@ -175,14 +182,20 @@ struct WideCfg {
   static constexpr int IMG_A = BM * kBK * 2, IMG_B = BN * kBK * 2;
   static constexpr int STAGE = IMG_A + IMG_B;
   static constexpr int SC = BN + 4;  // f32 epilogue tile row stride (floats)
-  static constexpr int EPI = BM * SC * 4;
+  // the f32 epilogue tile is staged one wave-row band at a time when the whole tile would not fit
+  // in LDS (256 x 256 tiles: two 128-row halves of 133 KB)
+  static constexpr int EH = BM * SC * 4 > 160 * 1024 ? WM : 1;
+  static constexpr int ER = BM / EH;  // rows per epilogue band
+  static constexpr int EPI = ER * SC * 4;
   static constexpr int LDS = (NS * STAGE > EPI ? NS * STAGE : EPI);
   // LDS-DMA wave-instructions per wave per k-tile (equal for every wave: counted vmcnt waits)
-  static constexpr int NI_A = TT ? ColImage<BM, NW>::NINST : RowImage<BM, NW>::NINST;
-  static constexpr int NI_B = TT ? ColImage<BN, NW>::NINST : RowImage<BN, NW>::NINST;
+  static constexpr int NI_A = ImageInst<TT, BM, NW>::v;
+  static constexpr int NI_B = ImageInst<TT, BN, NW>::v;
   static_assert(NI_A % NW == 0 && NI_B % NW == 0, "uneven LDS-DMA split over the waves");
   static constexpr int PER = (NI_A + NI_B) / NW;
   static_assert(PER * (NS - 2) < 64, "vmcnt range");
+  static_assert(EH == 1 || !TT, "banded epilogue only for the NT kinds");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
 // s_waitcnt vmcnt(PER * n) for a runtime n in [0, NMAX]: the immediate is an instruction field
@@ -284,13 +297,15 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
     for (int ks = 0; ks < kBK / 16; ++ks) {
       bf16x8 av[TM], bv[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        av[i] = C::TT ? ColImage<BM, NW>::frag(ia, (wm * TM + i) * 32, ks, lane)
-                      : RowImage<BM, NW>::frag(ia, (wm * TM + i) * 32, ks, lane);
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (C::TT) av[i] = ColImage<BM, NW>::frag(ia, (wm * TM + i) * 32, ks, lane);
+        else av[i] = RowImage<BM, NW>::frag(ia, (wm * TM + i) * 32, ks, lane);
+      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bv[j] = C::TT ? ColImage<BN, NW>::frag(ib, (wn * TN + j) * 32, ks, lane)
-                      : RowImage<BN, NW>::frag(ib, (wn * TN + j) * 32, ks, lane);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (C::TT) bv[j] = ColImage<BN, NW>::frag(ib, (wn * TN + j) * 32, ks, lane);
+        else bv[j] = RowImage<BN, NW>::frag(ib, (wn * TN + j) * 32, ks, lane);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -301,21 +316,25 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
   }
   __syncthreads();  // the staging buffers become the epilogue tile
 
-  // ---- accumulators -> f32 LDS tile [BM][SC] --------------------------------------------------
   float *tile = reinterpret_cast<float *>(lds);
+  // accumulators of wave-row band eh -> f32 LDS tile [ER][SC]
+  auto stage_band = [&](int eh) {
+    if (C::EH > 1 && wm != eh) return;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = (wn * TN + j) * 32 + (lane & 31);
-        tile[row * C::SC + col] = acc[i][j][r];
-      }
-  __syncthreads();
+        for (int r = 0; r < 16; ++r) {
+          const int row = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) - eh * C::ER;
+          const int col = (wn * TN + j) * 32 + (lane & 31);
+          tile[row * C::SC + col] = acc[i][j][r];
+        }
+  };
 
   if constexpr (KIND == WK_WGRAD) {
+    stage_band(0);
+    __syncthreads();
     // f32 slab store, 4 columns per item
     constexpr int CG = BN / 4, RSTEP = NT / CG;
     static_assert(NT % CG == 0, "epilogue layout");
@@ -341,6 +360,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
     // 8 columns per item: bf16 16-B stores (FWD / DGRAD) or f32 2 x 16-B stores (F32)
     constexpr int CG = BN / 8, RSTEP = NT / CG;
     static_assert(NT % CG == 0, "epilogue layout");
+    static_assert(KIND != WK_DGRAD || BN <= NT, "one column-sum thread per column");
     const int cg = tid % CG, r0 = tid / CG;
     const int n = n0 + 8 * cg;
     const bool ncol = n < P.n;  // P.n is a multiple of 8 on this path (host-checked)
@@ -353,51 +373,57 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
       bias[0] = b0.x, bias[1] = b0.y, bias[2] = b0.z, bias[3] = b0.w;
       bias[4] = b1.x, bias[5] = b1.y, bias[6] = b1.z, bias[7] = b1.w;
     }
-    for (int r = r0; r < BM; r += RSTEP) {
-      const int m = m0 + r;
-      if (m >= P.m) break;  // never past the allocation's row bound
-      float *t = tile + r * C::SC + 8 * cg;
-      const float4 x0 = *reinterpret_cast<const float4 *>(t);
-      const float4 x1 = *reinterpret_cast<const float4 *>(t + 4);
-      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      const bool live = m < count;
-      if (!ncol) continue;
-      if constexpr (KIND == WK_F32) {
-        float *dst = static_cast<float *>(P.c) + static_cast<int64_t>(m) * P.ldc + n;
-        *reinterpret_cast<float4 *>(dst) =
-            live ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4 *>(dst + 4) =
-            live ? make_float4(v[4], v[5], v[6], v[7]) : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        if constexpr (KIND == WK_FWD) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = live ? act_forward(v[e] + bias[e], wb.act) : 0.f;
-        } else {  // DGRAD: act'(y) with y the bf16 layer output, in place
-          const uint4 y = *reinterpret_cast<const uint4 *>(P.aux + static_cast<int64_t>(m) * P.ldc + n);
-          const float yf[8] = {bf_lo(y.x), bf_hi(y.x), bf_lo(y.y), bf_hi(y.y),
-                               bf_lo(y.z), bf_hi(y.z), bf_lo(y.w), bf_hi(y.w)};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = live ? act_backward(v[e], yf[e], wb.act) : 0.f;
-          if (P.colsum) {  // the bias gradient sums the f32 values (before bf16 rounding)
-            *reinterpret_cast<float4 *>(t) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4 *>(t + 4) = make_float4(v[4], v[5], v[6], v[7]);
-          }
-        }
-        const uint4 o = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]),
-                                   pack2(v[6], v[7]));
-        *reinterpret_cast<uint4 *>(static_cast<__bf16 *>(P.c) + static_cast<int64_t>(m) * P.ldc + n) = o;
-      }
-    }
-    if (KIND == WK_DGRAD && P.colsum) {
+    float csum = 0.f;  // DGRAD: column n0 + tid, summed over the tile's rows in row order
+#pragma unroll 1
+    for (int eh = 0; eh < C::EH; ++eh) {
+      if (eh > 0) __syncthreads();  // the previous band's tile reads are done
+      stage_band(eh);
       __syncthreads();
-      const int rows = min(BM, P.m - m0);
-      for (int c = tid; c < BN; c += NT) {
-        if (n0 + c >= P.n) continue;
-        float s = 0.f;
-        for (int r = 0; r < rows; ++r) s += tile[r * C::SC + c];
-        P.colsum[static_cast<int64_t>(tile_m) * P.n_colsum + n0 + c] = s;
+      const int mb = m0 + eh * C::ER;  // first row of the band
+      for (int r = r0; r < C::ER; r += RSTEP) {
+        const int m = mb + r;
+        if (m >= P.m) break;  // never past the allocation's row bound
+        float *t = tile + r * C::SC + 8 * cg;
+        const float4 x0 = *reinterpret_cast<const float4 *>(t);
+        const float4 x1 = *reinterpret_cast<const float4 *>(t + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const bool live = m < count;
+        if (!ncol) continue;
+        if constexpr (KIND == WK_F32) {
+          float *dst = static_cast<float *>(P.c) + static_cast<int64_t>(m) * P.ldc + n;
+          *reinterpret_cast<float4 *>(dst) =
+              live ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4 *>(dst + 4) =
+              live ? make_float4(v[4], v[5], v[6], v[7]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          if constexpr (KIND == WK_FWD) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = live ? act_forward(v[e] + bias[e], wb.act) : 0.f;
+          } else {  // DGRAD: act'(y) with y the bf16 layer output, in place
+            const uint4 y = *reinterpret_cast<const uint4 *>(P.aux + static_cast<int64_t>(m) * P.ldc + n);
+            const float yf[8] = {bf_lo(y.x), bf_hi(y.x), bf_lo(y.y), bf_hi(y.y),
+                                 bf_lo(y.z), bf_hi(y.z), bf_lo(y.w), bf_hi(y.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = live ? act_backward(v[e], yf[e], wb.act) : 0.f;
+            if (P.colsum) {  // the bias gradient sums the f32 values (before bf16 rounding)
+              *reinterpret_cast<float4 *>(t) = make_float4(v[0], v[1], v[2], v[3]);
+              *reinterpret_cast<float4 *>(t + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+          }
+          const uint4 o = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]),
+                                     pack2(v[6], v[7]));
+          *reinterpret_cast<uint4 *>(static_cast<__bf16 *>(P.c) + static_cast<int64_t>(m) * P.ldc + n) = o;
+        }
+      }
+      if (KIND == WK_DGRAD && P.colsum) {
+        __syncthreads();
+        const int rows = min(C::ER, P.m - mb);
+        if (tid < BN)
+          for (int r = 0; r < rows; ++r) csum += tile[r * C::SC + tid];
       }
     }
+    if (KIND == WK_DGRAD && P.colsum && tid < BN && n0 + tid < P.n)
+      P.colsum[static_cast<int64_t>(tile_m) * P.n_colsum + n0 + tid] = csum;
   }
 }
 

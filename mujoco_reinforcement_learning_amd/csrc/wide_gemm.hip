@@ -48,6 +48,8 @@ static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kf
     switch (f) {
       case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
       case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
+      // 256 x 128 tiles, 8 waves of 64 x 64, 3 stages (144 KB)
+      case 6: return launch_cfg<2, 2, 4, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
       default: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
     }
   }
@@ -57,6 +59,12 @@ static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kf
     if (f == 5) return launch_cfg<1, 1, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
     return launch_cfg<1, 1, 2, 2, KIND, 8>(wb, nprob, max_m, max_n, kflops, st);
   }
+  // minibatch-sized rows: 256 x 256 tiles, 8 waves of 128 x 64 (2 waves per SIMD), double-buffered
+  // LDS (128 KB) -- twice the MFMA work per byte staged of the 128 x 128 tile, whose operand
+  // stream co-limits at the per-CU L2 rate; PPO_WIDE_CFG=3 keeps the 128 x 128 tile for A/B
+  if constexpr (KIND != WK_WGRAD)
+    if (max_n >= 256 && f != 1 && f != 2 && f != 3)
+      return launch_cfg<4, 2, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
   switch (f) {
     case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
     case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
@@ -79,7 +87,10 @@ int run(int kind, const WideBatch &wb, int nprob, int max_m, int max_n, int kflo
 
 int row_tile(int kind, int max_m, int max_n) {
   if (kind == WK_F32 || (kind == WK_FWD && max_n <= 32)) return 128;
-  return max_m <= 4096 ? 64 : 128;
+  if (max_m <= 4096) return 64;
+  const char *force = getenv("PPO_WIDE_CFG");
+  const int f = force ? atoi(force) : -1;
+  return (max_n >= 256 && f != 1 && f != 2 && f != 3) ? 256 : 128;
 }
 
 }  // namespace wide

@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "ctx.h"
+#include "fused_policy.h"
 
 namespace ppo {
 
@@ -49,7 +50,13 @@ void wide_free(ppo_ctx *ctx);
 int wide_pack(ppo_ctx *ctx, hipStream_t st);
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                      uint64_t offset, float *action_d, float *logp_d, float *value_d,
-                     float *mean_d, bool pack, hipStream_t st);  // pack: refresh the images first
+                     float *mean_d, bool pack, hipStream_t st,
+                     bool staged = false);  // pack: refresh the images first; staged: x holds the rows
+// rollout observation step in one launch: window push + standardisation + the bf16 operand rows
+bool wide_observe_ok(const ppo_ctx *ctx);
+int wide_observe(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint8_t *reset_d,
+                 int all_reset, const PolicySlices &tab, int normalize, float *state_d, int n,
+                 hipStream_t st);
 int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                         const float *old_logp_d, const float *adv_d, const float *vtarget_d,
                         const int32_t *rows_d, int b, const int32_t *count_d, float clip_lo,

@@ -175,23 +175,25 @@ def _python_pipelined(cls):
     return _Py
 
 
-@pytest.mark.parametrize("prec,hidden,path,rng", [("f32", (64, 64), "native", "philox"),
-                                                  ("bf16", (256, 256), "native", "philox"),
-                                                  ("f32", (64, 64), "python", "torch"),
-                                                  ("bf16", (256, 256), "python", "philox")])
-def test_host_physics_pool_matches_device_env(gpu, prec, hidden, path, rng):
-    """HostPhysicsVecEnvHelper (P=2 worker processes, page-locked shared memory) drives two PPO
+@pytest.mark.parametrize("prec,hidden,path,rng,n,workers", [
+    ("f32", (64, 64), "native", "philox", 96, 2),
+    ("bf16", (256, 256), "native", "philox", 96, 2),
+    ("f32", (64, 64), "python", "torch", 96, 2),
+    ("bf16", (256, 256), "python", "philox", 96, 2),
+    ("bf16", (256, 256), "native", "philox", 4096, 8)])   # the bench leg's pool (N=4096, P=8)
+def test_host_physics_pool_matches_device_env(gpu, prec, hidden, path, rng, n, workers):
+    """HostPhysicsVecEnvHelper (P worker processes, page-locked shared memory) drives two PPO
     iterations to the same rollout buffers, losses and parameters, bit for bit, as the
     device-resident synthetic env on the same streams -- through the native driver
     (ppo_host_rollout) and through the Python pipelined protocol, with host (torch) and device
-    (Philox) noise."""
+    (Philox) noise; at the bench leg's size (4096 envs, 8 workers) too."""
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
     from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
     from mujoco_reinforcement_learning_amd.environments import (HostPhysicsVecEnvHelper,
                                                                 SyntheticVecEnvHelper,
                                                                 make_synthetic_streams)
     from mujoco_reinforcement_learning_amd.runconfig import make_run
-    n, t, b = 96, 16, 512
+    t, b = 16, (512 if n < 4096 else 16384)
     streams = make_synthetic_streams(n, t, 17, seed=9, p_terminate=0.05)
     host_cls = HostPhysicsVecEnvHelper if path == "native" else _python_pipelined(
         HostPhysicsVecEnvHelper)
@@ -201,7 +203,7 @@ def test_host_physics_pool_matches_device_env(gpu, prec, hidden, path, rng):
                        seed=2, precision=prec)
         torch.manual_seed(2)
         agent = PPOEngineAgent(run, device=gpu)
-        kw = {"workers": 2} if cls is host_cls else {}
+        kw = {"workers": workers} if cls is host_cls else {}
         helper = cls(streams, run, device=gpu, **kw)
         algo = PPOEngine(helper, agent, log=lambda m: None)
         snaps = []

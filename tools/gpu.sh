@@ -17,6 +17,7 @@
 #   cnntrace  rocprofv3 --kernel-trace --stats over the CNN bench
 #   dp2       2-rank data-parallel rehearsal on the one GPU (gloo) -> bench_${TAG}_dp2.json
 #   hum       Humanoid configs[3] shard (1024 envs, O=376, A=17, 3x512) -> bench_${TAG}_hum.json
+#   humtrace  rocprofv3 --kernel-trace --stats over the Humanoid shard bench (graph replay, no events)
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1; fold off and on)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
@@ -121,6 +122,12 @@ for S in $STEPS; do
         --steps 3 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
         2> gpurun_out/bench_${TAG}_hum.err || fail hum gpurun_out/bench_${TAG}_hum.err
       cat gpurun_out/bench_${TAG}_hum.json ;;
+    humtrace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_${TAG}_hum -o hum --output-format csv \
+        -- python3 bench.py --num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 \
+        --steps 2 --warmup 1 --no-legs --no-cpu-baseline --no-timing > gpurun_out/rp_${TAG}_hum.json \
+        2> gpurun_out/rp_${TAG}_hum.log || fail humtrace gpurun_out/rp_${TAG}_hum.log
+      head -25 $(find gpurun_out/rp_${TAG}_hum -name "*kernel_stats.csv") | cut -c1-160 ;;
     wbench)
       timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
       cat gpurun_out/wbench_${TAG}.txt ;;
