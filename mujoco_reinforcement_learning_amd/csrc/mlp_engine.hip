@@ -1473,7 +1473,7 @@ extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs
                 "ppo_observe_act: bounds must be ascending within [0, O]");
     tab.edge[i] = bounds[i];
   }
-  if (!fused_active(ctx) && wide_active(ctx) && wide_observe_ok(ctx)) {
+  if (!fused_active(ctx) && wide_active(ctx) && wide_observe_ok(ctx, tab.count)) {
     // wide path: window push + standardisation + bf16 operand rows in one launch, then the GEMMs
     TimingScope timing_scope(ctx);
     if (int rc = wide_observe(ctx, window_d, obs_d, reset_d, all_reset, tab, normalize, state_d, n,

@@ -385,8 +385,14 @@ __global__ __launch_bounds__(256) void wide_policy_head_kernel(WidePolicyArgs q)
       const float var = sd * sd;
       lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
     }
+    // the row's log-prob in action order (policy_head_kernel's sequential sum); a fixed trip
+    // count so the 32 cross-lane reads issue back to back instead of one round trip per action
     float s = 0.f;
-    for (int k = 0; k < q.act_dim; ++k) s += __shfl(lp, (lane & 32) + k, 64);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float v = __shfl(lp, (lane & 32) + k, 64);
+      if (k < q.act_dim) s += v;
+    }
     if (row_ok && a == 0 && q.logp) q.logp[j] = s;
   }
   if (row_ok && a == 0 && q.zc && q.value) {
@@ -406,7 +412,8 @@ __global__ __launch_bounds__(256) void wide_policy_head_kernel(WidePolicyArgs q)
 // bitwise that kernel's.  Waves of rows in [n, rows_pad) write the zero operand rows of the
 // padding contract (wide_gemm.h).
 // ============================================================================================
-constexpr int kObsMaxK = 8;  // W*O <= 64 * kObsMaxK elements per row
+constexpr int kObsMaxK = 8;       // W*O <= 64 * kObsMaxK elements per row
+constexpr int kObsMaxSlices = 8;  // standardisation slices (Humanoid-v4: 6)
 struct WideObserveArgs {
   double *window;        // (N, O, W) f64, updated in place when obs != null
   const double *obs;     // (N, O) f64 new observations, nullable (no push)
@@ -480,25 +487,48 @@ __global__ __launch_bounds__(256) void wide_observe_kernel(WideObserveArgs q) {
       }
       continue;
     }
-    for (int sl = 0; sl < q.tab.count; ++sl) {
-      const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
-      const int cnt = hi - lo;
-      if (cnt <= 0) continue;
-      double sum = 0.0;
-      for (int f = lo + lane; f < hi; f += 64) sum += src[f * w];
-      const double mean = wave_sum64(sum) / cnt;
-      double csum = 0.0;
-      for (int f = lo + lane; f < hi; f += 64) csum += src[f * w] - mean;
-      const double cmean = wave_sum64(csum) / cnt;
-      double ss = 0.0;
-      for (int f = lo + lane; f < hi; f += 64) {
-        const double d = (src[f * w] - mean) - cmean;
-        ss += d * d;
-      }
-      double sd = sqrt(wave_sum64(ss) / (cnt - 1));  // cnt == 1 -> NaN, as torch.std
-      if (sd == 0.0) sd = 1.0;
-      for (int f = lo + lane; f < hi; f += 64) {
-        const float v = static_cast<float>((src[f * w] - mean) / sd);
+    // the slices' statistics side by side: each pass's partials for every slice, then their
+    // xor trees interleaved (independent shuffle chains) -- per slice the same operations in the
+    // same order as obs_normalize_wide_kernel, so bitwise its state
+    double mean[kObsMaxSlices], cmean[kObsMaxSlices], sd[kObsMaxSlices], acc[kObsMaxSlices];
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl) {
+      acc[sl] = 0.0;
+      if (sl < q.tab.count)
+        for (int f = q.tab.edge[sl] + lane; f < q.tab.edge[sl + 1]; f += 64) acc[sl] += src[f * w];
+    }
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl)
+      mean[sl] = wave_sum64(acc[sl]) / (q.tab.edge[sl + 1] - q.tab.edge[sl]);
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl) {
+      acc[sl] = 0.0;
+      if (sl < q.tab.count)
+        for (int f = q.tab.edge[sl] + lane; f < q.tab.edge[sl + 1]; f += 64) acc[sl] += src[f * w] - mean[sl];
+    }
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl)
+      cmean[sl] = wave_sum64(acc[sl]) / (q.tab.edge[sl + 1] - q.tab.edge[sl]);
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl) {
+      acc[sl] = 0.0;
+      if (sl < q.tab.count)
+        for (int f = q.tab.edge[sl] + lane; f < q.tab.edge[sl + 1]; f += 64) {
+          const double d = (src[f * w] - mean[sl]) - cmean[sl];
+          acc[sl] += d * d;
+        }
+    }
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl) {
+      // cnt == 1 -> NaN, as torch.std
+      sd[sl] = sqrt(wave_sum64(acc[sl]) / (q.tab.edge[sl + 1] - q.tab.edge[sl] - 1));
+      if (sd[sl] == 0.0) sd[sl] = 1.0;
+    }
+#pragma unroll
+    for (int sl = 0; sl < kObsMaxSlices; ++sl) {
+      if (sl >= q.tab.count) continue;
+      for (int f = q.tab.edge[sl] + lane; f < q.tab.edge[sl + 1]; f += 64) {
+        const float v = static_cast<float>((src[f * w] - mean[sl]) / sd[sl]);
         dst[f] = v;
         xd[f] = static_cast<__bf16>(v);
       }
@@ -513,6 +543,8 @@ int wide_observe(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint
   WideWork &W = *ctx->wide;
   const int o = ctx->cfg.obs_dim, w = ctx->cfg.window;
   PPO_REQUIRE(o * w <= 64 * kObsMaxK, "wide_observe: W*O = %d exceeds %d", o * w, 64 * kObsMaxK);
+  PPO_REQUIRE(tab.count <= kObsMaxSlices, "wide_observe: %d slices (at most %d)", tab.count,
+              kObsMaxSlices);
   WideObserveArgs q{};
   q.window = window_d;
   q.obs = obs_d;
@@ -535,8 +567,8 @@ int wide_observe(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint
   return 0;
 }
 
-bool wide_observe_ok(const ppo_ctx *ctx) {
-  return ctx->cfg.obs_dim * ctx->cfg.window <= 64 * kObsMaxK;
+bool wide_observe_ok(const ppo_ctx *ctx, int n_slices) {
+  return ctx->cfg.obs_dim * ctx->cfg.window <= 64 * kObsMaxK && n_slices <= kObsMaxSlices;
 }
 
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,

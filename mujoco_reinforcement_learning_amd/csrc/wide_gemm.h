@@ -416,10 +416,23 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
         }
       }
       if (KIND == WK_DGRAD && P.colsum) {
+        // column sums over the band's rows: NT / BN row groups of consecutive rows per column,
+        // then the groups combined in group order (fixed: bitwise reproducible)
+        constexpr int RG = NT / BN, RPG = (C::ER + RG - 1) / RG;
         __syncthreads();
         const int rows = min(C::ER, P.m - mb);
-        if (tid < BN)
-          for (int r = 0; r < rows; ++r) csum += tile[r * C::SC + tid];
+        const int c = tid % BN, g = tid / BN;
+        float s = 0.f;
+        for (int r = g * RPG; r < min(rows, (g + 1) * RPG); ++r) s += tile[r * C::SC + c];
+        __syncthreads();  // every group's reads of the band are done: reuse its first row
+        tile[g * C::SC + c] = s;
+        __syncthreads();
+        if (tid < BN) {
+          float t = tile[tid];
+#pragma unroll
+          for (int q = 1; q < RG; ++q) t += tile[q * C::SC + tid];
+          csum += t;
+        }
       }
     }
     if (KIND == WK_DGRAD && P.colsum && tid < BN && n0 + tid < P.n)

@@ -45,12 +45,13 @@ static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kf
   const int f = force ? atoi(force) : -1;
   if (KIND == WK_WGRAD) {
     if (max_m <= 32) return launch_cfg<1, 1, 1, 4, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
-    switch (f) {
+    switch (f) {  // default: 128 x 128 tiles of 8 waves, two stages, two workgroups per CU
       case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
       case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
-      // 256 x 128 tiles, 8 waves of 64 x 64, 3 stages (144 KB)
-      case 6: return launch_cfg<2, 2, 4, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
-      default: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+      case 3: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+      case 10: return launch_cfg<1, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+      case 12: return launch_cfg<1, 2, 4, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+      default: return launch_cfg<2, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
     }
   }
   if (KIND == WK_F32 || (KIND == WK_FWD && max_n <= 32))
@@ -62,13 +63,24 @@ static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kf
   // minibatch-sized rows: 256 x 256 tiles, 8 waves of 128 x 64 (2 waves per SIMD), double-buffered
   // LDS (128 KB) -- twice the MFMA work per byte staged of the 128 x 128 tile, whose operand
   // stream co-limits at the per-CU L2 rate; PPO_WIDE_CFG=3 keeps the 128 x 128 tile for A/B
-  if constexpr (KIND != WK_WGRAD)
-    if (max_n >= 256 && f != 1 && f != 2 && f != 3)
-      return launch_cfg<4, 2, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
-  switch (f) {
+  // minibatch-sized rows (measured, tools/wide_bench.py at B = 65,536): 128 x 128 tiles of 8 waves
+  // (64 x 32 each), two LDS stages -- 64 KB + the aliased 68 KB epilogue tile, so two workgroups
+  // (16 waves) per CU keep twice the loads in flight of the 4-wave / 3-stage tile (fwd 66 -> 54 us,
+  // dgrad 84 -> 64); the 256 x 256 tile (one 8-wave workgroup per CU) measured as slow as the old one
+  switch (f) {  // tuning variants
     case 1: return launch_cfg<2, 2, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
     case 2: return launch_cfg<2, 2, 2, 2, KIND, 4>(wb, nprob, max_m, max_n, kflops, st);
-    default: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    case 3: return launch_cfg<2, 2, 2, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    case 4:
+      if constexpr (KIND != WK_WGRAD) return launch_cfg<4, 2, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+      else return launch_cfg<2, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    case 6: return launch_cfg<2, 2, 4, 2, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    case 7: return launch_cfg<2, 1, 2, 4, KIND, 3>(wb, nprob, max_m, max_n, kflops, st);
+    case 9: return launch_cfg<1, 1, 2, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    case 10: return launch_cfg<1, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    case 11: return launch_cfg<2, 1, 4, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    case 12: return launch_cfg<1, 2, 4, 2, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
+    default: return launch_cfg<2, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
   }
 }
 
@@ -90,7 +102,9 @@ int row_tile(int kind, int max_m, int max_n) {
   if (max_m <= 4096) return 64;
   const char *force = getenv("PPO_WIDE_CFG");
   const int f = force ? atoi(force) : -1;
-  return (max_n >= 256 && f != 1 && f != 2 && f != 3) ? 256 : 128;
+  if (max_n >= 256 && f == 4) return 256;
+  if (f == 9 || f == 10) return 64;
+  return f == 11 ? 256 : 128;
 }
 
 }  // namespace wide

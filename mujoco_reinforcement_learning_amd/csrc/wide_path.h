@@ -53,7 +53,7 @@ int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps
                      float *mean_d, bool pack, hipStream_t st,
                      bool staged = false);  // pack: refresh the images first; staged: x holds the rows
 // rollout observation step in one launch: window push + standardisation + the bf16 operand rows
-bool wide_observe_ok(const ppo_ctx *ctx);
+bool wide_observe_ok(const ppo_ctx *ctx, int n_slices);
 int wide_observe(ppo_ctx *ctx, double *window_d, const double *obs_d, const uint8_t *reset_d,
                  int all_reset, const PolicySlices &tab, int normalize, float *state_d, int n,
                  hipStream_t st);

@@ -485,6 +485,50 @@ def test_observe_act_fused_matches_layered(gpu, act, n, window, obs, na, reset_p
     assert torch.isfinite(act_).all()
 
 
+@pytest.mark.parametrize("hidden,n,window,obs,na,reset_p", [
+    ((512, 512, 512), 1024, 1, 376, 17, 0.0),   # Humanoid-v4 shard (its six slices)
+    ((512, 512, 512), 77, 1, 376, 17, 0.3),     # ragged: padding operand rows
+    ((64, 64), 300, 3, 27, 8, 0.3)])            # window of 3 (push shifts the kept slots)
+def test_observe_act_wide_matches_layered(gpu, hidden, n, window, obs, na, reset_p):
+    """precision="bf16", ReLU nets off the fused shapes (the wide path): ppo_observe_act (one
+    wide_observe_kernel launch: window push, f64 standardisation, bf16 operand rows; then the
+    wide GEMMs) against ppo_obs_window_push + ppo_obs_normalize + policy_step (which stages the
+    rows itself) on the same context: window, state and every output bit for bit."""
+    E = _E()
+    run, eng, ref, cfg = _agents(gpu, 5, num_envs=n, hidden=hidden, batch_size=n,
+                                 precision="bf16", obs_dim=obs, act_dim=na, window=window)
+    e = eng.engine
+    g = torch.Generator().manual_seed(n + obs + window)
+    win0 = torch.randn(n, obs, window, generator=g, dtype=torch.float64) * 3 + 1
+    new_obs = torch.randn(n, obs, generator=g, dtype=torch.float64) * 3 + 1
+    reset = (torch.rand(n, generator=g) < reset_p).to(torch.uint8)
+    eps = torch.randn(n, na, generator=g)
+    e.pack_weights()
+    outs = {}
+    for mode in ("observe_act", "layered"):
+        win = win0.clone().to(gpu)
+        st = torch.full((n, window * obs), float("nan"), device=gpu)
+        act_, lp, val, mu = (torch.empty(n, na, device=gpu), torch.empty(n, device=gpu),
+                             torch.empty(n, device=gpu), torch.empty(n, na, device=gpu))
+        e.timing(True)
+        if mode == "observe_act":
+            e.observe_act(win, st, obs=new_obs.to(gpu), reset=reset.to(gpu), eps=eps.to(gpu),
+                          action=act_, logp=lp, value=val, mean=mu)
+        else:
+            E.obs_window_push(win, new_obs.to(gpu), reset=reset.to(gpu))
+            E.obs_normalize(win, st)
+            e.policy_step(st, eps=eps.to(gpu), action=act_, logp=lp, value=val, mean=mu)
+        torch.cuda.synchronize()
+        kernels = e.timing_kernels()
+        e.timing(False)
+        assert ("wide_observe_kernel" in kernels) == (mode == "observe_act"), kernels
+        assert any(k.startswith("wide_gemm_kernel") for k in kernels), kernels
+        outs[mode] = [x.cpu() for x in (win, st, act_, lp, val, mu)]
+    for name, a, b in zip(("window", "state", "action", "logp", "value", "mean"),
+                          outs["observe_act"], outs["layered"]):
+        assert torch.equal(a, b), f"{name} differs between observe_act and the layered calls"
+
+
 def test_fused_kernels_bitwise_deterministic(gpu):
     """The fused bf16 kernels reduce in a fixed order: repeating a call on the same inputs gives
     bit-identical outputs (rollout policy step and minibatch gradient at the bench shapes)."""

@@ -70,7 +70,7 @@ def test_wide_dgrad(gpu, m, n, k):
     wt = _bf(torch.randn(n, k, generator=g) / k ** 0.5)  # W^T image [in][out]
     y = _bf(torch.relu(torch.randn(m, n, generator=g)))    # layer output (ReLU)
     count = m - 100
-    tile = 64 if m <= 4096 else 256  # wide_gemm.hip row_tile: 256 x 256 minibatch tiles
+    tile = 64 if m <= 4096 else 128  # wide_gemm.hip row_tile: 128-row minibatch tiles
     tiles = (m + tile - 1) // tile
     yd = _pad_rows(y, 128).to(gpu)
     c = yd.clone()  # in place over the activations

@@ -56,14 +56,14 @@ def main():
             b = r(n, k)
             c = (torch.empty(m, n, device=dev) if kind == F32 else r(m, n))
             aux = c.clone() if kind == DGRAD else None
-            cs = torch.empty((m + 127) // 128, n, device=dev) if kind == DGRAD else None
+            cs = torch.empty((m + 63) // 64, n, device=dev) if kind == DGRAD else None  # >= any row tile
             bias = torch.zeros(n, device=dev) if kind == FWD else None
             fn = lambda: _lib.check(lib.ppo_wide_gemm(kind, m, n, k, p(a), k, p(b), k, p(c), n,
                                                       p(bias), p(aux), p(cs), 0, 1, None, st))
             flops = 2.0 * m * n * k
             ref = lambda: torch.matmul(a, b.t())
         us_ref = timed(ref)
-        for cfg in ("default", "3", "1", "6"):  # PPO_WIDE_CFG variants (wide_gemm.hip run_kind)
+        for cfg in ("default", "3", "4", "10", "11", "12"):  # PPO_WIDE_CFG variants (wide_gemm.hip run_kind)
             if cfg == "default":
                 os.environ.pop("PPO_WIDE_CFG", None)
             else:
