@@ -40,6 +40,11 @@ static const int g_wide_enabled = [] {
   const char *v = getenv("PPO_WIDE");
   return v ? atoi(v) : 1;
 }();
+static bool wide_fused_rollout_enabled() {  // PPO_WIDE_FUSED_ROLLOUT=0 at context creation:
+  const char *v = getenv("PPO_WIDE_FUSED_ROLLOUT");  // the layered rollout GEMMs (parity tests)
+  return v ? atoi(v) != 0 : true;
+}
+constexpr int kFMaxW = 512;  // widest layer (and input row) of the fused rollout kernel
 
 bool wide_shapes_ok(const ppo_ctx *ctx) {
   if (!g_wide_enabled || ctx->fused_ok) return false;
@@ -63,7 +68,7 @@ int wide_alloc(ppo_ctx *ctx) {
   const int64_t R = rup(ctx->cfg.max_rows, 256);
   w->rpad = static_cast<int>(R);
   const int din = ctx->cfg.obs_dim * ctx->cfg.window;
-  w->ldx = static_cast<int>(rup(din, 64));
+  w->ldx = static_cast<int>(rup(din, 128));  // whole 8-k-step groups for the fused rollout
   const int blocks = static_cast<int>(R / kWideLossRows);
   // carve-out in bytes; every buffer 256-B aligned, 1 KB of slack after each (tile reads past a
   // row end stay inside the allocation)
@@ -109,6 +114,25 @@ int wide_alloc(ppo_ctx *ctx) {
     }
   }
   bytes += 1024;
+  // fused rollout: every hidden width a multiple of 128 and at most kFMaxW, the input row too,
+  // the actor head at most 32 wide
+  bool fr = w->ldx <= kFMaxW && ctx->cfg.act_dim <= 32;
+  for (int z = 0; z < 2; ++z)
+    for (int l = 0; l < ctx->net[z].n_hidden; ++l)
+      fr = fr && ctx->net[z].layer[l].out % 128 == 0 && ctx->net[z].layer[l].out <= kFMaxW;
+  w->fused_rollout = fr && wide_fused_rollout_enabled();
+  int64_t off_wf[2][PPO_MAX_LAYERS + 1] = {};
+  if (w->fused_rollout)
+    for (int z = 0; z < 2; ++z) {
+      const NetDesc &nd = ctx->net[z];
+      WideNetWork &wn = w->net[z];
+      for (int l = 0; l <= nd.n_hidden; ++l) {
+        const LayerDesc &L = nd.layer[l];
+        wn.wf_tiles[l] = static_cast<int>(rup(L.out, 32) / 32);
+        wn.wf_ks[l] = static_cast<int>(rup(L.in, 128) / 16);
+        off_wf[z][l] = take(static_cast<int64_t>(wn.wf_tiles[l]) * wn.wf_ks[l] * 512 * 2);
+      }
+    }
   const int64_t opart = take(static_cast<int64_t>(blocks) * kWidePart * 4);
   const int64_t oloss = take(static_cast<int64_t>(blocks) * 2 * 4);
   void *arena = nullptr;
@@ -142,6 +166,8 @@ int wide_alloc(ppo_ctx *ctx) {
     }
     wn.dz = reinterpret_cast<__bf16 *>(base + off[z].dz);
     wn.z = reinterpret_cast<float *>(base + off[z].z);
+    for (int l = 0; l <= nd.n_hidden; ++l)
+      wn.wf[l] = w->fused_rollout ? reinterpret_cast<__bf16 *>(base + off_wf[z][l]) : nullptr;
   }
   w->part = reinterpret_cast<float *>(base + opart);
   w->loss_part = reinterpret_cast<float *>(base + oloss);
@@ -210,7 +236,71 @@ __global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q) {
   }
 }
 
-int wide_pack(ppo_ctx *ctx, hipStream_t st) {
+// Fragment-major image of one layer: element j of lane `lane` in the block of (k-step ks, tile ot)
+// holds W[32 ot + (lane & 31)][16 ks + 8 (lane >> 5) + j] (zero outside the tensor); one thread
+// writes one lane's 16-B fragment from 8 consecutive master elements.
+struct FragDesc {
+  const float *w;
+  __bf16 *dst;
+  int out, in, tiles, ks;
+  int blocks;  // first block of this image
+};
+struct FragArgs {
+  FragDesc img[2 * (PPO_MAX_LAYERS + 1)];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wide_frag_pack_kernel(FragArgs q) {
+  int i = 0;
+  while (i + 1 < q.n && q.img[i + 1].blocks <= static_cast<int>(blockIdx.x)) ++i;
+  const FragDesc d = q.img[i];
+  const int64_t f = static_cast<int64_t>(blockIdx.x - d.blocks) * 256 + threadIdx.x;  // fragment
+  if (f >= static_cast<int64_t>(d.tiles) * d.ks * 64) return;
+  const int lane = static_cast<int>(f & 63);
+  const int blk = static_cast<int>(f >> 6), ks = blk / d.tiles, ot = blk - ks * d.tiles;
+  const int o = 32 * ot + (lane & 31), i0 = 16 * ks + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool ok = o < d.out && i0 + j < d.in;
+    const float u = d.w[ok ? static_cast<int64_t>(o) * d.in + i0 + j : 0];
+    v[j] = ok ? u : 0.f;
+  }
+  reinterpret_cast<uint4 *>(d.dst)[f] =
+      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
+                 wide::pack2(v[6], v[7]));
+}
+
+static int wide_frag_pack(ppo_ctx *ctx, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  FragArgs q{};
+  int blocks = 0;
+  double elems = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    const WideNetWork &wn = W.net[z];
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      FragDesc &d = q.img[q.n++];
+      d.w = ctx->params + nd.layer[l].w_off;
+      d.dst = wn.wf[l];
+      d.out = nd.layer[l].out;
+      d.in = nd.layer[l].in;
+      d.tiles = wn.wf_tiles[l];
+      d.ks = wn.wf_ks[l];
+      d.blocks = blocks;
+      blocks += static_cast<int>(ceil_div(static_cast<int64_t>(d.tiles) * d.ks * 64, 256));
+      elems += static_cast<double>(d.out) * d.in;
+    }
+  }
+  launch_k(TimRec{KC_GATHER, "wide_frag_pack_kernel", 0.0, elems * (4.0 + 2.0)},
+           wide_frag_pack_kernel, dim3(blocks), dim3(256), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
+  if (frag && ctx->wide->fused_rollout)
+    if (int rc = wide_frag_pack(ctx, st)) return rc;
   WideWork &W = *ctx->wide;
   PackArgs q{};
   int blocks = 0;
@@ -571,6 +661,238 @@ bool wide_observe_ok(const ppo_ctx *ctx, int n_slices) {
   return ctx->cfg.obs_dim * ctx->cfg.window <= 64 * kObsMaxK && n_slices <= kObsMaxSlices;
 }
 
+// ============================================================================================
+// Fused rollout policy step of the wide path (A2-A4 in one launch per step): both nets' hidden
+// layers, heads, sampling and log-prob for 32 rollout rows per workgroup -- five launches of the
+// layered rollout (three FWD GEMMs, the head GEMM, wide_policy_head_kernel) before.
+//
+// grid (rows_pad / 32, 2 nets), 8 waves.  The 32 rows' activations stay in LDS (two ping-pong
+// [32][512] bf16 images, 16-B chunk c of row r at c ^ (r & 15): the B-operand row reads are
+// conflict-free); each layer's weights stream from L2 as 32x32x16 A fragments of the
+// fragment-major image (one 1 KB block per (k-step, 32-feature tile)), two 8-k-step groups in
+// flight per wave.  Wave w owns the output features 64w..64w+63 (two tiles): C = W . act^T, so a
+// lane holds one row's 4-feature runs and writes them as 8-B image stores.  Bias + ReLU in f32,
+// the stored activation rounded to bf16 (the layered FWD epilogue).  The head (at most 32
+// outputs) runs on wave 0 in the same k order as the head GEMM; then one thread per (row, action
+// pair) applies wide_policy_head_kernel's formulas and the row's log-prob is summed in action order.
+// ============================================================================================
+constexpr int kFRows = 32;
+constexpr int kFPitch = kFMaxW * 2;  // bytes per LDS image row
+constexpr int kFGroup = 8;           // k-steps per fragment group
+
+struct WideFusedNet {
+  const __bf16 *wf[PPO_MAX_LAYERS + 1];
+  const float *b[PPO_MAX_LAYERS + 1];
+  int tiles[PPO_MAX_LAYERS + 1], ks[PPO_MAX_LAYERS + 1];
+  int n_hidden;
+};
+struct WideFusedArgs {
+  WideFusedNet net[2];
+  int use[2];
+  const __bf16 *x;
+  int ldx, n;
+  int act_dim;
+  float omv;
+  const float *logstd;
+  const float *eps;
+  uint64_t seed, offset;
+  const uint64_t *offset_base;
+  float *action, *logp, *value, *mean;
+};
+
+__device__ __forceinline__ int fimg_off(int row, int chunk) {
+  return row * kFPitch + ((chunk ^ (row & 15)) << 4);
+}
+
+// one group of kFGroup k-steps of a wave's fragments (tiles ot0, ot0 + 1; NT of them valid)
+template <int NT>
+__device__ __forceinline__ void frag_load(const __bf16 *wf, int tiles, int ot0, int g, int lane,
+                                          wide::bf16x8 (&f)[kFGroup][2]) {
+#pragma unroll
+  for (int s = 0; s < kFGroup; ++s)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t blk = static_cast<int64_t>(g * kFGroup + s) * tiles + ot0 + t;
+      f[s][t] = *reinterpret_cast<const wide::bf16x8 *>(wf + (blk * 64 + lane) * 8);
+    }
+}
+
+// acc[t] += W[tile ot0 + t] . img^T over the layer's k-steps
+template <int NT>
+__device__ __forceinline__ void fused_layer(const __bf16 *wf, int tiles, int ks, int ot0,
+                                            const char *img, int lane, wide::f32x16 (&acc)[2]) {
+  const int ng = ks / kFGroup;
+  const int row = lane & 31, h = lane >> 5;
+  wide::bf16x8 cur[kFGroup][2], nxt[kFGroup][2];
+  frag_load<NT>(wf, tiles, ot0, 0, lane, cur);
+  for (int g = 0; g < ng; ++g) {
+    if (g + 1 < ng) frag_load<NT>(wf, tiles, ot0, g + 1, lane, nxt);
+#pragma unroll
+    for (int s = 0; s < kFGroup; ++s) {
+      const int k16 = g * kFGroup + s;
+      const wide::bf16x8 bv = *reinterpret_cast<const wide::bf16x8 *>(img + fimg_off(row, 2 * k16 + h));
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[s][t], bv, acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < kFGroup; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) cur[s][t] = nxt[s][t];
+  }
+}
+
+__global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kFRows * kFPitch];
+  __shared__ float zt[kFRows][33];   // head outputs [row][output]
+  __shared__ float lpt[kFRows][33];  // per-(row, action) log-prob terms
+  // (row block, net) from the linear block id: with a multiple of 4 row blocks per net, the actor
+  // runs on XCDs 0-3 and the critic on XCDs 4-7 (blocks b, b + 8, ... share an XCD), so each
+  // XCD's L2 holds one net's weight images instead of both
+  const int nb = (q.n + kFRows - 1) / kFRows, b = static_cast<int>(blockIdx.x);
+  int z, rb;
+  if (nb % 4 == 0) {
+    const int x = b % 8;
+    z = x / 4;
+    rb = (x % 4) + 4 * (b / 8);
+  } else {
+    z = b / nb;
+    rb = b % nb;
+  }
+  if (!q.use[z]) return;  // uniform per block
+  const WideFusedNet &N = q.net[z];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = rb * kFRows;
+  // ---- the rows' bf16 states (x, zero-padded to ldx) -> image 0 ----
+  const int cpr = q.ldx / 8;
+  for (int e = tid; e < kFRows * cpr; e += 512) {
+    const int row = e / cpr, c = e - row * cpr;
+    const uint4 v = *reinterpret_cast<const uint4 *>(q.x + static_cast<int64_t>(r0 + row) * q.ldx + 8 * c);
+    *reinterpret_cast<uint4 *>(lds + fimg_off(row, c)) = v;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < N.n_hidden; ++l) {
+    const int tiles = N.tiles[l];
+    const int ot0 = 2 * w;
+    wide::f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    const char *src = lds + cur * kFRows * kFPitch;
+    char *dst = lds + (cur ^ 1) * kFRows * kFPitch;
+    if (ot0 + 1 < tiles) fused_layer<2>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
+    else if (ot0 < tiles) fused_layer<1>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
+    // epilogue: bias + ReLU, bf16 4-feature runs of row (lane & 31)
+    const int row = lane & 31;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (ot0 + t >= tiles) continue;  // uniform per wave
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o = 32 * (ot0 + t) + 8 * g + 4 * (lane >> 5);
+        const float4 bv = N.b[l] ? *reinterpret_cast<const float4 *>(N.b[l] + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float y0 = act_forward(acc[t][4 * g] + bv.x, PPO_ACT_RELU);
+        const float y1 = act_forward(acc[t][4 * g + 1] + bv.y, PPO_ACT_RELU);
+        const float y2 = act_forward(acc[t][4 * g + 2] + bv.z, PPO_ACT_RELU);
+        const float y3 = act_forward(acc[t][4 * g + 3] + bv.w, PPO_ACT_RELU);
+        *reinterpret_cast<uint2 *>(dst + fimg_off(row, o >> 3) + 2 * (o & 7)) =
+            make_uint2(wide::pack2(y0, y1), wide::pack2(y2, y3));
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // ---- head pre-activations (<= 32 outputs) on wave 0 ----
+  const int L = N.n_hidden;
+  if (w == 0) {
+    wide::f32x16 acc[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
+    fused_layer<1>(N.wf[L], N.tiles[L], N.ks[L], 0, lds + cur * kFRows * kFPitch, lane, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) zt[lane & 31][(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = acc[0][r];
+  }
+  __syncthreads();
+  const int row = tid >> 4, j = r0 + row;
+  const bool row_ok = j < q.n;
+  if (z == 0) {
+    const int A = q.act_dim;
+    const uint64_t base = q.offset + (q.offset_base ? *q.offset_base : 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int a = (tid & 15) + 16 * u;
+      float lp = 0.f;
+      if (row_ok && a < A) {
+        const float zr = zt[row][a];
+        const float zz = N.b[L] ? zr + N.b[L][a] : zr;
+        const float mu = q.omv * tanhf(zz);
+        const float sd = expf(q.logstd[a]);
+        const int64_t idx = static_cast<int64_t>(j) * A + a;
+        const float e = q.eps ? q.eps[idx] : philox_normal_at(q.seed, base + idx);
+        const float x = e * sd + mu;  // torch.normal: randn*std then + mean (two roundings)
+        if (q.action) q.action[idx] = x;
+        if (q.mean) q.mean[idx] = mu;
+        const float d = x - mu;
+        const float var = sd * sd;
+        lp = ((-(d * d)) / (2.f * var) - logf(sd)) - kLogSqrt2Pi;
+      }
+      lpt[row][a] = lp;
+    }
+    __syncthreads();
+    if ((tid & 15) == 0 && row_ok && q.logp) {
+      float s = 0.f;
+      for (int a = 0; a < A; ++a) s += lpt[row][a];  // action order (policy_head_kernel)
+      q.logp[j] = s;
+    }
+  } else if ((tid & 15) == 0 && row_ok && q.value) {
+    const float v = zt[row][0];
+    q.value[j] = N.b[L] ? v + N.b[L][0] : v;
+  }
+}
+
+static int wide_policy_fused(ppo_ctx *ctx, const bool use[2], int n, const float *eps_d,
+                             uint64_t seed, uint64_t offset, float *action_d, float *logp_d,
+                             float *value_d, float *mean_d, hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  WideFusedArgs q{};
+  double flops = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    const WideNetWork &wn = W.net[z];
+    WideFusedNet &f = q.net[z];
+    q.use[z] = use[z];
+    f.n_hidden = nd.n_hidden;
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      f.wf[l] = wn.wf[l];
+      f.b[l] = L.b_off >= 0 ? ctx->params + L.b_off : nullptr;
+      f.tiles[l] = wn.wf_tiles[l];
+      f.ks[l] = wn.wf_ks[l];
+      if (use[z]) flops += 2.0 * n * L.out * L.in;
+    }
+  }
+  q.x = W.x;
+  q.ldx = W.ldx;
+  q.n = n;
+  q.act_dim = ctx->cfg.act_dim;
+  q.omv = ctx->cfg.output_max_value;
+  q.logstd = ctx->params + ctx->net[0].logstd_off;
+  q.eps = eps_d;
+  q.seed = seed;
+  q.offset = offset;
+  q.offset_base = ctx->rng_counter;
+  q.action = action_d;
+  q.logp = logp_d;
+  q.value = value_d;
+  q.mean = mean_d;
+  launch_k(TimRec{KC_POLICY_HEAD, "wide_policy_fused_kernel", flops, 0.0},
+           wide_policy_fused_kernel, dim3(2 * ceil_div(n, kFRows)), dim3(512), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                      uint64_t offset, float *action_d, float *logp_d, float *value_d,
                      float *mean_d, bool pack, hipStream_t st, bool staged) {
@@ -582,6 +904,9 @@ int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps
     if (int rc = wide_pack(ctx, st)) return rc;
   if (!staged)  // (wide_observe wrote x already)
     if (int rc = stage_rows(ctx, state_d, nullptr, nullptr, n, rows_pad, st)) return rc;
+  if (W.fused_rollout)  // the images are current (pack above, or ppo_pack_weights)
+    return wide_policy_fused(ctx, use, n, eps_d, seed, offset, action_d, logp_d, value_d, mean_d,
+                             st);
   if (int rc = forward(ctx, use, rows_pad, nullptr, st)) return rc;
   const NetDesc &A = ctx->net[0], &C = ctx->net[1];
   WidePolicyArgs q{};
@@ -760,7 +1085,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   const int64_t P = ctx->total_params;
   const int A = ctx->cfg.act_dim;
   NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
-  if (int rc = wide_pack(ctx, st)) return rc;
+  if (int rc = wide_pack(ctx, st, false)) return rc;
   if (int rc = stage_rows(ctx, states_d, rows_d, count_d, b, rows_pad, st)) return rc;
   const bool both[2] = {true, true};
   if (int rc = forward(ctx, both, rows_pad, count_d, st)) return rc;

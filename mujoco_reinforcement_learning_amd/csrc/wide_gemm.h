@@ -219,9 +219,27 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = (P.m + BM - 1) / BM, tiles_n = (P.n + BN - 1) / BN;
-  if (static_cast<int>(blockIdx.x) >= tiles_m * tiles_n) return;
-  int id;
-  xcd_map(blockIdx.x, tiles_m * tiles_n, id);
+  const int tiles = tiles_m * tiles_n;
+  int id, split = 0;
+  if constexpr (C::TT) {
+    // WGRAD: blockIdx.x enumerates (split, tile).  Every tile of a split reads the same k-rows of
+    // both operands, so all of them go to one XCD (blocks b, b + 8, ... share an XCD and its L2):
+    // split s on XCD s % 8, its rows fetched from HBM once instead of once per XCD holding one of
+    // its tiles.  Bijective when the split count is a multiple of 8; otherwise split-major.
+    const int b = static_cast<int>(blockIdx.x);
+    if (b >= tiles * wb.splits) return;
+    if (wb.splits % 8 == 0) {
+      const int x = b % 8, j = b / 8;
+      split = x + 8 * (j / tiles);
+      id = j % tiles;
+    } else {
+      split = b / tiles;
+      id = b % tiles;
+    }
+  } else {
+    if (static_cast<int>(blockIdx.x) >= tiles) return;
+    xcd_map(blockIdx.x, tiles, id);
+  }
   const int tile_m = id / tiles_n, tile_n = id % tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int count = wb.rows_n ? *wb.rows_n : (C::TT ? P.k : P.m);
@@ -230,8 +248,8 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
   int kt0 = 0, kt1;
   if constexpr (C::TT) {
     const int nk = (count + kBK - 1) / kBK;
-    kt0 = static_cast<int>((static_cast<int64_t>(blockIdx.y) * nk) / wb.splits);
-    kt1 = static_cast<int>((static_cast<int64_t>(blockIdx.y + 1) * nk) / wb.splits);
+    kt0 = static_cast<int>((static_cast<int64_t>(split) * nk) / wb.splits);
+    kt1 = static_cast<int>((static_cast<int64_t>(split + 1) * nk) / wb.splits);
   } else {
     kt1 = P.k / kBK;
     if (m0 >= count) {  // tile wholly past the row count: zero output rows and colsum row
@@ -340,7 +358,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
     static_assert(NT % CG == 0, "epilogue layout");
     const int cg = tid % CG, r0 = tid / CG;
     const int n = n0 + 4 * cg;
-    float *slab = static_cast<float *>(P.c) + static_cast<int64_t>(blockIdx.y) * P.slab_stride;
+    float *slab = static_cast<float *>(P.c) + static_cast<int64_t>(split) * P.slab_stride;
     for (int r = r0; r < BM; r += RSTEP) {
       const int m = m0 + r;
       if (m >= P.m) break;

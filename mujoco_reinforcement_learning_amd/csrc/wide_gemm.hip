@@ -15,7 +15,7 @@ static int launch_cfg(const WideBatch &wb, int nprob, int max_m, int max_n, int 
                       hipStream_t st) {
   using C = WideCfg<TM, TN, WM, WN, KIND, NS>;
   const int tiles = ceil_div(max_m, C::BM) * ceil_div(max_n, C::BN);
-  const dim3 grid(tiles, KIND == WK_WGRAD ? wb.splits : 1, nprob);
+  const dim3 grid(KIND == WK_WGRAD ? tiles * wb.splits : tiles, 1, nprob);  // WGRAD: (split, tile)
   TimRec rec{KIND == WK_FWD || KIND == WK_F32 ? KC_GEMM_FWD
                                               : (KIND == WK_DGRAD ? KC_GEMM_DGRAD : KC_GEMM_WGRAD),
              nullptr, 0.0, 0.0};

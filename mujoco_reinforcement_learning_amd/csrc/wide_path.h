@@ -23,12 +23,18 @@ struct WideNetWork {
   float *colsum[PPO_MAX_LAYERS];   // [rpad / 64][out] bias-gradient partials per DGRAD row tile
   __bf16 *dz;                      // [rpad][64] head pre-activation gradients (bf16 operand)
   float *z;                        // [rpad][32] head pre-activations (f32)
+  // rollout (wide_policy_fused_kernel): fragment-major W images, one 1 KB block of the 64 lanes'
+  // 32x32x16 A fragments per (k-step, 32-feature tile); null when the fused rollout is off
+  __bf16 *wf[PPO_MAX_LAYERS + 1];
+  int wf_tiles[PPO_MAX_LAYERS + 1];  // 32-feature tiles (round_up(out, 32) / 32)
+  int wf_ks[PPO_MAX_LAYERS + 1];     // 16-deep k-steps (round_up(in, 128) / 16)
 };
 
 struct WideWork {
   int rpad;                        // rows allocated: round_up(max_rows, 128)
   __bf16 *x;                       // [rpad][ldx] bf16 states (gathered minibatch / rollout rows)
-  int ldx;                         // round_up(W*O, 64)
+  int ldx;                         // round_up(W*O, 128)
+  bool fused_rollout;              // wide_policy_fused_kernel covers the nets (wide_alloc)
   WideNetWork net[2];
   float *part;                     // loss-kernel partials [blocks][kWidePart]
   float *loss_part;                // [blocks][2]
@@ -47,7 +53,8 @@ bool wide_active(const ppo_ctx *ctx);
 int wide_alloc(ppo_ctx *ctx);
 void wide_free(ppo_ctx *ctx);
 // refresh the bf16 weight images from the f32 master parameters
-int wide_pack(ppo_ctx *ctx, hipStream_t st);
+// frag: also the fragment-major images of the fused rollout (before a rollout / policy step)
+int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag = true);
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                      uint64_t offset, float *action_d, float *logp_d, float *value_d,
                      float *mean_d, bool pack, hipStream_t st,

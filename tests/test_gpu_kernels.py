@@ -522,11 +522,51 @@ def test_observe_act_wide_matches_layered(gpu, hidden, n, window, obs, na, reset
         kernels = e.timing_kernels()
         e.timing(False)
         assert ("wide_observe_kernel" in kernels) == (mode == "observe_act"), kernels
-        assert any(k.startswith("wide_gemm_kernel") for k in kernels), kernels
+        # the fused rollout kernel when the widths allow it, else the layered GEMMs
+        assert ("wide_policy_fused_kernel" in kernels or
+                any(k.startswith("wide_gemm_kernel") for k in kernels)), kernels
         outs[mode] = [x.cpu() for x in (win, st, act_, lp, val, mu)]
     for name, a, b in zip(("window", "state", "action", "logp", "value", "mean"),
                           outs["observe_act"], outs["layered"]):
         assert torch.equal(a, b), f"{name} differs between observe_act and the layered calls"
+
+
+@pytest.mark.parametrize("n", [1024, 77])
+def test_policy_step_wide_fused_matches_layered(gpu, monkeypatch, n):
+    """Humanoid shapes (3x512, O=376, A=17), bf16: the fused rollout kernel
+    (wide_policy_fused_kernel: hidden layers, heads, sampling in one launch) against the layered
+    wide rollout (FWD GEMMs + head GEMM + wide_policy_head_kernel; PPO_WIDE_FUSED_ROLLOUT=0) on
+    the same parameters and noise.  Both sum every product in the same k order on the same bf16
+    operands; the bar allows for the MFMA computing W.act^T instead of act.W^T: mean / value
+    within 1e-6 of their scale, actions fl(fl(eps*std)+mean) of each one's own mean, log-prob
+    within 1e-5."""
+    outs = {}
+    for mode in ("layered", "fused"):
+        monkeypatch.setenv("PPO_WIDE_FUSED_ROLLOUT", "1" if mode == "fused" else "0")
+        run, eng, ref, cfg = _agents(gpu, 3, num_envs=n, hidden=(512, 512, 512), batch_size=n,
+                                     precision="bf16", obs_dim=376, act_dim=17)
+        e = eng.engine
+        g = torch.Generator().manual_seed(5)
+        state = torch.randn(n, 376, generator=g).to(gpu)
+        eps = torch.randn(n, 17, generator=g).to(gpu)
+        act_, lp, val, mu = (torch.empty(n, 17, device=gpu), torch.empty(n, device=gpu),
+                             torch.empty(n, device=gpu), torch.empty(n, 17, device=gpu))
+        e.timing(True)
+        e.policy_step(state, eps=eps, action=act_, logp=lp, value=val, mean=mu)
+        torch.cuda.synchronize()
+        kernels = e.timing_kernels()
+        e.timing(False)
+        assert ("wide_policy_fused_kernel" in kernels) == (mode == "fused"), kernels
+        outs[mode] = [x.cpu() for x in (act_, lp, val, mu)]
+        std = eng.networks["actor"].actor_logstd.detach().exp().cpu()
+        assert torch.equal(outs[mode][0], eps.cpu() * std + outs[mode][3])
+    (a_f, lp_f, v_f, m_f), (a_l, lp_l, v_l, m_l) = outs["fused"], outs["layered"]
+    for name, x, y in (("mean", m_f, m_l), ("value", v_f, v_l)):
+        err = float((x - y).abs().max()) / (float(y.abs().max()) + 1e-12)
+        print(f"fused vs layered rollout {name}: max err {err:.3e} of scale, "
+              f"bitwise {torch.equal(x, y)}")
+        assert err <= 1e-6, (name, err)
+    torch.testing.assert_close(lp_f, lp_l, rtol=1e-5, atol=1e-5)
 
 
 def test_fused_kernels_bitwise_deterministic(gpu):

@@ -63,7 +63,7 @@ def main():
             flops = 2.0 * m * n * k
             ref = lambda: torch.matmul(a, b.t())
         us_ref = timed(ref)
-        for cfg in ("default", "3", "4", "10", "11", "12"):  # PPO_WIDE_CFG variants (wide_gemm.hip run_kind)
+        for cfg in ("default", "1"):  # PPO_WIDE_CFG variants (wide_gemm.hip run_kind)
             if cfg == "default":
                 os.environ.pop("PPO_WIDE_CFG", None)
             else:
