@@ -17,6 +17,7 @@
 #   cnntrace  rocprofv3 --kernel-trace --stats over the CNN bench
 #   dp2       2-rank data-parallel rehearsal on the one GPU (gloo) -> bench_${TAG}_dp2.json
 #   hum       Humanoid configs[3] shard (1024 envs, O=376, A=17, 3x512) -> bench_${TAG}_hum.json
+#   configs   bench lines of Ant, Humanoid 8192 on one GPU, the pixel CNN and the BiLSTM
 #   humtrace  rocprofv3 --kernel-trace --stats over the Humanoid shard bench (graph replay, no events)
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1; fold off and on)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
@@ -128,6 +129,19 @@ for S in $STEPS; do
         --steps 2 --warmup 1 --no-legs --no-cpu-baseline --no-timing > gpurun_out/rp_${TAG}_hum.json \
         2> gpurun_out/rp_${TAG}_hum.log || fail humtrace gpurun_out/rp_${TAG}_hum.log
       head -25 $(find gpurun_out/rp_${TAG}_hum -name "*kernel_stats.csv") | cut -c1-160 ;;
+    configs)
+      # the BASELINE configs beside the headline (profiles/r03_configs.md): Ant, Humanoid 8192 on
+      # one GPU, the pixel CNN, the main.py BiLSTM
+      timeout -k 10 300 python bench.py --obs-dim 27 --act-dim 8 --no-legs --no-cpu-baseline \
+        > gpurun_out/bench_${TAG}_ant.json 2> gpurun_out/bench_${TAG}_ant.err || fail ant gpurun_out/bench_${TAG}_ant.err
+      timeout -k 10 400 python bench.py --num-envs 8192 --obs-dim 376 --act-dim 17 --hidden 512,512,512 \
+        --steps 2 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum8k.json \
+        2> gpurun_out/bench_${TAG}_hum8k.err || fail hum8k gpurun_out/bench_${TAG}_hum8k.err
+      timeout -k 10 500 python bench.py --model cnn --steps 2 --warmup 1 --no-cpu-baseline \
+        > gpurun_out/bench_${TAG}_cnn.json 2> gpurun_out/bench_${TAG}_cnn.err || fail cnn gpurun_out/bench_${TAG}_cnn.err
+      timeout -k 10 500 python bench.py --model lstm --steps 2 --warmup 1 \
+        > gpurun_out/bench_${TAG}_lstm.json 2> gpurun_out/bench_${TAG}_lstm.err || fail lstm gpurun_out/bench_${TAG}_lstm.err
+      for c in ant hum8k cnn lstm; do cut -c1-200 gpurun_out/bench_${TAG}_$c.json; done ;;
     wbench)
       timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
       cat gpurun_out/wbench_${TAG}.txt ;;
