@@ -215,7 +215,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
 
   // ---- per-unit row state, fixed across k-steps -------------------------------------------
   float va[IA::NU][4], vb[IB::NU][4];
+  // Every gather below loads unconditionally from a clamped, in-bounds address and masks the value
+  // (a load under a branch makes the compiler drain every earlier load at the merge, so a k-tile's
+  // NU gathers would run one memory round trip after another; DESIGN.md s4 "loads behind branches")
   const TIN *arow[IA::NU];  // FWD: receptive field of the unit's row
+  bool arow_ok[IA::NU];
   int aimg[IA::NU], ajy[IA::NU], ajx[IA::NU];  // DGRAD: the unit row's image / phase position
   if constexpr (MODE == MODE_FWD) {
 #pragma unroll
@@ -223,7 +227,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
       int rr, kk;
       IA::coords(tid + u * NT, rr, kk);
       const int m = m0 + rr;
-      arow[u] = m < M ? field(m / G::P, m % G::P) : nullptr;
+      const int mc = m < M ? m : M - 1;  // clamped: every gather loads, masked at use
+      arow[u] = field(mc / G::P, mc % G::P);
+      arow_ok[u] = m < M;
     }
   }
   if constexpr (MODE == MODE_DGRAD) {
@@ -239,25 +245,30 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
     }
   }
 
+  auto mask4 = [](bool ok, float (&o)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = ok ? o[j] : 0.f;
+  };
   auto gload = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < IA::NU; ++u) {
       int rr, kk;
       IA::coords(tid + u * NT, rr, kk);
       if constexpr (MODE == MODE_FWD) {
-        if (arow[u]) im2col4(arow[u], k0 + kk, va[u]);
-        else zero4(va[u]);
+        im2col4(arow[u], k0 + kk, va[u]);
+        mask4(arow_ok[u], va[u]);
       } else if constexpr (MODE == MODE_DGRAD) {
         const int c = k0 + kk, t = c / G::cout, co = c - t * G::cout;
         const int oy = ajy[u] - t / G::tk, ox = ajx[u] - t % G::tk;
-        if (aimg[u] >= 0 && oy >= 0 && oy < G::hout && ox >= 0 && ox < G::wout)
-          dz4(aimg[u], oy * G::wout + ox, co, va[u]);
-        else
-          zero4(va[u]);
+        const bool ok = aimg[u] >= 0 && oy >= 0 && oy < G::hout && ox >= 0 && ox < G::wout;
+        dz4(ok ? aimg[u] : 0, ok ? oy * G::wout + ox : 0, co, va[u]);
+        mask4(ok, va[u]);
       } else {  // WGRAD: A[k = position][m = co]
         const int kr = k0 + kk;
-        if (kr < kend) dz4(kr / G::P, kr % G::P, m0 + rr, va[u]);
-        else zero4(va[u]);
+        const bool ok = kr < kend;
+        const int kc = ok ? kr : kbeg;
+        dz4(kc / G::P, kc % G::P, m0 + rr, va[u]);
+        mask4(ok, va[u]);
       }
     }
 #pragma unroll
@@ -272,8 +283,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
         load4(Nt.w + static_cast<int64_t>(co) * G::kdim + (ky * G::k + kx) * G::cin + n0 + rr, vb[u]);
       } else {  // WGRAD: B[k = position][n = (tap, ci)]
         const int kr = k0 + kk, c = n0 + rr;
-        if (kr < kend && c < N) im2col4(field(kr / G::P, kr % G::P), c, vb[u]);
-        else zero4(vb[u]);
+        const bool ok = kr < kend && c < N;
+        const int kc = ok ? kr : kbeg;
+        im2col4(field(kc / G::P, kc % G::P), ok ? c : 0, vb[u]);
+        mask4(ok, vb[u]);
       }
     }
   };
@@ -372,7 +385,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + (wn * TN + j) * 32 + (lane & 31);
       float bias = 0.f;
-      if (MODE == MODE_FWD && Nt.bias) bias = Nt.bias[n];
+      if (MODE == MODE_FWD && Nt.bias) {
+        const float bv = Nt.bias[n < N ? n : N - 1];
+        bias = n < N ? bv : 0.f;
+      }
+      // DGRAD: the 16 activation operands of act' first, from clamped addresses (no load behind
+      // the bounds test), then the stores
+      float yv[16];
+      if constexpr (MODE == MODE_DGRAD) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int mc = m < M ? m : M - 1, nc = n < N ? n : N - 1;
+          const int img = mc / (G::hq * G::wq), jj = mc - img * (G::hq * G::wq);
+          const int qy = py + G::s * (jj / G::wq), qx = px + G::s * (jj % G::wq);
+          yv[r] = load1(xin + (static_cast<int64_t>(img) * G::PIN + qy * G::win + qx) * G::cin + nc);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -390,7 +419,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
           const int img = m / (G::hq * G::wq), jj = m - img * (G::hq * G::wq);
           const int qy = py + G::s * (jj / G::wq), qx = px + G::s * (jj % G::wq);
           const int64_t e = (static_cast<int64_t>(img) * G::PIN + qy * G::win + qx) * G::cin + n;
-          Nt.dout[e] = act_backward(v, load1(xin + e), PPO_ACT_RELU);
+          Nt.dout[e] = act_backward(v, yv[r], PPO_ACT_RELU);
         } else {
           const int tap = n / G::cin, ci = n - tap * G::cin;
           Nt.slab[sb + static_cast<int64_t>(m) * G::kdim + ci * (G::k * G::k) + tap] = v;
