@@ -356,7 +356,8 @@ int launch_conv(const ConvArgs &a, int nets, hipStream_t st) {
   const int N = MODE == MODE_FWD ? G::cout : MODE == MODE_DGRAD ? G::cin : G::kdim;
   if (M == 0) return 0;
   const int tiles = ceil_div(M, BM) * ceil_div(N, BN);
-  dim3 grid(tiles, MODE == MODE_WGRAD ? a.splits : 1, nets * NCLS);
+  // DGRAD: (tile, class) in x; WGRAD: (split, tile) in x
+  dim3 grid(tiles * NCLS * (MODE == MODE_WGRAD ? a.splits : 1), 1, nets);
   const char *name = nullptr;
   if (tim_active())
     name = intern_name("conv_kernel<%dx%dx%d k%d s%d, %s, %s, %d>", G::hin, G::win, G::cin, G::k,

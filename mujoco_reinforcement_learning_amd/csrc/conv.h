@@ -18,7 +18,7 @@
 //            M = img*(HIN/ST)*(WIN/ST), N = CIN, K = (KS/ST)^2 * COUT -- no zero taps except at
 //            the borders; A gathered from dz, B gathered from W
 //   WGRAD  dW[co, k] = sum_{img, p} dz[img, p, co] im2col(x)[img, p, k]   (+ db = sum dz)
-//            M = COUT, N = KS*KS*CIN, K = img*P split over blockIdx.y; one f32 slab per split in
+//            M = COUT, N = KS*KS*CIN, K = img*P split over workgroups; one f32 slab per split in
 //            torch order, reduced in a fixed order afterwards (deterministic)
 // The last layer's output (the flattened features) is written f32 in torch's CHW flatten order
 // [img][co*P + p], which is what the first Linear layer expects, and its gradient arrives in the
@@ -168,7 +168,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
   static_assert(BK % 16 == 0, "BK");
   __shared__ __attribute__((aligned(16))) char lds[2 * (IA::BYTES + IB::BYTES)];
 
-  const int z = static_cast<int>(blockIdx.z) / NCLS, cls = static_cast<int>(blockIdx.z) % NCLS;
+  // DGRAD: blockIdx.x enumerates (tile, stride-phase class).  The s^2 classes of one row tile read
+  // the same images' dz, so they run on one XCD at the same time (blocks b, b + 8, ... share an
+  // XCD and its L2): dz streams from HBM once per launch instead of once per class.
+  const int z = static_cast<int>(blockIdx.z);
+  int cls = 0, bx = static_cast<int>(blockIdx.x);
+  if constexpr (NCLS > 1) {
+    const int tiles_all = ((q.nimg * G::hq * G::wq + BM - 1) / BM) * ((G::cin + BN - 1) / BN);
+    const int b = bx;
+    if (tiles_all % 8 == 0) {
+      cls = (b / 8) % NCLS;
+      bx = (b % 8) + 8 * (b / (8 * NCLS));
+    } else {
+      cls = b % NCLS;
+      bx = b / NCLS;
+    }
+  }
   const int py = cls / G::s, px = cls % G::s;
   const ConvNet &Nt = q.net[z];
   const TIN *const xin = static_cast<const TIN *>(Nt.in);
@@ -177,12 +192,35 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
   constexpr int N = MODE == MODE_FWD ? G::cout : MODE == MODE_DGRAD ? G::cin : G::kdim;
   const int K = MODE == MODE_FWD ? G::kdim
               : MODE == MODE_DGRAD ? G::tk * G::tk * G::cout : q.nimg * G::P;
-  int tile_m, tile_n;
-  if (!xcd_tile(static_cast<int>(blockIdx.x), (M + BM - 1) / BM, (N + BN - 1) / BN, tile_m, tile_n))
-    return;
+  int tile_m, tile_n, wsplit = 0;
+  if constexpr (NCLS > 1) {  // the class map above already groups a tile's work on one XCD
+    const int tn = (N + BN - 1) / BN;
+    if (bx >= ((M + BM - 1) / BM) * tn) return;
+    tile_m = bx / tn;
+    tile_n = bx - tile_m * tn;
+  } else if constexpr (MODE == MODE_WGRAD) {
+    // blockIdx.x enumerates (split, tile): every tile of a split reads the same positions' dz and
+    // frames, so they go to one XCD (split s on XCD s % 8) -- the layer's dz and inputs stream from
+    // HBM once per launch instead of once per tile
+    const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN, tiles = tm * tn;
+    if (bx >= tiles * q.splits) return;
+    int id;
+    if (q.splits % 8 == 0) {
+      const int x = bx % 8, j = bx / 8;
+      wsplit = x + 8 * (j / tiles);
+      id = j % tiles;
+    } else {
+      wsplit = bx / tiles;
+      id = bx % tiles;
+    }
+    tile_m = id / tn;
+    tile_n = id - tile_m * tn;
+  } else {
+    if (!xcd_tile(bx, (M + BM - 1) / BM, (N + BN - 1) / BN, tile_m, tile_n)) return;
+  }
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   int kbeg = 0, kend = K;
-  const int split = MODE == MODE_WGRAD ? static_cast<int>(blockIdx.y) : 0;
+  const int split = MODE == MODE_WGRAD ? wsplit : 0;
   if (MODE == MODE_WGRAD) {
     kbeg = static_cast<int>((static_cast<int64_t>(split) * K) / q.splits);
     kend = static_cast<int>((static_cast<int64_t>(split + 1) * K) / q.splits);
