@@ -355,6 +355,12 @@ int launch_conv(const ConvArgs &a, int nets, hipStream_t st) {
               : MODE == MODE_DGRAD ? a.nimg * G::hq * G::wq : G::cout;
   const int N = MODE == MODE_FWD ? G::cout : MODE == MODE_DGRAD ? G::cin : G::kdim;
   if (M == 0) return 0;
+  if constexpr (MODE == MODE_WGRAD) {
+    const int64_t per_split = ceil_div(static_cast<int64_t>(a.nimg) * G::P, a.splits);
+    PPO_REQUIRE(per_split / G::P + 2 <= kWgradMaxFrames,
+                "conv wgrad: %lld positions per split span more than %d frames",
+                static_cast<long long>(per_split), kWgradMaxFrames);
+  }
   const int tiles = ceil_div(M, BM) * ceil_div(N, BN);
   // DGRAD: (tile, class) in x; WGRAD: (split, tile) in x
   dim3 grid(tiles * NCLS * (MODE == MODE_WGRAD ? a.splits : 1), 1, nets);

@@ -56,6 +56,7 @@ using L3 = Geo<9, 9, 64, 64, 3, 1>;    // -> 7x7x64 = 3136 features
 constexpr int kFeatures = L3::P * L3::cout;
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+constexpr int kWgradMaxFrames = 1024;  // frames one WGRAD split may span (host-checked)
 
 struct ConvNet {
   const void *in;       // layer input: u8 pixel frames (through rows) / bf16 / f32 HWC
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
   constexpr int NCLS = MODE == MODE_DGRAD ? G::s * G::s : 1;
   static_assert(BK % 16 == 0, "BK");
   __shared__ __attribute__((aligned(16))) char lds[2 * (IA::BYTES + IB::BYTES)];
+  __shared__ int sframe[MODE == MODE_WGRAD ? kWgradMaxFrames : 1];  // WGRAD: the split's rows[]
 
   // DGRAD: blockIdx.x enumerates (tile, stride-phase class).  The s^2 classes of one row tile read
   // the same images' dz, so they run on one XCD at the same time (blocks b, b + 8, ... share an
@@ -233,6 +235,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
   auto field = [&](int img, int p) -> const TIN * {
     const int oy = p / G::wout, ox = p - oy * G::wout;
     const int64_t frame = q.rows ? static_cast<int64_t>(q.rows[img]) : img;
+    return xin + frame * (G::PIN * G::cin) + (G::s * oy * G::win + G::s * ox) * G::cin;
+  };
+  // WGRAD over minibatch frames (the pixel layer): the split's frame indices rows[img] staged in
+  // LDS once, so a k-tile's im2col gathers are one global round trip, not a dependent index load
+  // followed by the pixel load
+  int img0 = 0;
+  if constexpr (MODE == MODE_WGRAD) {
+    if (q.rows) {
+      img0 = kbeg / G::P;
+      const int nimg_split = (kend > kbeg ? (kend - 1) / G::P : img0) - img0 + 1;
+      for (int i = tid; i < nimg_split; i += NT) sframe[i] = q.rows[img0 + i];
+      __syncthreads();  // uniform (q.rows is a kernel argument)
+    }
+  }
+  auto field_w = [&](int img, int p) -> const TIN * {
+    const int oy = p / G::wout, ox = p - oy * G::wout;
+    const int64_t frame = q.rows ? static_cast<int64_t>(sframe[img - img0]) : img;
     return xin + frame * (G::PIN * G::cin) + (G::s * oy * G::win + G::s * ox) * G::cin;
   };
   // 4 consecutive reduction columns c..c+3 of an im2col row (one window row: contiguous)
@@ -323,7 +342,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvArgs q) {
         const int kr = k0 + kk, c = n0 + rr;
         const bool ok = kr < kend && c < N;
         const int kc = ok ? kr : kbeg;
-        im2col4(field(kc / G::P, kc % G::P), ok ? c : 0, vb[u]);
+        im2col4(field_w(kc / G::P, kc % G::P), ok ? c : 0, vb[u]);
         mask4(ok, vb[u]);
       }
     }
