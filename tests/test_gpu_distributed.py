@@ -88,10 +88,15 @@ def test_exact_dp_two_ranks_match_single_process(gpu):
     assert_params_match(got[0][0], p_single, g_single, agent, 1e-4, label="exact DP x2")
 
 
-def _local_worker(rank, world, port, q):
-    """Weak-scaling ("local") data parallel on the fused bf16 path: each rank its own env shard
-    and Philox shuffles; per step the fused gradient, the all-reduce, Adam + images + next
-    gather.  Returns the parameters after two iterations and the kernels that ran."""
+_LOCAL_SHAPES = {  # name -> (hidden, obs, act)
+    "fused": ((256, 256), 17, 6),           # fused_update_kernel (HalfCheetah shapes)
+    "wide": ((512, 512, 512), 376, 17)}     # the wide bf16 path (Humanoid, BASELINE configs[3])
+
+
+def _local_worker(rank, world, port, q, shape="fused"):
+    """Weak-scaling ("local") data parallel on the bf16 paths: each rank its own env shard and
+    Philox shuffles; per step the gradient, the all-reduce, Adam (+ images + next gather on the
+    fused path).  Returns the parameters after two iterations and the kernels that ran."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
@@ -101,9 +106,10 @@ def _local_worker(rank, world, port, q):
     from mujoco_reinforcement_learning_amd.runconfig import make_run
     dev = torch.device("cuda", 0)
     n, t, b = 64, 16, 256
-    s = make_synthetic_streams(n, t, 17, seed=31 + rank, p_terminate=0.05, device=dev)
-    run = make_run(num_envs=n, horizon=t, hidden=(256, 256), batch_size=b, epochs=2,
-                   rng="philox", seed=rank, dp_mode="local", precision="bf16")
+    hidden, obs, act = _LOCAL_SHAPES[shape]
+    s = make_synthetic_streams(n, t, obs, seed=31 + rank, p_terminate=0.05, device=dev)
+    run = make_run(num_envs=n, horizon=t, hidden=hidden, batch_size=b, epochs=2, obs_dim=obs,
+                   act_dim=act, rng="philox", seed=rank, dp_mode="local", precision="bf16")
     torch.manual_seed(0)
     agent = PPOEngineAgent(run, device=dev)
     algo = PPOEngine(SyntheticVecEnvHelper(s, run, device=dev), agent, log=lambda m: None)
@@ -119,14 +125,15 @@ def _local_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-def test_local_dp_two_ranks_fused_replicas_agree(gpu):
+@pytest.mark.parametrize("shape", ["fused", "wide"])
+def test_local_dp_two_ranks_fused_replicas_agree(gpu, shape):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, q, shape)) for r in range(2)]
     for p in procs:
         p.start()
     got = {}
@@ -140,6 +147,11 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu):
     assert torch.equal(got[0][0], got[1][0])
     assert all(abs(x) < 1e6 for x in got[0][2])
     kernels, fold = got[0][1]
+    if shape == "wide":  # layered bf16-resident GEMMs, the fixed-order slab fold, Adam
+        assert any(k.startswith("wide_gemm_kernel") for k in kernels), kernels
+        assert "wide_reduce_kernel" in kernels and "wide_policy_fused_kernel" in kernels, kernels
+        assert not any(k.startswith("fused_update_kernel") for k in kernels), kernels
+        return
     # the data-parallel optimizer step: the fused kernel (slabs folded to the flat gradient in
     # the same launch, or by reduce_slabs_kernel without the in-launch fold), the all-reduce,
     # then ONE tail launch: Adam + weight images + the next minibatch's gather
