@@ -717,28 +717,73 @@ __device__ __forceinline__ void frag_load(const __bf16 *wf, int tiles, int ot0, 
     }
 }
 
-// acc[t] += W[tile ot0 + t] . img^T over the layer's k-steps
-template <int NT>
+// acc[t][u] += W[tile ot0 + t] . img[rows 32u..32u+31]^T over the layer's k-steps
+template <int NT, int RT>
 __device__ __forceinline__ void fused_layer(const __bf16 *wf, int tiles, int ks, int ot0,
-                                            const char *img, int lane, wide::f32x16 (&acc)[2]) {
+                                            const char *img, int lane,
+                                            wide::f32x16 (&acc)[2][RT]) {
   const int ng = ks / kFGroup;
   const int row = lane & 31, h = lane >> 5;
   wide::bf16x8 cur[kFGroup][2], nxt[kFGroup][2];
   frag_load<NT>(wf, tiles, ot0, 0, lane, cur);
   for (int g = 0; g < ng; ++g) {
-    if (g + 1 < ng) frag_load<NT>(wf, tiles, ot0, g + 1, lane, nxt);
+    // unconditional (the last group re-reads itself): a load behind the g + 1 < ng test would
+    // make the compiler wait for it at the branch merge, exposing the L2 latency every group
+    frag_load<NT>(wf, tiles, ot0, g + 1 < ng ? g + 1 : g, lane, nxt);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's MFMAs
 #pragma unroll
     for (int s = 0; s < kFGroup; ++s) {
       const int k16 = g * kFGroup + s;
-      const wide::bf16x8 bv = *reinterpret_cast<const wide::bf16x8 *>(img + fimg_off(row, 2 * k16 + h));
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[s][t], bv, acc[t], 0, 0, 0);
+      for (int u = 0; u < RT; ++u) {
+        const wide::bf16x8 bv =
+            *reinterpret_cast<const wide::bf16x8 *>(img + fimg_off(32 * u + row, 2 * k16 + h));
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[s][t], bv, acc[t][u], 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int s = 0; s < kFGroup; ++s)
 #pragma unroll
       for (int t = 0; t < 2; ++t) cur[s][t] = nxt[s][t];
+  }
+}
+
+// One hidden layer of a fused workgroup over RT row tiles: wave w's feature tiles 2w, 2w + 1,
+// bias + ReLU, bf16 4-feature runs into the dst image.
+template <int RT>
+__device__ __forceinline__ void fused_hidden(const WideFusedNet &N, int l, const char *src,
+                                             char *dst, int w, int lane) {
+  const int tiles = N.tiles[l];
+  const int ot0 = 2 * w;
+  wide::f32x16 acc[2][RT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < RT; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+  if (ot0 + 1 < tiles) fused_layer<2, RT>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
+  else if (ot0 < tiles) fused_layer<1, RT>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
+  const int row = lane & 31;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (ot0 + t >= tiles) continue;  // uniform per wave
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int o = 32 * (ot0 + t) + 8 * g + 4 * (lane >> 5);
+      const float4 bv = N.b[l] ? *reinterpret_cast<const float4 *>(N.b[l] + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < RT; ++u) {
+        const float y0 = act_forward(acc[t][u][4 * g] + bv.x, PPO_ACT_RELU);
+        const float y1 = act_forward(acc[t][u][4 * g + 1] + bv.y, PPO_ACT_RELU);
+        const float y2 = act_forward(acc[t][u][4 * g + 2] + bv.z, PPO_ACT_RELU);
+        const float y3 = act_forward(acc[t][u][4 * g + 3] + bv.w, PPO_ACT_RELU);
+        *reinterpret_cast<uint2 *>(dst + fimg_off(32 * u + row, o >> 3) + 2 * (o & 7)) =
+            make_uint2(wide::pack2(y0, y1), wide::pack2(y2, y3));
+      }
+    }
   }
 }
 
@@ -773,46 +818,19 @@ __global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q)
   __syncthreads();
   int cur = 0;
   for (int l = 0; l < N.n_hidden; ++l) {
-    const int tiles = N.tiles[l];
-    const int ot0 = 2 * w;
-    wide::f32x16 acc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-    const char *src = lds + cur * kFRows * kFPitch;
-    char *dst = lds + (cur ^ 1) * kFRows * kFPitch;
-    if (ot0 + 1 < tiles) fused_layer<2>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
-    else if (ot0 < tiles) fused_layer<1>(N.wf[l], tiles, N.ks[l], ot0, src, lane, acc);
-    // epilogue: bias + ReLU, bf16 4-feature runs of row (lane & 31)
-    const int row = lane & 31;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (ot0 + t >= tiles) continue;  // uniform per wave
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int o = 32 * (ot0 + t) + 8 * g + 4 * (lane >> 5);
-        const float4 bv = N.b[l] ? *reinterpret_cast<const float4 *>(N.b[l] + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float y0 = act_forward(acc[t][4 * g] + bv.x, PPO_ACT_RELU);
-        const float y1 = act_forward(acc[t][4 * g + 1] + bv.y, PPO_ACT_RELU);
-        const float y2 = act_forward(acc[t][4 * g + 2] + bv.z, PPO_ACT_RELU);
-        const float y3 = act_forward(acc[t][4 * g + 3] + bv.w, PPO_ACT_RELU);
-        *reinterpret_cast<uint2 *>(dst + fimg_off(row, o >> 3) + 2 * (o & 7)) =
-            make_uint2(wide::pack2(y0, y1), wide::pack2(y2, y3));
-      }
-    }
+    fused_hidden<1>(N, l, lds + cur * kFRows * kFPitch, lds + (cur ^ 1) * kFRows * kFPitch, w, lane);
     __syncthreads();
     cur ^= 1;
   }
   // ---- head pre-activations (<= 32 outputs) on wave 0 ----
   const int L = N.n_hidden;
   if (w == 0) {
-    wide::f32x16 acc[2];
+    wide::f32x16 acc[2][1];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
-    fused_layer<1>(N.wf[L], N.tiles[L], N.ks[L], 0, lds + cur * kFRows * kFPitch, lane, acc);
+    for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
+    fused_layer<1, 1>(N.wf[L], N.tiles[L], N.ks[L], 0, lds + cur * kFRows * kFPitch, lane, acc);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) zt[lane & 31][(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = acc[0][r];
+    for (int r = 0; r < 16; ++r) zt[lane & 31][(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = acc[0][0][r];
   }
   __syncthreads();
   const int row = tid >> 4, j = r0 + row;
@@ -850,6 +868,118 @@ __global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q)
     const float v = zt[row][0];
     q.value[j] = N.b[L] ? v + N.b[L][0] : v;
   }
+}
+
+// Minibatch forward of the wide path in one launch per optimizer step (ppo.py:109-115): both
+// nets' hidden layers and head pre-activations for 64 minibatch rows per workgroup, the activations
+// kept in LDS between layers (each layer's input is read from LDS, not HBM) and each hidden output
+// copied out once, as the backward's operand -- the three FWD GEMM launches and the head GEMM of
+// the layered forward, whose layer inputs made a round trip through HBM.  Same per-layer arithmetic
+// as the rollout kernel above; rows at or past the device row count are written as zeros (the
+// padding contract of wide_gemm.h).
+constexpr int kFwdRows = 64;
+struct WideFwdArgs {
+  WideFusedNet net[2];
+  const __bf16 *x;
+  int ldx, rows_pad, b;
+  const int32_t *rows_n;
+  __bf16 *h[2][PPO_MAX_LAYERS];
+  int ldh[2][PPO_MAX_LAYERS];
+  float *z[2];  // [rows][32]
+};
+
+__global__ __launch_bounds__(512) void wide_forward_fused_kernel(WideFwdArgs q) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kFwdRows * kFPitch];
+  const int nb = q.rows_pad / kFwdRows, b = static_cast<int>(blockIdx.x);
+  int z, rb;
+  if (nb % 4 == 0) {  // actor on XCDs 0-3, critic on 4-7 (one net's weights per L2)
+    const int x = b % 8;
+    z = x / 4;
+    rb = (x % 4) + 4 * (b / 8);
+  } else {
+    z = b / nb;
+    rb = b % nb;
+  }
+  const WideFusedNet &N = q.net[z];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = rb * kFwdRows;
+  const int count = q.rows_n ? *q.rows_n : q.b;
+  const int cpr = q.ldx / 8;
+  for (int e = tid; e < kFwdRows * cpr; e += 512) {
+    const int row = e / cpr, c = e - row * cpr;
+    const uint4 v = *reinterpret_cast<const uint4 *>(q.x + static_cast<int64_t>(r0 + row) * q.ldx + 8 * c);
+    *reinterpret_cast<uint4 *>(lds + fimg_off(row, c)) = v;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < N.n_hidden; ++l) {
+    char *dst = lds + (cur ^ 1) * kFwdRows * kFPitch;
+    fused_hidden<2>(N, l, lds + cur * kFwdRows * kFPitch, dst, w, lane);
+    __syncthreads();
+    // the layer's output rows out (16-B coalesced), zero past the device count
+    const int width = 32 * N.tiles[l], cw = width / 8, ld = q.ldh[z][l];
+    __bf16 *hout = q.h[z][l];
+    for (int e = tid; e < kFwdRows * cw; e += 512) {
+      const int row = e / cw, c = e - row * cw;
+      const uint4 v = *reinterpret_cast<const uint4 *>(dst + fimg_off(row, c));
+      *reinterpret_cast<uint4 *>(hout + static_cast<int64_t>(r0 + row) * ld + 8 * c) =
+          r0 + row < count ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+    cur ^= 1;  // the next layer reads dst and writes the other image (nobody reads it now)
+  }
+  // head pre-activations: waves 0 and 1, one 32-row tile each, in the head GEMM's k order
+  const int L = N.n_hidden;
+  if (w < 2) {
+    wide::f32x16 acc[2][1];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
+    fused_layer<1, 1>(N.wf[L], N.tiles[L], N.ks[L], 0,
+                      lds + cur * kFwdRows * kFPitch + 32 * w * kFPitch, lane, acc);
+    const int row = r0 + 32 * w + (lane & 31);
+    const bool live = row < count;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int o = 8 * g + 4 * (lane >> 5);
+      *reinterpret_cast<float4 *>(q.z[z] + static_cast<int64_t>(row) * 32 + o) =
+          live ? make_float4(acc[0][0][4 * g], acc[0][0][4 * g + 1], acc[0][0][4 * g + 2], acc[0][0][4 * g + 3])
+               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+static int wide_forward_fused(ppo_ctx *ctx, int rows_pad, int b, const int32_t *count_d,
+                              hipStream_t st) {
+  WideWork &W = *ctx->wide;
+  WideFwdArgs q{};
+  double flops = 0;
+  for (int z = 0; z < 2; ++z) {
+    const NetDesc &nd = ctx->net[z];
+    const WideNetWork &wn = W.net[z];
+    WideFusedNet &f = q.net[z];
+    f.n_hidden = nd.n_hidden;
+    for (int l = 0; l <= nd.n_hidden; ++l) {
+      const LayerDesc &L = nd.layer[l];
+      f.wf[l] = wn.wf[l];
+      f.b[l] = L.b_off >= 0 ? ctx->params + L.b_off : nullptr;
+      f.tiles[l] = wn.wf_tiles[l];
+      f.ks[l] = wn.wf_ks[l];
+      flops += 2.0 * rows_pad * L.out * L.in;
+      if (l < nd.n_hidden) {
+        q.h[z][l] = wn.h[l];
+        q.ldh[z][l] = wn.ldh[l];
+      }
+    }
+    q.z[z] = wn.z;
+  }
+  q.x = W.x;
+  q.ldx = W.ldx;
+  q.rows_pad = rows_pad;
+  q.b = b;
+  q.rows_n = count_d;
+  launch_k(TimRec{KC_GEMM_FWD, "wide_forward_fused_kernel", flops, 0.0}, wide_forward_fused_kernel,
+           dim3(2 * (rows_pad / kFwdRows)), dim3(512), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
 }
 
 static int wide_policy_fused(ppo_ctx *ctx, const bool use[2], int n, const float *eps_d,
@@ -1085,10 +1215,14 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   const int64_t P = ctx->total_params;
   const int A = ctx->cfg.act_dim;
   NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
-  if (int rc = wide_pack(ctx, st, false)) return rc;
+  if (int rc = wide_pack(ctx, st, W.fused_rollout)) return rc;
   if (int rc = stage_rows(ctx, states_d, rows_d, count_d, b, rows_pad, st)) return rc;
   const bool both[2] = {true, true};
-  if (int rc = forward(ctx, both, rows_pad, count_d, st)) return rc;
+  if (W.fused_rollout) {  // one launch: hidden layers + heads, activations LDS-resident
+    if (int rc = wide_forward_fused(ctx, rows_pad, b, count_d, st)) return rc;
+  } else if (int rc = forward(ctx, both, rows_pad, count_d, st)) {
+    return rc;
+  }
 
   // ---- loss heads -----------------------------------------------------------------------------
   const int blocks = ceil_div(rows_pad, kWideLossRows);
