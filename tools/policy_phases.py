@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 PHASES = ["prologue: obs / param / eps loads issued, Philox noise", "LDS images + raw window out",
-          "per-(row, slice) f64 mean / std (wave 0)", "standardised states -> X image + state out",
+          "per-(row, slice) f64 mean / std (lane-parallel butterflies)", "standardised states -> X image + state out",
           "L0 MFMA + act -> A1", "L1 MFMA pass (issue)", "act -> A2 image",
           "heads (tanh, sample, logp / value) + writes"]
 
@@ -34,7 +34,7 @@ def main():
         e.observe_act(win, st, obs=obs, seed=1, offset=rep, action=a, logp=lp, value=v)
         # the policy kernel writes 11 slots per workgroup (phase_stamps views them as 13)
         s = e.phase_stamps(False).flatten()[:2 * 128 * 11].view(2, 128, 11).double()
-    g = n // 64
+    g = n // 32  # 32-row workgroups
     for y, name in ((0, "actor"), (1, "critic")):
         rows = s[y, :g]
         tot = rows[:, 9].mean()
