@@ -153,20 +153,25 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   }
   __syncthreads();
   PSTAMP(2);
-  // ---- per-(row, slice) mean and std: wave 0, lane = row, row_stats.h (the layered A1
-  //      kernel's arithmetic, bit-identical) ----
-  if (q.normalize && tid < RP) {
-    double x[kFusedKX];  // the row in registers: the slice loops below are unrolled over f
-#pragma unroll
-    for (int f = 0; f < kFusedKX; ++f) x[f] = xd[tid * kPolicyXsPitch + f];
+  // ---- per-(row, slice) mean and std on every wave: lane = feature (lanes 0-31 and 32-63 are
+  //      two rows), each wave 4 rows as two interleaved chains.  row_stats.h's pairwise tree over
+  //      the 32 slots is a DPP / permlane butterfly across the 32 lanes (slice_stats_lanes), so
+  //      mean / std are bitwise the layered A1 kernel's ----
+  static_assert(4 * NW == RP, "four rows per wave");
+  if (q.normalize) {
+    const int f = lane & 31;
+    const int ra = 4 * w + 2 * (lane >> 5), rb = ra + 1;  // the two rows of this lane
+    const double xa = xd[ra * kPolicyXsPitch + f], xb = xd[rb * kPolicyXsPitch + f];
     for (int sl = 0; sl < q.tab.count; ++sl) {
       const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
-      if (hi - lo <= 0) continue;
-      // row_stats.h: the layered A1 kernel's exact arithmetic (pairwise trees, depth 5)
-      const SliceStats ss = slice_stats32(x, lo, hi);
-      const double mean = ss.mean, sd = ss.sd;
-      st[(tid * 16 + sl) * 2] = mean;
-      st[(tid * 16 + sl) * 2 + 1] = sd;
+      if (hi - lo <= 0) continue;  // uniform
+      const SliceStats2 s2 = slice_stats_lanes(xa, xb, f >= lo && f < hi, hi - lo);
+      if (f == 0) {
+        st[(ra * 16 + sl) * 2] = s2.mean[0];
+        st[(ra * 16 + sl) * 2 + 1] = s2.sd[0];
+        st[(rb * 16 + sl) * 2] = s2.mean[1];
+        st[(rb * 16 + sl) * 2 + 1] = s2.sd[1];
+      }
     }
   }
   __syncthreads();

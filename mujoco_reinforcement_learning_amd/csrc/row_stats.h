@@ -44,4 +44,68 @@ __device__ __forceinline__ SliceStats slice_stats32(const double (&x)[32], int l
   return SliceStats{mean, sd};
 }
 
+// The same statistics with the row spread over 32 lanes (lane = slot, `in` = slot inside the
+// slice), two rows per lane interleaved.  tree32's pairwise tree is a butterfly: after level k
+// every lane of a 2^k-lane group holds that group's sum (its two halves added in the tree's order
+// on the group's first lane, commuted elsewhere: the same value), so any partner lane in the
+// sibling group gives the tree's next sum.  Partners on the VALU, no LDS round trips: quad_perm
+// xor 1 and xor 2, row_half_mirror (sibling quad), row_ror:8 (sibling 8-lane half of a row), then
+// v_permlane16_swap between the 16-lane rows of each 32-lane half (summed as row 0 + row 1: the
+// tree's order on every lane).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
+                                                     static_cast<uint32_t>(lo)));
+}
+__device__ __forceinline__ double rows16_pair_sum(double v) {  // row0 + row1 of each 32-lane half
+  const uint64_t u = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(u), static_cast<uint32_t>(u), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(u >> 32), static_cast<uint32_t>(u >> 32), false, false);
+  const double p0 = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi[0]) << 32) | lo[0]));
+  const double p1 = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi[1]) << 32) | lo[1]));
+  return p0 + p1;  // row-0 lanes: own + row-1 partner; row-1 lanes: row-0 partner + own
+}
+__device__ __forceinline__ void butterfly2(double &a, double &b) {
+  a = a + dpp_d<0xB1>(a);   // quad_perm [1,0,3,2]
+  b = b + dpp_d<0xB1>(b);
+  a = a + dpp_d<0x4E>(a);   // quad_perm [2,3,0,1]
+  b = b + dpp_d<0x4E>(b);
+  a = a + dpp_d<0x141>(a);  // row_half_mirror: the sibling quad
+  b = b + dpp_d<0x141>(b);
+  a = a + dpp_d<0x128>(a);  // row_ror:8: the other 8 lanes of the row
+  b = b + dpp_d<0x128>(b);
+  a = rows16_pair_sum(a);
+  b = rows16_pair_sum(b);
+}
+
+struct SliceStats2 {
+  double mean[2], sd[2];
+};
+
+__device__ __forceinline__ SliceStats2 slice_stats_lanes(double xa, double xb, bool in, int cnt) {
+  SliceStats2 r;
+  double ta = in ? xa : 0.0, tb = in ? xb : 0.0;
+  butterfly2(ta, tb);
+  const double ma = ta / cnt, mb = tb / cnt;
+  ta = in ? xa - ma : 0.0;
+  tb = in ? xb - mb : 0.0;
+  butterfly2(ta, tb);
+  const double ca = ta / cnt, cb = tb / cnt;
+  const double da = (xa - ma) - ca, db = (xb - mb) - cb;
+  ta = in ? da * da : 0.0;
+  tb = in ? db * db : 0.0;
+  butterfly2(ta, tb);
+  double sa = sqrt(ta / (cnt - 1)), sb = sqrt(tb / (cnt - 1));
+  if (sa == 0.0) sa = 1.0;
+  if (sb == 0.0) sb = 1.0;
+  r.mean[0] = ma;
+  r.mean[1] = mb;
+  r.sd[0] = sa;
+  r.sd[1] = sb;
+  return r;
+}
+
 }  // namespace ppo
