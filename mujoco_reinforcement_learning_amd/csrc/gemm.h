@@ -648,9 +648,20 @@ static int env_knob(const char *name, int dflt) {
 }
 static const int g_nbuf = env_knob("PPO_GEMM_NBUF", 2);
 static const int g_wide = env_knob("PPO_GEMM_WIDE", 0);
+// The 128x128 tiles as 8 waves of 64x32 (two waves per SIMD; PPO_GEMM_W8=0: 4 waves of 64x64) --
+// the occupancy that paid on the wide path's LDS-DMA GEMMs; measured here
+// (tools/ab_w8.sh): BiLSTM line +6 %, f32 leg +11 %, pixel CNN +2 %
+static const int g_w8 = env_knob("PPO_GEMM_W8", 1);
 
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_big(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+  if constexpr (TM == 2 && TN == 2 && WM == 2 && WN == 2) {
+    if (g_w8) {
+      if (g_nbuf == 1)
+        return launch_gemm<2, 1, 2, 4, AMODE, BMODE, EPI, 1>(gb, nprob, max_m, max_n, st);
+      return launch_gemm<2, 1, 2, 4, AMODE, BMODE, EPI, 2>(gb, nprob, max_m, max_n, st);
+    }
+  }
   if (g_nbuf == 1)
     return launch_gemm<TM, TN, WM, WN, AMODE, BMODE, EPI, 1>(gb, nprob, max_m, max_n, st);
   return launch_gemm<TM, TN, WM, WN, AMODE, BMODE, EPI, 2>(gb, nprob, max_m, max_n, st);
