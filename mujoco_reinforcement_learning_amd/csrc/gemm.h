@@ -648,11 +648,11 @@ static int env_knob(const char *name, int dflt) {
 }
 static const int g_nbuf = env_knob("PPO_GEMM_NBUF", 2);
 static const int g_wide = env_knob("PPO_GEMM_WIDE", 0);
-// PPO_GEMM_W8=1: the 128x128 tiles as 8 waves of 64x32 (two waves per SIMD) instead of 4 of
-// 64x64 -- the occupancy that paid on the wide path's LDS-DMA GEMMs; measured
-// (tools/ab_w8.sh): BiLSTM line +6 %, f32 leg +11 %, pixel CNN +2 %.  Off by default until the
-// parity suite has run with it on hardware.
-static const int g_w8 = env_knob("PPO_GEMM_W8", 0);
+// The 128x128 tiles as 8 waves of 64x32 (two waves per SIMD; PPO_GEMM_W8=0: 4 waves of 64x64) --
+// the occupancy that paid on the wide path's LDS-DMA GEMMs; measured
+// (tools/ab_w8.sh): BiLSTM line +6 %, f32 leg +11 %, pixel CNN +2 %; the GPU parity suite passes
+// with either (gpurun r03z / r03z2).
+static const int g_w8 = env_knob("PPO_GEMM_W8", 1);
 
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_big(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
