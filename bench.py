@@ -13,7 +13,7 @@ Also reported on the same JSON line:
                 HIP events on its dispatch packets (hipExtLaunchKernelGGL) recorded live:
                 algorithmic FLOPs or bytes per launch / mean launch time vs the MI355X peak;
                 `kernel` is its rocprofv3 name; `traffic` = PMC HBM bytes per launch from
-                profiles/traffic.json when present (same command under rocprofv3 --pmc)
+                bench_traffic.json when present (same command under rocprofv3 --pmc)
   gae_roofline  the same for the GAE scan (north-star >= 40 % HBM target)
   cpu_baseline  the oracle (oracle/ppo_ref.py, torch-CPU restatement of ppo.py) on a bounded
                 sample of the same workload, on rank 0 at N_gpus = 1 only
@@ -84,27 +84,36 @@ def parse():
     p.add_argument("--leg-steps", type=int, default=3, help="timed iterations per extra leg")
     p.add_argument("--no-graphs", action="store_true",
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "bench_traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+    p.add_argument("--legs", default="ant,humanoid,cnn,lstm",
+                   help="BASELINE-config legs the default N=1 line carries (comma list of ant, "
+                        "humanoid, cnn, lstm; empty for none)")
     args = p.parse_args()
+    apply_model_defaults(args, p.get_default)
+    return args
+
+
+MODEL_DEFAULTS = {
+    "lstm": {"num_envs": 1024, "obs_dim": 348, "act_dim": 17, "hidden": "256,256,128,128",
+             "batch": 16384, "window": 5},
+    "cnn": {"num_envs": 1024, "obs_dim": 84 * 84 * 3, "act_dim": 6, "batch": 16384},
+}
+
+
+def apply_model_defaults(args, default_of) -> None:
+    """The --model lstm / cnn workloads' shapes where the command line left the MLP defaults."""
+    for k, v in MODEL_DEFAULTS.get(args.model, {}).items():
+        if getattr(args, k) == default_of(k):
+            setattr(args, k, v)
     if args.model == "lstm":
-        defaults = {"num_envs": 1024, "obs_dim": 348, "act_dim": 17, "hidden": "256,256,128,128",
-                    "batch": 16384, "window": 5}
-        for k, v in defaults.items():
-            if getattr(args, k) == p.get_default(k):
-                setattr(args, k, v)
-        args.no_timing = True  # per-kernel times for this leg come from rocprofv3
+        args.no_timing = True  # the BiLSTM context has no per-kernel events: end-to-end roofline
         args.no_legs = True
         args.cpu_baseline = False
     if args.model == "cnn":
-        defaults = {"num_envs": 1024, "obs_dim": 84 * 84 * 3, "act_dim": 6, "batch": 16384}
-        for k, v in defaults.items():
-            if getattr(args, k) == p.get_default(k):
-                setattr(args, k, v)
         args.no_legs = True
     if args.window is None:
         args.window = 1
-    return args
 
 
 def load_traffic(path):
@@ -327,28 +336,212 @@ def leg(args, precision, env_kind, dev) -> dict:
     _progress(f"leg: precision {precision}, env {env_kind}")
     run, agent, helper, algo = build(args, precision, env_kind, dev, 0)
     try:
-        elapsed = time_iterations(algo, args.leg_steps, 1, 1, dev)
+        elapsed = time_iterations(algo, args.leg_steps, 2, 1, dev)  # eager, then graph capture
     finally:
         if hasattr(helper, "close"):
             helper.close()
     n, t = args.num_envs, args.horizon
     return {"value": n * t * args.leg_steps / elapsed, "unit": "env-steps/s",
             "ms_per_step": 1000 * elapsed / args.leg_steps, "steps": args.leg_steps,
-            "warmup": 1, "precision": precision,
+            "warmup": 2, "precision": precision,
             "env": ("device (synthetic dynamics on the GPU)" if env_kind == "device" else
                     f"host pool ({args.env_workers} worker processes in 2 groups, page-locked "
                     "device-mapped shared memory: obs / reward / terminated read and actions "
                     "written over PCIe every step, pipelined by ppo_host_rollout)")}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """``bench.py --gpus N`` started as one plain process: start N rank processes of this same
+    command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their env,
+    as torch.distributed.run would set them), forward rank 0's JSON line, and return non-zero if
+    any rank fails.  This parent never touches the GPU (no HIP call before or after the
+    children start), and when one rank dies the others are terminated by their own PIDs rather
+    than left waiting in a collective."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    import threading
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rcs = [None] * n
+    # reap in completion order; after the first failure terminate the rest
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0):
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+        time.sleep(0.05)
+    reader.join(timeout=10)
+    # rank 0's JSON line to stdout; library chatter (e.g. gloo's connection lines) to stderr
+    for ln in b"".join(chunks).decode().splitlines():
+        print(ln, file=sys.stdout if ln.startswith("{") else sys.stderr)
+    sys.stdout.flush()
+    bad = [(i, rc) for i, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        _progress(f"rank(s) failed: {bad}")
+        return 1
+    return 0
+
+
+def launch_check(args, world, rank) -> None:
+    """PPO_BENCH_LAUNCH_CHECK=1 (CPU tests of the launcher): the rank plumbing of main() -- gloo
+    rendezvous, barrier-bracketed timing, max over ranks, rank 0's JSON line -- with no GPU work.
+    PPO_BENCH_LAUNCH_CHECK_FAIL_RANK=r makes rank r exit with status 3 before the rendezvous (the
+    launcher must then stop the other ranks and fail)."""
+    if os.environ.get("PPO_BENCH_LAUNCH_CHECK_FAIL_RANK") == str(rank):
+        sys.exit(3)
+    torch.distributed.init_process_group("gloo")
+    t0 = time.perf_counter()
+    torch.distributed.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "launch_check": True}), flush=True)
+    torch.distributed.destroy_process_group()
+
+
+def _macs_per_row(agent) -> int:
+    """Forward multiply-accumulates per row of both nets, counted from the modules: Linear
+    in*out; LSTM per layer and direction W * 4H * (in + H) over the window (the recurrent GEMMs
+    run once per window slot)."""
+    window = agent.run.environment_config.window_length
+    macs = 0
+    for m in agent.networks.modules():
+        if isinstance(m, torch.nn.Linear):
+            macs += m.in_features * m.out_features
+        elif isinstance(m, torch.nn.LSTM):
+            dirs = 2 if m.bidirectional else 1
+            for layer in range(m.num_layers):
+                inp = m.input_size if layer == 0 else m.hidden_size * dirs
+                macs += dirs * window * 4 * m.hidden_size * (inp + m.hidden_size)
+    return macs
+
+
+# BASELINE.json configs carried as legs of the default line (their own metric strings)
+CONFIG_LEGS = {
+    "ant": dict(model="mlp", num_envs=4096, obs_dim=27, act_dim=8, hidden="256,256", batch=65536,
+                window=1, baseline="configs[2] Ant-v4, 4096 envs, 2x256 MLP, 1x MI355X"),
+    # configs[3]: 8192 envs over 8 GPUs = 1024 envs per rank; global minibatch 65,536 = 8 ranks x
+    # B_local 8,192, i.e. 16 minibatches per epoch (local data parallelism divides each rank's
+    # loss by B_local * world, so the all-reduced gradient is the global-minibatch mean)
+    "humanoid": dict(model="mlp", num_envs=1024, obs_dim=376, act_dim=17, hidden="512,512,512",
+                     batch=8192, window=1,
+                     baseline="configs[3] Humanoid-v4, 8192 envs, 3x512 MLP, 8x MI355X env-sharded: "
+                              "one rank's shard (1024 envs, B_local 8192 of the global 65,536)"),
+    "cnn": dict(model="cnn", baseline="configs[4] dm_control cheetah-run 84x84x3 pixels, 1024 "
+                                      "envs, Nature-DQN CNN encoder, 1x MI355X"),
+    "lstm": dict(model="lstm", baseline="the reference PPOAgent's BiLSTM actor-critic on main.py's "
+                                        "network (O=348, W=5, latent 256, [256,256,128,128], A=17), "
+                                        "1024 envs, 1x MI355X"),
+}
+
+
+def config_leg(args, name, dev, steps=None, **over) -> dict:
+    """One BASELINE-config leg on this GPU: its own workload, metric string, ms_per_step and
+    roofline (the leg's dominant kernel from live events, or -- for the BiLSTM context, which has
+    no per-kernel events -- the whole iteration's algorithmic FLOPs against the bf16 peak)."""
+    spec = dict(CONFIG_LEGS[name], **over)
+    baseline = spec.pop("baseline")
+    ns = argparse.Namespace(**vars(args))
+    ns.model = spec.pop("model")
+    for k in ("num_envs", "obs_dim", "act_dim", "hidden", "batch", "window", "horizon", "epochs"):
+        setattr(ns, k, parse_defaults[k])
+    ns.window, ns.no_timing = None, False
+    for k, v in spec.items():
+        setattr(ns, k, v)
+    apply_model_defaults(ns, parse_defaults.get)
+    steps = steps or args.leg_steps
+    _progress(f"leg {name}: {ns.num_envs} envs, obs {ns.obs_dim}, act {ns.act_dim}, "
+              f"hidden {ns.hidden}, B {ns.batch}, model {ns.model}")
+    run, agent, helper, algo = build(ns, ns.precision, "device", dev, 0)
+    try:
+        elapsed = time_iterations(algo, steps, 2, 1, dev)  # warm-up 2: eager, then graph capture
+        kernels = {}
+        if hasattr(agent.engine, "timing"):
+            ec = run.engine_config
+            ec.rollout_graph, ec.train_graph = False, False
+            agent.engine.timing(True, capacity=400000)
+            algo._iterate()
+            torch.cuda.synchronize()
+            kernels = agent.engine.timing_kernels()
+            agent.engine.timing(False)
+        macs = _macs_per_row(agent)
+    finally:
+        if hasattr(helper, "close"):
+            helper.close()
+    n, t = ns.num_envs, ns.horizon
+    hidden = tuple(int(h) for h in ns.hidden.split(","))
+    out = {"metric": leg_metric(ns, hidden, 1), "baseline_config": baseline,
+           "value": n * t * steps / elapsed, "unit": "env-steps/s",
+           "ms_per_step": 1000 * elapsed / steps, "steps": steps, "warmup": 2,
+           "dtype": ns.precision, "workload": workload(ns, hidden),
+           "minibatches_per_epoch": n * t // ns.batch}
+    flop_step = (2 + 6 * ns.epochs) * macs  # SURVEY s8(d): 2F rollout + E x 3 x 2F update
+    e2e = flop_step * n * t * steps / elapsed / 1e12
+    out["end_to_end"] = {"flop_per_env_step": flop_step, "achieved": e2e, "unit": "TFLOP/s",
+                         "peak": PEAK_BF16_MFMA_TFLOPS, "frac": e2e / PEAK_BF16_MFMA_TFLOPS}
+    if kernels:
+        kname, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])
+        out["roofline"] = roofline(kname, c, load_traffic(args.traffic))
+        out["kernels_ms_per_step"] = {k: round(v["ms"], 4) for k, v in
+                                      sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:8]}
+    else:
+        out["roofline"] = dict(out["end_to_end"], bound="mfma", kernel="whole iteration (no "
+                               "per-kernel events in this context)", traffic=None)
+    del algo, agent, helper, run
+    torch.cuda.empty_cache()
+    return out
+
+
+def leg_metric(ns, hidden, world) -> str:
+    if ns.model in ("lstm", "cnn"):
+        return METRICS[ns.model]
+    return (f"env-steps/sec {_ENV_NAMES.get((ns.obs_dim, ns.act_dim), 'custom')} "
+            f"{ns.num_envs} envs/GPU, {'x'.join(map(str, hidden))} MLP, {world}x MI355X")
+
+
+def workload(ns, hidden) -> str:
+    n, t = ns.num_envs, ns.horizon
+    return (f"{_ENV_NAMES.get((ns.obs_dim, ns.act_dim), 'custom')} shapes: {n} envs/GPU x {t} "
+            f"steps, obs {ns.obs_dim}, act {ns.act_dim}, actor+critic "
+            + (f"BiLSTM(latent {ns.latent}, window {ns.window}) + " if ns.model == "lstm" else "")
+            + ("Nature-DQN CNN encoder (84x84x3 u8 frames -> 3136) + " if ns.model == "cnn" else "")
+            + f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {ns.epochs} epochs x "
+            f"{n * t // ns.batch} minibatches of {ns.batch}")
+
+
+parse_defaults = {"num_envs": 4096, "obs_dim": 17, "act_dim": 6, "hidden": "256,256",
+                  "batch": 65536, "window": None, "horizon": 128, "epochs": 10}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("PPO_BENCH_LAUNCH_CHECK") == "1":
+        return launch_check(args, world, rank)
     # rehearsal knobs (not the measured configuration): PPO_BENCH_BACKEND=gloo and
     # PPO_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the data-parallel path
     if os.environ.get("PPO_BENCH_ONE_DEVICE") == "1":
@@ -392,21 +585,12 @@ def main():
     if args.model == "mlp" and (args.obs_dim, args.act_dim, hidden, n) != (17, 6, (256, 256), 4096):
         # a non-headline MLP config (e.g. BASELINE configs[2] Ant, configs[3]'s Humanoid shard):
         # its own metric string, never the HalfCheetah headline's
-        metric = (f"env-steps/sec {_ENV_NAMES.get((args.obs_dim, args.act_dim), 'custom')} "
-                  f"{n} envs/GPU, {'x'.join(map(str, hidden))} MLP, {world}x MI355X")
+        metric = leg_metric(args, hidden, world)
     line = {"metric": metric, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded device streams; action-dependent synthetic dynamics)",
-            "config": {"workload": (f"{_ENV_NAMES.get((args.obs_dim, args.act_dim), 'custom')} "
-                                    f"shapes: {n} envs/GPU x {t} steps, obs "
-                                    f"{args.obs_dim}, act {args.act_dim}, actor+critic "
-                                    + (f"BiLSTM(latent {args.latent}, window {args.window}) + "
-                                       if args.model == "lstm" else "")
-                                    + ("Nature-DQN CNN encoder (84x84x3 u8 frames -> 3136) + "
-                                       if args.model == "cnn" else "")
-                                    + f"{'x'.join(map(str, hidden))} ReLU MLP, PPO {args.epochs} "
-                                    f"epochs x {n * t // args.batch} minibatches of {args.batch}"),
+            "config": {"workload": workload(args, hidden),
                        "num_envs_per_gpu": n, "horizon": t, "minibatch": args.batch,
                        "epochs": args.epochs, "rng": args.rng, "hipgraphs": not args.no_graphs,
                        "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
@@ -423,7 +607,20 @@ def main():
         gae = {k: v for k, v in kernels.items() if v["class"] == "gae"}
         if gae:
             gname, gc = max(gae.items(), key=lambda kv: kv[1]["ms"])
-            line["gae_roofline"] = roofline(gname, gc, traffic, force_hbm=True)
+            gr = roofline(gname, gc, traffic, force_hbm=True)
+            if "records" in gname:
+                # the fused scan + record pass counts every byte it moves, including the padding
+                # of the 128-B row records; the payload-only figure drops that padding
+                rows = n * t
+                payload = 2 * args.window * args.obs_dim + 4 * args.act_dim + 12
+                pb = gr["algorithmic_per_launch"] - (128 - payload) * rows
+                gr["bytes_counted"] = (f"reads: reward f64, V, V', terminated (scan, 25 B) + "
+                                       f"state f32 {4 * args.window * args.obs_dim} B + actions "
+                                       f"{4 * args.act_dim} B + old log-prob 4 B; writes: "
+                                       f"adv / target and the full 128-B record per (env, step)")
+                gr["payload_only"] = {"bytes_per_launch": pb, "record_payload_bytes": payload,
+                                      "frac": pb / (gr["avg_launch_us"] * 1e-6) / 1e9 / PEAK_HBM_GBS}
+            line["gae_roofline"] = gr
         ti = max(args.timing_iters, 1)
         line["kernel_classes_ms_per_step"] = {k: v["ms"] / ti for k, v in classes.items()
                                               if v["launches"]}
@@ -438,6 +635,16 @@ def main():
         if args.env != "host":
             # s8(d)'s t_iter includes the per-step obs H2D and action D2H: the host-pool env
             line["pcie_inclusive_leg"] = leg(args, args.precision, "host", dev)
+        if args.model == "mlp" and (args.obs_dim, args.act_dim, hidden, n) == (17, 6, (256, 256),
+                                                                                4096):
+            for name in [x for x in args.legs.split(",") if x]:
+                line[f"{name}_leg"] = config_leg(args, name, dev)
+                if name == "humanoid":
+                    # the same shard with one rank's B = 65,536 (2 minibatches per epoch): the
+                    # round-3 measurement's setting, fewer and larger optimizer steps
+                    line["humanoid_leg"]["b65536"] = {
+                        k: v for k, v in config_leg(args, name, dev, batch=65536).items()
+                        if k in ("value", "ms_per_step", "minibatches_per_epoch", "roofline")}
     if rank == 0 and world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = (cpu_baseline_cnn(args, hidden) if args.model == "cnn"
                                 else cpu_baseline(args, hidden))

@@ -16,7 +16,14 @@ from torch import nn
 from . import engine as E
 from .features import REFERENCE_CRITIC_HIDDEN, Run
 
-ENGINE_RNG_FILE = "engine_rng.pth"  # the per-rank torch generator of local data parallelism
+ENGINE_RNG_FILE = "engine_rng_rank{rank}.pth"  # the per-rank torch generator of local data parallelism
+
+
+def _dist_rank() -> int:
+    """This process's torch.distributed rank (0 when not initialised)."""
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank()
+    return 0
 from .models import EngineActor, EngineCritic, move_to_flat
 
 _ACT_NAMES = {nn.ReLU: "relu", nn.Tanh: "tanh", nn.ELU: "elu"}
@@ -306,8 +313,8 @@ class PPOEngineAgent:
             torch.save(sd, f"{path}/optimizer_{name}.pth")
         algo = getattr(self, "_algorithm", None)
         state = algo.rng_state() if algo is not None else None
-        if state is not None:  # engine-only file: the reference never reads it
-            torch.save(state, f"{path}/{ENGINE_RNG_FILE}")
+        if state is not None:  # engine-only file (one per rank): the reference never reads it
+            torch.save(state, f"{path}/{ENGINE_RNG_FILE.format(rank=state['rank'])}")
         run.save()
 
     def load(self):
@@ -325,5 +332,12 @@ class PPOEngineAgent:
             opt.load_state_dict(torch.load(f"{path}/optimizer_{name}.pth", map_location="cpu",
                                            weights_only=True))
         algo = getattr(self, "_algorithm", None)
-        if algo is not None and os.path.exists(f"{path}/{ENGINE_RNG_FILE}"):
-            algo.set_rng_state(torch.load(f"{path}/{ENGINE_RNG_FILE}", weights_only=True))
+        rank = algo.dp.rank if algo is not None else _dist_rank()
+        rng_file = f"{path}/{ENGINE_RNG_FILE.format(rank=rank)}"
+        state = torch.load(rng_file, weights_only=True) if os.path.exists(rng_file) else None
+        if algo is not None:
+            algo.set_rng_state(state)
+        else:
+            # the reference's order builds the agent, loads, then builds the trainer: keep the
+            # state for PPOEngine.__init__ to pick up
+            self._loaded_rng_state = state

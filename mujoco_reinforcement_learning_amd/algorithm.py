@@ -43,7 +43,9 @@ class PPOEngine:
                                                            "local"))
         self.world = self.dp.world
         self.dp.broadcast_params(agent.flat_params)  # every replica starts from rank 0's params
-        agent._algorithm = self  # agent.save / load carry the per-rank generator (engine_rng.pth)
+        agent._algorithm = self  # agent.save / load carry the per-rank generator (engine_rng_rank*.pth)
+        self.set_rng_state(getattr(agent, "_loaded_rng_state", None))  # agent.load() before us
+        agent._loaded_rng_state = None
         ec, nc = self.run.environment_config, self.run.network_config
         if hasattr(agent, "make_buffer"):  # agents with their own state storage (u8 frames)
             self.buffer = agent.make_buffer(ec.num_envs, ec.maximum_timesteps)
@@ -73,7 +75,7 @@ class PPOEngine:
         parallel mode every rank draws the GLOBAL (N, A) normals and keeps its shard's rows, so
         the sharded run consumes the reference RNG stream exactly like one process."""
         if self._rng() == "torch":
-            if self.dp.active and self.dp.mode == "exact":
+            if self.dp.world > 1 and self.dp.mode == "exact":
                 lo, hi = self.dp.my_shard(n)
                 eps = torch.randn(self.dp.global_envs(n), a)[lo:hi]
             else:
@@ -90,7 +92,7 @@ class PPOEngine:
         rank; it is a CPU Mersenne-Twister stream, independent of the device Philox key
         (seed * 1_000_003 + 17 + 7919 * rank) that only keys counter-based rollout noise.  Its
         state is checkpointed by agent.save() (engine_rng.pth) and restored by agent.load()."""
-        if not (self.dp.active and self.dp.mode == "local"):
+        if not (self.dp.world > 1 and self.dp.mode == "local"):
             return None
         if getattr(self, "_rank_gen", None) is None:
             key = (torch.initial_seed() * 1_000_003 + self._seed() * 7_919_993
@@ -316,7 +318,7 @@ class PPOEngine:
 
     # ---- ppo.py:93-154 ---------------------------------------------------------------------
     def _scheduled_ok(self) -> bool:
-        return self._rng() == "philox" and (not self.dp.active or self.dp.mode == "local")
+        return self._rng() == "philox" and (self.dp.world == 1 or self.dp.mode == "local")
 
     def _train_scheduled(self, memory: RolloutBuffer, b: int, epochs: int, batches: int, clip_lo,
                          clip_hi, inv_b, inv_ba):
@@ -418,7 +420,7 @@ class PPOEngine:
         n, t_len, a = buf.num_envs, buf.horizon, buf.act_dim
         bs = run.training_config.batch_size
         epochs = int(run.training_config.epochs_per_iteration)
-        exact = self.dp.active and self.dp.mode == "exact"
+        exact = self.dp.world > 1 and self.dp.mode == "exact"
         # exact DP: ppo.py:97-106 over the GLOBAL buffer (single-process N*T and B)
         n_glob = self.dp.global_envs(n) if exact else n
         batches_per_epoch = int(t_len * n_glob / bs)
@@ -495,9 +497,13 @@ class PPOEngine:
         return self._loss_buf
 
     def _finish_logging(self, loss_buf: torch.Tensor) -> None:
-        losses = loss_buf.double().cpu()
         if self.world > 1:
-            pass  # per-rank contributions; the rank-0 line reports its own shard
+            # every rank's loss terms are already divided by the GLOBAL minibatch size
+            # (DataParallel.loss_scale), so the SUM over ranks is the reference's per-minibatch
+            # mean loss (ppo.py:139-153); one all-reduce per iteration, for logging only
+            loss_buf = loss_buf.clone()
+            self.dp.allreduce_grad(loss_buf)
+        losses = loss_buf.double().cpu()
         epoch_means = losses.mean(dim=1)
         actor_loss = float(epoch_means[:, 0].mean())
         critic_loss = float(epoch_means[:, 1].mean())

@@ -277,6 +277,13 @@ class CNNEngineAgent(PPOEngineAgent):
         if act_cls not in _ACT_NAMES:
             raise ValueError(f"activation {act_cls} not supported by the engine (ReLU/Tanh/ELU)")
         hidden = list(nc.linear_hidden_shapes)[:nc.num_linear_layers]
+        # the pixel engine builds both heads with one width list; record it as the critic's so a
+        # saved run (Run.save) describes the networks.pth it sits beside
+        ch = run.engine_config.critic_hidden_shapes
+        if ch is not None and list(ch) != hidden:
+            raise ValueError(f"the CNN engine's critic head uses the actor's widths {hidden}, "
+                             f"not critic_hidden_shapes={list(ch)}")
+        run.engine_config.critic_hidden_shapes = list(hidden)
         self.networks = nn.ModuleDict()
         # PPOAgent.initialize_networks: Actor() then Critic() (RNG order)
         self.networks["actor"] = EngineCNNActor(hidden, nc.output_shape, act_cls, nc.use_bias,

@@ -47,10 +47,17 @@ class DataParallel:
         # gradient folded to HBM, the separate Adam / gather tail) with a no-op exchange -- the
         # DP kernel cost measured without a second process contending for the GPU
         import os
+        # Only the kernel sequence follows it (``active``); the RNG streams and the loss scale
+        # follow ``world`` alone, so the rehearsal computes what the single-rank run computes.
         self.rehearse = self.world == 1 and os.environ.get("PPO_DP_REHEARSE") == "1"
+        if self.rehearse:
+            import warnings
+            warnings.warn("PPO_DP_REHEARSE=1: running the data-parallel kernel sequence (eager, "
+                          "no hipGraphs) with a no-op exchange on one rank", stacklevel=2)
 
     @property
     def active(self) -> bool:
+        """The data-parallel kernel sequence (fold to HBM, exchange, separate Adam tail) runs."""
         return self.world > 1 or self.rehearse
 
     def allreduce_grad(self, flat_grad: torch.Tensor) -> None:

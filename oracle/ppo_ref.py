@@ -504,8 +504,9 @@ def math_log_sqrt_2pi() -> float:
 # operands with f32 accumulation; biases, activations, the distribution / loss math, GAE and Adam
 # stay f32.
 def _bf(x: torch.Tensor) -> torch.Tensor:
-    """Round to bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32) and back to f32."""
-    return x.to(torch.bfloat16).to(torch.float32)
+    """Round to bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32) and back to x's dtype (f32;
+    f64 for the f64-accumulated emulation the bf16 gradient tests compare against)."""
+    return x.to(torch.bfloat16).to(x.dtype)
 
 
 class _BF16Linear(torch.autograd.Function):

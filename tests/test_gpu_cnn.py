@@ -150,13 +150,18 @@ def _oracle_minibatch(cfg, seed, bf16, dtype, frames, actions, old_logp, adv, vt
     return grads, float(la), float(lc)
 
 
+# bf16 gradients against the f64-accumulated bf16 emulation: max error per tensor / its max,
+# relative L2 per tensor
+CNN_BF16_GRAD_BAR = (2e-2, 1e-2)
+
+
 @pytest.mark.parametrize("precision", ["f32", "bf16"])
 def test_minibatch_grad_matches_oracle(gpu, precision):
     """f32: every gradient within 2e-5 of its tensor's max.  bf16: the engine against the bf16
-    emulation, held to the emulation's own noise floor -- the same bf16-rounded minibatch
-    evaluated with f32 and with f64 accumulation already differs by 1-20 % of a tensor's max
-    here (bf16 rounding flips of intermediates, amplified through 6 layers and the ReLU kinks,
-    measured in the test): the engine must stay within 3x that spread (and 2e-3 absolute)."""
+    emulation evaluated with f64 accumulation, at a fixed bar (CNN_BF16_GRAD_BAR).  The f32-
+    accumulated emulation is not the reference for the bar: it differs from the f64 one by up
+    to ~20 % of a tensor's max here (bf16 rounding flips of intermediates, amplified through 6
+    layers and the ReLU kinks), so it is printed beside the engine's error, not used."""
     rows_total, b = 160, 96
     run, agent, ref, cfg = _pair(gpu, rows_total, b, hidden=(256, 256), precision=precision, seed=4)
     g = torch.Generator().manual_seed(10)
@@ -176,9 +181,10 @@ def test_minibatch_grad_matches_oracle(gpu, precision):
                                 loss, 0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
     bf16 = precision == "bf16"
     args = (frames, actions, old_logp, adv, vt, rows)
-    ref_g, la, lc = _oracle_minibatch(cfg, 4, bf16, torch.float32, *args)
-    floor_g = _oracle_minibatch(cfg, 4, bf16, torch.float64, *args)[0] if bf16 else None
+    f32_g, la, lc = _oracle_minibatch(cfg, 4, bf16, torch.float32, *args)
+    ref_g = _oracle_minibatch(cfg, 4, bf16, torch.float64, *args)[0] if bf16 else f32_g
     gd = agent.packed(grad).cpu().double()
+    bar, bar_l2 = CNN_BF16_GRAD_BAR if bf16 else (2e-5, 2e-5)
     worst, worst_l2, off = 0.0, 0.0, 0
     for i, (name, r_) in enumerate(ref_g):
         k = r_.numel()
@@ -187,19 +193,17 @@ def test_minibatch_grad_matches_oracle(gpu, precision):
         err = float((a - r_).abs().max()) / scale
         l2 = float((a - r_).norm() / (r_.norm() + 1e-20))
         if bf16:
-            f = floor_g[i][1]
-            f_err = float((r_ - f).abs().max()) / scale
-            f_l2 = float((r_ - f).norm() / (f.norm() + 1e-20))
-            bar, bar_l2 = max(3 * f_err, 2e-3), max(3 * f_l2, 2e-3)
-            print(f"bf16 {name}: err {err:.3e} of max, rel L2 {l2:.3e} (emulation f32 vs f64: "
-                  f"{f_err:.3e}, {f_l2:.3e})")
+            f = f32_g[i][1]
+            f_err = float((f - r_).abs().max()) / scale
+            print(f"bf16 {name}: err {err:.3e} of max, rel L2 {l2:.3e} vs the f64 emulation "
+                  f"(f32 emulation vs f64: {f_err:.3e})")
         else:
-            bar, bar_l2 = 2e-5, 2e-5
             print(f"f32 {name}: err {err:.3e} of max, rel L2 {l2:.3e}")
         worst, worst_l2 = max(worst, err), max(worst_l2, l2)
         assert err <= bar and l2 <= bar_l2, (name, err, l2, bar, bar_l2)
         off += k
-    print(f"cnn minibatch grad {precision}: worst {worst:.3e} of max, rel L2 {worst_l2:.3e}")
+    print(f"cnn minibatch grad {precision}: worst {worst:.3e} of max, rel L2 {worst_l2:.3e} "
+          f"(bar {bar}, {bar_l2})")
     lt = 1e-5 if precision == "f32" else 1e-3
     assert abs(float(loss[1]) - lc) <= lt * (abs(lc) + 1e-2)
     assert abs(float(loss[0]) - la) <= max(lt, 1e-4) * (abs(la) + 1e-2)

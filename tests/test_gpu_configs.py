@@ -97,26 +97,24 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
                               1.0 / (b * act))
     if precision == "bf16":
         R.use_bf16_gemms(ref)
-    idx = rows.long()
-    x = states[idx].reshape(b, w, obs)
-    _, dist = ref.act(x, return_dist=True)
-    new_lp = dist.log_prob(actions[idx]).sum(dim=1)
-    v = ref.get_state_value(x)
-    lc = torch.nn.functional.huber_loss(v, vt[idx][:, None], reduction="mean")
-    ratio = (new_lp - old_logp[idx]).exp()[:, None]
-    a_ = adv[idx][:, None]
-    la = -torch.min(ratio * a_, torch.clamp(ratio, 0.9, 1.1) * a_).mean() \
-        - dist.entropy().mean() * 1e-4
-    ref.networks.zero_grad()
-    (la + lc).backward()
-    gd = eng.packed(grad).cpu()
+    lc, la, ref_g = _oracle_loss_grads(ref, states, actions, old_logp, adv, vt, rows, b, w, obs,
+                                       torch.float32)
+    if precision == "bf16":
+        # the bar's reference: the same bf16-rounded operands accumulated in f64.  The f32-
+        # accumulated emulation differs from it by bf16 rounding flips of intermediates (the
+        # engine's MFMA order flips different ones), so the engine is held to the f64 value with
+        # a fixed bar, not to the f32 emulation's own spread
+        ref.networks.to(torch.float64)
+        ref_g = _oracle_loss_grads(ref, states, actions, old_logp, adv, vt, rows, b, w, obs,
+                                   torch.float64)[2]
+    gd = eng.packed(grad).cpu().double()
     worst, worst_l2, off = 0.0, 0.0, 0
-    # f32: summation order only.  bf16: the same plus occasional flips of an intermediate's bf16
-    # rounding (1 bf16 ulp = 2^-8 relative) that compound over 3 hidden layers of 512
-    bar, bar_l2 = (2e-5, 2e-5) if precision == "f32" else (1e-2, 5e-3)
-    for name, p in ref.networks.named_parameters():
-        k = p.numel()
-        a, r_ = gd[off:off + k], p.grad.flatten()
+    # f32: summation order only.  bf16 vs the f64-accumulated emulation: bf16 rounding flips of
+    # intermediates (1 bf16 ulp = 2^-8 relative) through 3 hidden layers of 512
+    bar, bar_l2 = (2e-5, 2e-5) if precision == "f32" else BF16_GRAD_BAR
+    for name, r_ in ref_g:
+        k = r_.numel()
+        a = gd[off:off + k]
         scale = float(r_.abs().max()) + 1e-12
         err = float((a - r_).abs().max()) / scale
         l2 = float((a - r_).norm() / (r_.norm() + 1e-20))
@@ -126,9 +124,32 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
     print(f"minibatch grad {precision}: worst per-tensor error {worst:.3e} of max (bar {bar}), "
           f"rel L2 {worst_l2:.3e} (bar {bar_l2})")
     lt = 1e-5 if precision == "f32" else 1e-3
-    lc, la = float(lc.detach()), float(la.detach())
     assert abs(float(loss[1]) - lc) <= lt * (abs(lc) + 1e-2)
     assert abs(float(loss[0]) - la) <= max(lt, 1e-4) * (abs(la) + 1e-2)
+
+
+# bf16 gradients against the f64-accumulated bf16 emulation: max error per tensor / its max,
+# relative L2 per tensor
+BF16_GRAD_BAR = (1e-2, 5e-3)
+
+
+def _oracle_loss_grads(ref, states, actions, old_logp, adv, vt, rows, b, w, obs, dtype):
+    """ppo.py:109-135's minibatch loss on the oracle nets in ``dtype`` and its gradient in
+    parameters() order: (critic loss, actor loss, [(name, f64 grad)])."""
+    idx = rows.long()
+    x = states[idx].reshape(b, w, obs).to(dtype)
+    _, dist = ref.act(x, return_dist=True)
+    new_lp = dist.log_prob(actions[idx].to(dtype)).sum(dim=1)
+    v = ref.get_state_value(x)
+    lc = torch.nn.functional.huber_loss(v, vt[idx][:, None].to(dtype), reduction="mean")
+    ratio = (new_lp - old_logp[idx].to(dtype)).exp()[:, None]
+    a_ = adv[idx][:, None].to(dtype)
+    la = -torch.min(ratio * a_, torch.clamp(ratio, 0.9, 1.1) * a_).mean() \
+        - dist.entropy().mean() * 1e-4
+    ref.networks.zero_grad()
+    (la + lc).backward()
+    grads = [(n, p.grad.double().flatten()) for n, p in ref.networks.named_parameters()]
+    return float(lc.detach()), float(la.detach()), grads
 
 
 @pytest.mark.parametrize("precision", ["f32", "bf16"])

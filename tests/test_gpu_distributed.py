@@ -158,3 +158,128 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu, shape):
     assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
     assert "step_tail_kernel" in kernels, kernels
     assert ("reduce_slabs_kernel" in kernels) == (not fold), (fold, kernels)
+
+
+def _ckpt_worker(rank, world, port, q, exp):
+    """Local data parallel with the torch RNG (each rank its own forked generator): one
+    iteration, agent.save(); then a fresh agent that load()s BEFORE its PPOEngine exists (the
+    reference's order, main.py:117-124) must continue with the same per-rank generator."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    dev = torch.device("cuda", 0)
+    n, t, b = 16, 16, 64
+
+    def build():
+        s = make_synthetic_streams(n, t, 17, seed=41 + rank, p_terminate=0.05, device=dev)
+        run = make_run(num_envs=n, horizon=t, hidden=(64, 64), batch_size=b, epochs=1, rng="torch",
+                       seed=rank, dp_mode="local", experiment_path=exp)
+        torch.manual_seed(0)
+        agent = PPOEngineAgent(run, device=dev)
+        return run, agent, s
+
+    run, agent, s = build()
+    algo = PPOEngine(SyntheticVecEnvHelper(s, run, device=dev), agent, log=lambda m: None)
+    algo.iterate(verbose=False)
+    ep = run.dynamic_config.current_episode
+    run.dynamic_config.current_episode = ep - 1
+    agent.save()
+    torch.distributed.barrier()  # every rank's files written before anyone loads
+    ahead = torch.randn(4, generator=algo._local_gen())  # the saved generator's next draws
+    run2, agent2, s2 = build()
+    run2.dynamic_config.current_episode = ep - 1
+    agent2.load()  # no PPOEngine yet
+    algo2 = PPOEngine(SyntheticVecEnvHelper(s2, run2, device=dev), agent2, log=lambda m: None)
+    got = torch.randn(4, generator=algo2._local_gen())
+    files = sorted(f for f in os.listdir(f"{exp}/networks/{ep - 1}") if f.startswith("engine_rng"))
+    q.put((rank, torch.equal(ahead, got), files))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_local_dp_checkpoint_round_trip_per_rank_generators(gpu, tmp_path):
+    """each rank's generator goes to its own file (engine_rng_rank{r}.pth) and a
+    resumed rank continues its own stream, also when load() runs before PPOEngine exists."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    exp = str(tmp_path / "exp")
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, 2, port, q, exp)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r, same, files = q.get(timeout=300)
+        got[r] = (same, files)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert got[r][0], f"rank {r} did not resume its own generator"
+        assert got[r][1] == ["engine_rng_rank0.pth", "engine_rng_rank1.pth"], got[r][1]
+
+
+def _rccl_worker(q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                      WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.distributed.init_process_group("nccl", device_id=dev)
+    from mujoco_reinforcement_learning_amd.distributed import DataParallel
+    x = torch.arange(142605, dtype=torch.float32, device=dev) * 0.5  # the 2x256 flat gradient size
+    want = x.clone()
+    torch.distributed.all_reduce(x, op=torch.distributed.ReduceOp.SUM)
+    work = DataParallel().allreduce_grad_async(x)  # world 1: no collective, no handle
+    torch.cuda.synchronize()
+    q.put((torch.equal(x.cpu(), want.cpu()), work is None, torch.distributed.get_backend()))
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_rccl_allreduce_known_answer(gpu):
+    """RCCL ("nccl" backend on ROCm) initialises on the device and an all-reduce of a
+    flat-gradient-sized buffer returns the known sum (one GPU on this box: world 1)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(q,))
+    p.start()
+    ok, no_handle, backend = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok and no_handle and backend == "nccl"
+
+
+def test_bench_self_launches_two_ranks_on_one_gpu(gpu):
+    """``python bench.py --gpus 2`` as a plain invocation (the driver's scaling run)
+    starts its own two ranks; here both share cuda:0 over gloo (PPO_BENCH_ONE_DEVICE=1) on a tiny
+    workload, and rank 0 prints one JSON line with n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PPO_BENCH_BACKEND="gloo", PPO_BENCH_ONE_DEVICE="1")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
+                        "2", "--warmup", "1", "--num-envs", "64", "--horizon", "16", "--batch",
+                        "256", "--epochs", "1", "--no-cpu-baseline", "--no-legs"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    print(f"bench --gpus 2 (one GPU, gloo): {rec['value']:.4g} env-steps/s, "
+          f"{rec['ms_per_step']:.2f} ms/step")
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["steps"] == 2

@@ -11,7 +11,7 @@ import torch
 
 from oracle import ppo_ref as R
 from parity_util import (assert_params_match, compare_step_grads, make_pair, own_gae,
-                         run_iteration_pair)
+                         replay_rows, run_iteration_pair, tensor_slices)
 
 pytestmark = pytest.mark.gpu
 
@@ -93,6 +93,94 @@ def test_bf16_iteration_matches_bf16_emulation(gpu):
         print(f"bf16 update {name}: rel L2 {rel:.3e}")
         assert rel <= 5e-3, (name, rel)
         off += k
+
+
+def _first_step_grad_f64(ref0, mem, rows, n, t, cfg):
+    """The first optimizer step's gradient (ppo.py:109-135) of the bf16 emulation accumulated in
+    f64, on the ENGINE's rollout buffer and the initial parameters (``ref0``, a copy of the
+    oracle agent taken before training): isolates the kernels from the rollout's own drift."""
+    import copy
+    ref = copy.deepcopy(ref0)
+    R.use_bf16_gemms(ref)
+    ref.networks.to(torch.float64)
+    r = rows.long()
+    em = (r % n) * t + r // n  # storage row t*N + n -> the reference's env-major n*T + t
+    flat = {k: mem[k].cpu().reshape(n * t, *mem[k].shape[2:]) for k in
+            ("current_state", "action", "action_log_prob", "advantage",
+             "current_state_value_target")}
+    x = flat["current_state"][em].double()
+    _, dist = ref.act(x, return_dist=True)
+    new_lp = dist.log_prob(flat["action"][em].double()).sum(dim=1)
+    v = ref.get_state_value(x)
+    lc = torch.nn.functional.huber_loss(v, flat["current_state_value_target"][em].double(),
+                                        reduction="mean")
+    ratio = (new_lp - flat["action_log_prob"][em].double()).exp()[:, None]
+    a_ = flat["advantage"][em].double()
+    la = -torch.min(ratio * a_, torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon)
+                    * a_).mean() - dist.entropy().mean() * cfg.entropy_eps
+    ref.networks.zero_grad()
+    (la + lc).backward()
+    return torch.cat([p.grad.flatten() for p in ref.networks.parameters()])
+
+
+def test_bf16_wide_iteration_matches_bf16_emulation(gpu):
+    """The wide bf16-resident path (BASELINE configs[3] shapes: Humanoid 3x512, O=376, A=17; the
+    bench's Humanoid route) through one full iteration -- rollout -> GAE -> 2 epochs x 4
+    minibatches -> Adam -- against the bf16 emulation oracle on the same torch RNG streams:
+      * the wide kernels ran (wide_* kernel names in the engine's launch records);
+      * GAE of the engine's own rollout bit-exact;
+      * rollout values / actions / log-probs within 2e-3 of their scale;
+      * the first step's gradient against the f64-accumulated emulation on the engine's own
+        buffer within the fixed bf16 gradient bar (1e-2 of each tensor's max, 5e-3 relative L2);
+      * the parameter update (post - init) within 0.5 % relative L2 of the oracle's per tensor;
+      * every element within 2*lr*steps."""
+    n, t, b = 256, 32, 2048
+    algo, agent, ref, env, cfg = _setup(gpu, n=n, t=t, b=b, epochs=2, hidden=(512, 512, 512),
+                                        obs=376, act=17, precision="bf16", p_term=0.02)
+    import copy
+    ref0 = copy.deepcopy(ref)
+    R.use_bf16_gemms(ref)
+    p0 = R.flat_params(ref).clone()
+    agent.engine.timing(True, capacity=100000)
+    mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg, seed_train=99)
+    kernels = agent.engine.timing_kernels()
+    agent.engine.timing(False)
+    wide = sorted(k for k in kernels if k.startswith("wide_"))
+    print(f"wide kernels: {wide}")
+    assert any("wide_gemm" in k for k in wide) and any("wide_loss" in k for k in wide), kernels
+    adv_own, vt_own = own_gae(mem, cfg)
+    assert torch.equal(mem["advantage"].cpu(), adv_own)
+    assert torch.equal(mem["current_state_value_target"].cpu(), vt_own)
+    for key in ("current_state_value", "action", "action_log_prob"):
+        a, r = mem[key].cpu(), ref_mem[key]
+        err = float((a - r).abs().max()) / (float(r.abs().max()) + 1e-6)
+        print(f"wide bf16 rollout {key}: max err {err:.3e} of scale")
+        assert err <= 2e-3, (key, err)
+    rows0 = replay_rows(99, n, t, b, 2, 17)[0]
+    g64 = _first_step_grad_f64(ref0, mem, rows0, n, t, cfg)
+    worst, worst_l2 = 0.0, 0.0
+    for name, lo, hi in tensor_slices(ref):
+        ge, gr = g_eng[0][lo:hi].double(), g64[lo:hi]
+        err = float((ge - gr).abs().max()) / (float(gr.abs().max()) + 1e-30)
+        l2 = float((ge - gr).norm() / (gr.norm() + 1e-30))
+        worst, worst_l2 = max(worst, err), max(worst_l2, l2)
+        assert err <= 1e-2 and l2 <= 5e-3, (name, err, l2)
+    print(f"wide bf16 first-step grad vs f64 emulation: worst {worst:.3e} of max, rel L2 "
+          f"{worst_l2:.3e}")
+    p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
+    steps = len(g_ref)
+    assert steps == 8
+    dmax = float((p_eng - p_ref).abs().max())
+    print(f"wide bf16 params: max |diff| {dmax:.3e} (bound {2 * cfg.learning_rate * steps:.1e})")
+    assert dmax <= 2 * cfg.learning_rate * steps
+    worst_u = 0.0
+    for name, lo, hi in tensor_slices(ref):
+        du_e, du_r = p_eng[lo:hi] - p0[lo:hi], p_ref[lo:hi] - p0[lo:hi]
+        rel = float((du_e - du_r).norm() / (du_r.norm() + 1e-20))
+        worst_u = max(worst_u, rel)
+        print(f"wide bf16 update {name}: rel L2 {rel:.3e}")
+        assert rel <= 5e-3, (name, rel)
+    print(f"wide bf16 update: worst rel L2 {worst_u:.3e}")
 
 
 def test_philox_mode_runs_and_is_reproducible(gpu):
