@@ -135,6 +135,11 @@ int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
  * of the separate launches (same reduction order).  Off by default because it measured slower:
  * the fold adds 29 us to the fused launch against an 18 us standalone tail. */
 int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable);
+/* Which fused bf16 update kernel the ctx launches for ReLU 2x256 nets (A11-A13, ppo.py:109-135):
+ * 8 = fused_update_kernel (8 waves, 64-row chunks; also tanh / ELU), 4 = fused_update4_kernel
+ * (one wave per SIMD, 128-row chunks).  Default PPO_FUSED4 (1 -> 4, else 8);
+ * variant < 0 queries.  The two agree to f32 rounding; each is bitwise deterministic. */
+int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant);
 /* Host check (synchronises): PPO_EHIP if a fold's grid barrier timed out since the last check
  * (its step's gradients are wrong), with the message in ppo_last_error(). */
 int ppo_ctx_check_device_errors(ppo_ctx *ctx);

@@ -62,6 +62,7 @@ struct ppo_ctx {
   int *ffold_err;               // set by a fold whose grid barrier timed out
   int fold_on;                  // ppo_ctx_fused_fold (default: PPO_FUSED_FOLD, 0)
   int fold_g;                   // G the residency check last passed for (0: none)
+  int fused4;                   // ppo_ctx_fused_variant: 1 -> fused_update4_kernel (ReLU)
   ppo::WideWork *wide;          // wide bf16-resident layered path (wide_path.h), or null
   ppo::Timing tim;
 };

@@ -1,0 +1,639 @@
+// The fused minibatch update (ppo.py:109-135) re-decomposed for ReLU
+// nets: ONE wave per SIMD (4 waves, up to 512 registers each) and 128-row chunks, so every weight
+// fragment streamed from L2 and every activation fragment read from LDS feeds twice the MFMAs of
+// the 8-wave / 64-row kernel in fused_update.hip.
+//
+// Per 64 rows the 8-wave kernel's L1 and dgrad passes sat at ~3.2 k cycles against a 2,048-cycle
+// MFMA floor, co-limited by the W1 stream (128 KB per pass per CU at ~64 B/clk) and the LDS
+// B-operand reads (8 waves x 64 rows x 512 B at 128 B/clk).  Here a wave owns 64 output features
+// (two 32-feature MFMA tiles) for 128 rows (four row tiles): per 128 rows the W1 stream is 128 KB
+// (2,048 cycles) and the B reads 4 x 128 x 512 B (2,048 cycles) against 4,096 MFMA cycles.
+//
+// Registers (per lane): dW1 16 tiles (256) + dW0 2 tiles (32) + head dW 4 16x16 tiles (16),
+// persistent; the pass accumulators 8 tiles (128), the W1 fragment ring and the B operands.
+//
+// LDS (158.5 KB): the A1 / D1 image (D1 written in place over A1 once dW1 has read A1), the A2 /
+// D2 image (D2 in place over A2), the head image, biases and head constants, one 8 KB region that
+// holds the chunk's row scalars during the forward / loss phases and its X image for dW0, and the
+// dz images, whose 8.4 KB also park the NEXT chunk's X image between its prefetch and its L0 pass.
+//
+// Numerics are those of fused_update_kernel (oracle.use_bf16_gemms): bf16 operands of every fc
+// product with f32 accumulation; biases, ReLU', the loss heads and every bias gradient in f32.
+// Summation orders differ from fused_update_kernel (the head z is one K=256 chain here), so the
+// two kernels agree to f32 rounding, not bitwise; each is bitwise deterministic run to run.
+#include "fused_common.h"
+
+namespace ppo {
+
+using namespace fu;
+
+namespace f4 {
+
+constexpr int H = 256;
+constexpr int RR = 128;            // rows per chunk
+constexpr int NW4 = 4;             // waves per workgroup: one per SIMD
+constexpr int NT4 = 64 * NW4;
+constexpr int PITCH = 2 * H;       // A1 / A2 image row pitch (bytes)
+constexpr int DZTP = 2 * (RR + 8); // head-major dz image pitch (bytes)
+constexpr int KS = H / 16;         // k-steps of a 32x32x16 pass over H
+constexpr int PD4 = 3;             // weight-ring prefetch distance (k-steps)
+constexpr int P4 = PD4 + 1;        // ring period (divides KS)
+static_assert(KS % P4 == 0, "ring period must divide the k-steps");
+
+struct Lds4 {
+  static constexpr int WHB = 0;                              // bf16 head image [16][H + 8]
+  static constexpr int BIAS = WHB + HeadImg<H>::BYTES;       // f32 b0[H], b1[H]
+  static constexpr int HS = BIAS + 2 * H * 4;                // f32 head bias, logstd, log std, 1/var, 1/(2 var)
+  static constexpr int S = HS + 80 * 4;                      // SROW [128][16] f32 (phases 2-4) / X image (5-7)
+  static constexpr int IMG1 = S + RR * 64;                   // A1, then D1 in place
+  static constexpr int IMG2 = IMG1 + RR * PITCH;             // A2, then D2 in place
+  static constexpr int DZ = IMG2 + RR * PITCH;               // dz [128][16] bf16 (phases 4-5)
+  static constexpr int DZT = DZ + RR * kDzRowBytes;          // dz^T [16][128 + 8] bf16
+  static constexpr int XN = DZ;                              // the next chunk's X image (phases 6a-1)
+  static constexpr int TOTAL = DZT + 16 * DZTP;
+  static constexpr int RED = IMG1;                           // epilogue: f32 [4 waves][16][4]
+  static_assert(TOTAL <= 163840, "LDS budget");
+  static_assert(TOTAL - XN >= RR * 64, "the X image fits the dz region");
+  static_assert(S % 16 == 0 && IMG1 % 16 == 0 && IMG2 % 16 == 0 && DZ % 16 == 0 && DZT % 16 == 0,
+                "16-B aligned regions");
+};
+
+__device__ __forceinline__ uint16_t bf16_bits4(float x) { return static_cast<uint16_t>(pack2(x, 0.f) & 0xffffu); }
+
+// dW1 accumulation pinned to AGPRs: the 16 dW1 tiles (256 registers) fill the AGPR half of the
+// unified file, everything else lives in VGPRs.  Through inline asm the compiler cannot move these
+// accumulators (its allocator otherwise splits the MFMA accumulators of both kinds across the two
+// halves and spills).  The leading s_nop 1 covers a VALU write of an operand right before the MFMA
+// (the hazard recognizer does not see into the asm); srcC = dst chains need no wait states.
+__device__ __forceinline__ void mfma_agpr(f32x16 &acc, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// every other accumulator (pass tiles, dW0, head dW, head z) pinned to VGPRs the same way
+__device__ __forceinline__ f32x16 mfma_v(const bf16x8 &a, const bf16x8 &b, f32x16 acc) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+__device__ __forceinline__ f32x4 mfma16_v(const bf16x8 &a, const bf16x8 &b, f32x4 acc) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+  return z;
+}
+
+// 18 wait states before VALU reads of the last 32x32x16 results (fused_common.h mfma_drain), as a
+// scheduling fence: no register operands, so the accumulators may stay in AGPRs
+__device__ __forceinline__ void drain_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int NACC>
+__device__ __forceinline__ void drain8(f32x16 (&)[2][NACC]) { drain_fence(); }
+
+// acc[f][rt] += W[64w + 32(ft0 + f) + r][:] . img[32rt + r][:] over k = 0..H-1 for f < NF: A
+// operands from the fragment-major bf16 weight image (wf = the first tile's base for this lane),
+// B operands 16-B row reads of the LDS image (row tile t's next k-step read issued as soon as its
+// MFMAs have issued); weights PD4 k-steps ahead through the ring.
+template <int NF>
+__device__ __forceinline__ void pass4(const __bf16 *wf, const char *img, int r, int h,
+                                      bf16x8 (&ring)[P4][NF], f32x16 (&acc)[NF][4]) {
+  const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
+  const char *rowp = img + r * PITCH;
+  constexpr int64_t STEP = 16 * H;  // elements per k-step of the fragment-major image
+  constexpr int64_t TILE = 64 * 8;  // elements per 32-feature tile of one k-step
+  bf16x8 bc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * (h ^ swz));
+#pragma unroll 1
+  for (int s0 = 0; s0 < KS - P4; s0 += P4) {
+#pragma unroll
+    for (int u = 0; u < P4; ++u) {
+      const int s = s0 + u;
+      bf16x8 a[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        a[f] = ring[u][f];
+        ring[(u + PD4) % P4][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + PD4) + TILE * f);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bc[t], acc[f][t]);
+        bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * s + 2 + h) ^ swz));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // last period peeled: no weight prefetch past the end, no B read past the last k-step
+#pragma unroll
+  for (int u = 0; u < P4; ++u) {
+    const int s = KS - P4 + u;
+    bf16x8 a[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      a[f] = ring[u][f];
+      if (s + PD4 < KS)
+        ring[(u + PD4) % P4][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + PD4) + TILE * f);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bc[t], acc[f][t]);
+      if (s + 1 < KS) bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * s + 2 + h) ^ swz));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  drain_fence();
+}
+
+template <int NF>
+__device__ __forceinline__ void ring_prime4(const __bf16 *wf, bf16x8 (&ring)[P4][NF]) {
+#pragma unroll
+  for (int s = 0; s < PD4; ++s)
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      ring[s][f] = *reinterpret_cast<const bf16x8 *>(wf + static_cast<int64_t>(16 * H) * s + 64 * 8 * f);
+}
+
+// bias + ReLU of the accumulators of feature tiles ft0..ft0+NF-1 -> bf16 image columns
+template <int NF>
+__device__ __forceinline__ void store_act(char *img, const float *bias, f32x16 (&acc)[NF][4],
+                                          int w, int ft0, int r, int h) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ft = ft0 + f;
+      const float4 bv = *reinterpret_cast<const float4 *>(bias + 64 * w + 32 * ft + 8 * g + 4 * h);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float y0 = act_forward(acc[f][t][4 * g] + bv.x, PPO_ACT_RELU);
+        const float y1 = act_forward(acc[f][t][4 * g + 1] + bv.y, PPO_ACT_RELU);
+        const float y2 = act_forward(acc[f][t][4 * g + 2] + bv.z, PPO_ACT_RELU);
+        const float y3 = act_forward(acc[f][t][4 * g + 3] + bv.w, PPO_ACT_RELU);
+        *reinterpret_cast<uint2 *>(img + img_off(32 * t + r, 8 * w + 4 * ft + g, PITCH) + 8 * h) =
+            make_uint2(pack2(y0, y1), pack2(y2, y3));
+      }
+    }
+}
+
+// d = acc * ReLU'(y) with y the image's activation, written over it in place; the bias gradient
+// (sum over the chunk's rows) accumulated per feature in gb[ft] (rs16 layout)
+template <int NF>
+__device__ __forceinline__ void backward_in_place(char *img, f32x16 (&acc)[NF][4], float (&gb)[2],
+                                                  int w, int ft0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int ft = ft0 + f;
+    float bsum[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        char *p = img + img_off(32 * t + r, 8 * w + 4 * ft + g, PITCH) + 8 * h;
+        const uint2 yv = *reinterpret_cast<const uint2 *>(p);
+        const float d0 = act_backward(acc[f][t][4 * g], bf_lo(yv.x), PPO_ACT_RELU);
+        const float d1 = act_backward(acc[f][t][4 * g + 1], bf_hi(yv.x), PPO_ACT_RELU);
+        const float d2 = act_backward(acc[f][t][4 * g + 2], bf_lo(yv.y), PPO_ACT_RELU);
+        const float d3 = act_backward(acc[f][t][4 * g + 3], bf_hi(yv.y), PPO_ACT_RELU);
+        bsum[4 * g] += d0;
+        bsum[4 * g + 1] += d1;
+        bsum[4 * g + 2] += d2;
+        bsum[4 * g + 3] += d3;
+        *reinterpret_cast<uint2 *>(p) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+      }
+    gb[ft] += rs16(bsum, lane);
+  }
+}
+
+// One net's workgroup.  NH: head width (actor A padded, or 1), ACTOR selects the loss head.
+template <int NH, bool ACTOR, int NF>
+__device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, char *lds) {
+  using L = Lds4;
+  constexpr int z = ACTOR ? 0 : 1;
+  char *const whb = lds + L::WHB;
+  const float *const b0s = reinterpret_cast<const float *>(lds + L::BIAS);
+  const float *const b1s = b0s + H;
+  const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
+  char *const simg = lds + L::S;
+  char *const img1 = lds + L::IMG1;
+  char *const img2 = lds + L::IMG2;
+  char *const dzimg = lds + L::DZ;
+  char *const dztimg = lds + L::DZT;
+  char *const xnimg = lds + L::XN;
+
+  const int tid0 = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  int tid = tid0, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  // Lane-derived LDS addresses are loop-invariant across chunks; re-deriving them from an opaque
+  // copy of the thread id in every phase keeps the compiler from hoisting (and spilling) dozens of
+  // them out of the chunk loop (as fused_update.hip does).
+#define OPAQUE_LANE()           \
+  tid = tid0;                   \
+  asm volatile("" : "+v"(tid)); \
+  lane = tid & 63;              \
+  r = lane & 31;                \
+  h = lane >> 5
+  const int A = q.act_dim;
+  const int G = q.G;
+  const int nchunks = (q.b + RR - 1) / RR;
+  const int count = q.rows_n ? *q.rows_n : q.b;
+
+  stage_head_image<H>(whb, N.wh, ACTOR ? A : 1, tid, NT4);
+  for (int i = tid; i < 2 * H; i += NT4) {
+    const float *b = i < H ? N.b0 : N.b1;
+    (reinterpret_cast<float *>(lds + L::BIAS))[i] = b ? b[i % H] : 0.f;
+  }
+  if (tid < 32) {
+    const int a = tid & 15;
+    const bool ok = a < (ACTOR ? A : 1);
+    (reinterpret_cast<float *>(lds + L::HS))[tid] =
+        tid < 16 ? ((ok && N.bh) ? N.bh[a] : 0.f) : ((ACTOR && ok) ? q.logstd[a] : 0.f);
+  }
+  if (tid < 16) {  // per-head Normal constants: log(std), 1/var, 1/(2 var); std = exp(logstd)
+    const bool ok = ACTOR && tid < A;
+    const float sd = ok ? expf(q.logstd[tid]) : 1.f;
+    const float var = sd * sd;
+    (reinterpret_cast<float *>(lds + L::HS))[32 + tid] = ok ? logf(sd) : 0.f;
+    (reinterpret_cast<float *>(lds + L::HS))[48 + tid] = 1.f / var;
+    (reinterpret_cast<float *>(lds + L::HS))[64 + tid] = 1.f / (2.f * var);
+  }
+
+  // 32 B of a chunk's staged states (bf16 [row][32]) / row scalars (f32 [row][16]) per thread:
+  // row tid >> 1, half tid & 1; rows past the minibatch read row 0 and are zeroed
+  auto load_x = [&](int c, uint4 (&v)[2]) {
+    const int xrow = tid >> 1, xhalf = tid & 1;
+    const int j = c * RR + xrow;
+    const bool ok = c < nchunks && j < q.b;
+    const uint4 *src = reinterpret_cast<const uint4 *>(q.xb + static_cast<int64_t>(ok ? j : 0) * kFusedKX) + 2 * xhalf;
+    v[0] = src[0];
+    v[1] = src[1];
+    if (!ok) v[0] = v[1] = make_uint4(0u, 0u, 0u, 0u);
+  };
+  auto store_x = [&](char *img, const uint4 (&v)[2]) {
+    const int xrow = tid >> 1, xhalf = tid & 1;
+    *reinterpret_cast<uint4 *>(img + x_off(xrow, 2 * xhalf)) = v[0];
+    *reinterpret_cast<uint4 *>(img + x_off(xrow, 2 * xhalf + 1)) = v[1];
+  };
+  auto load_srow = [&](int c, uint4 (&v)[2]) {
+    const int xrow = tid >> 1, xhalf = tid & 1;
+    const int j = c * RR + xrow;
+    const bool ok = j < q.b;
+    const uint4 *src = reinterpret_cast<const uint4 *>(q.srow + static_cast<int64_t>(ok ? j : 0) * kFusedSP) + 2 * xhalf;
+    v[0] = src[0];
+    v[1] = src[1];
+    if (!ok) v[0] = v[1] = make_uint4(0u, 0u, 0u, 0u);
+  };
+
+  // ---- persistent accumulators ----
+  f32x16 gw1[2][8];  // dW1 tiles: o-tiles 2w + a (the wave's features), i-tiles b = 0..7
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) gw1[a][b] = zero16();
+  f32x16 gw0[2];     // dW0 tiles: features 64w + 32ft.., input columns 0..31
+  gw0[0] = zero16();
+  gw0[1] = zero16();
+  f32x4 ghw[4];      // head dW: heads 4 (lane >> 4) + i, features 64w + 16j + (lane & 15)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ghw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gb1[2] = {0.f, 0.f}, gb0[2] = {0.f, 0.f};   // rs16-scattered bias grads per feature tile
+  float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;       // head (lane & 15) partials
+
+
+  int chunk = blockIdx.x;
+  {
+    uint4 xv[2];
+    load_x(chunk, xv);
+    store_x(xnimg, xv);
+  }
+  __syncthreads();
+
+  bf16x8 ring[P4][NF];
+  f32x16 acc[NF][4];
+  for (; chunk < nchunks; chunk += G) {
+    // ---- phase 1: a1 = relu(W0 x + b0) -> A1 image; the row scalars issued; W1 ring primed ----
+    OPAQUE_LANE();
+    uint4 sv[2];
+    load_srow(chunk, sv);
+#pragma unroll
+    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+      bf16x8 w0f[NF][2];
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          w0f[f][s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (64 * w + 32 * (ft0 + f) + r) * kFusedKX + 16 * s + 8 * h);
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const bf16x8 xb = lds_b128(xnimg + x_off(32 * t + r, 2 * s + h));
+#pragma unroll
+          for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(w0f[f][s], xb, acc[f][t]);
+        }
+      if (ft0 + NF >= 2) ring_prime4<NF>(w_frag_base<H>(N.w1b, 2 * w, lane), ring);  // for phase 2
+      drain_fence();
+      store_act<NF>(img1, b0s, acc, w, ft0, r, h);
+    }
+    __syncthreads();
+
+    // ---- phase 2: a2 = W1 a1; the row scalars staged (the S region is free) ----
+    OPAQUE_LANE();
+    *reinterpret_cast<uint4 *>(simg + (tid >> 1) * 64 + 32 * (tid & 1)) = sv[0];
+    *reinterpret_cast<uint4 *>(simg + (tid >> 1) * 64 + 32 * (tid & 1) + 16) = sv[1];
+#pragma unroll
+    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
+      pass4<NF>(w_frag_base<H>(N.w1b, 2 * w + ft0, lane), img1, r, h, ring, acc);
+      if (ft0 + NF < 2) ring_prime4<NF>(w_frag_base<H>(N.w1b, 2 * w + ft0 + NF, lane), ring);
+      // ---- phase 3: bias + ReLU -> A2 image ----
+      OPAQUE_LANE();
+      store_act<NF>(img2, b1s, acc, w, ft0, r, h);
+    }
+    __syncthreads();
+
+    // ---- phase 4: head z = a2 . W_h^T (16x16x32 MFMA), the per-(row, action) loss head -> dz
+    //      images.  Wave w: rows 32w..32w+31 as two 16-row tiles; lane -> head n = lane & 15,
+    //      rows 32w + 16u + 4 (lane >> 4) + i ----
+    OPAQUE_LANE();
+    uint4 xc[2];
+    load_x(chunk, xc);  // this chunk's states again, for the X image dW0 reads (phase 5)
+    {
+      const int n = lane & 15, qg = lane >> 4;
+      const float *const srl = reinterpret_cast<const float *>(simg);
+      f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < H / 32; ++s) {
+        const bf16x8 bh = lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          zacc[u] = mfma16_v(lds_b128(img2 + img_off(32 * w + 16 * u + n, 4 * s + qg, PITCH)), bh, zacc[u]);
+      }
+      drain_fence();
+      const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float dz[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lr = 32 * w + 16 * u + 4 * qg + i;
+          const bool valid = chunk * RR + lr < count;
+          const float *sp = srl + lr * kFusedSP;
+          dz[i] = 0.f;
+          if constexpr (ACTOR) {
+            const bool act_lane = n < A;
+            float y = 0.f, d = 0.f, lp = 0.f;
+            if (act_lane) {
+              float zz = zacc[u][i];
+              if (N.bh) zz += hbias[n];
+              y = tanhf(zz);
+              const float mu = q.omv * y;
+              const float x = valid ? sp[n] : mu;
+              d = x - mu;
+              lp = ((-(d * d)) * (0.5f * h_ivar) - h_lsd) - kLogSqrt2Pi;
+            }
+            const float logp = row16_sum(lp);
+            const float old_lp = valid ? sp[A] : logp;
+            const float adv = valid ? sp[A + 1] : 0.f;
+            const float ratio = expf(logp - old_lp);
+            const float s1 = ratio * adv;
+            const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+            const float s2 = cl * adv;
+            const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+            const float gg = -q.inv_b;
+            const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+            const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+            const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+            const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+            const float dlogp = valid ? dratio * ratio : 0.f;
+            if (act_lane) {
+              const float dmu = dlogp * (d * h_ivar);
+              dz[i] = (dmu * q.omv) * (1.f - y * y);
+              if (valid) {
+                g_ls += dlogp * ((d * d) * h_ivar - 1.f) - q.ent_coef * q.inv_ba;
+                g_bh += dz[i];
+              }
+            }
+            if (valid && n == 0) g_loss += mn;
+          } else {
+            if (n == 0) {
+              float v = zacc[u][i];
+              if (N.bh) v += hbias[0];
+              const float vt = valid ? sp[A + 2] : v;
+              const float diff = v - vt;
+              const float ad = fabsf(diff);
+              if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+              dz[i] = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
+              g_bh += dz[i];
+            }
+          }
+        }
+        const int lr0 = 32 * w + 16 * u + 4 * qg;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<uint16_t *>(dzimg + (lr0 + i) * kDzRowBytes + 2 * n) = bf16_bits4(dz[i]);
+        *reinterpret_cast<uint2 *>(dztimg + n * DZTP + 2 * lr0) =
+            make_uint2(pack2(dz[0], dz[1]), pack2(dz[2], dz[3]));
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 5: the X image for dW0; head dW += dz^T a2 (own features); d2 = (dz . W_h) *
+    //      ReLU'(a2) -> bias grad, D2 written over A2 in place (own columns: this wave's reads of
+    //      them above precede the writes in its LDS order) ----
+    OPAQUE_LANE();
+    store_x(simg, xc);
+#pragma unroll
+    for (int ks = 0; ks < RR / 32; ++ks) {
+      const bf16x8 af = lds_b128(dztimg + (lane & 15) * DZTP + 2 * (32 * ks + 8 * (lane >> 4)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ghw[j] = mfma16_v(af, tr_frag16(img2, PITCH, 32 * ks, 64 * w + 16 * j, lane), ghw[j]);
+    }
+    OPAQUE_LANE();
+#pragma unroll
+    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+      bf16x8 wht[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) wht[f] = head_t_frag<H>(whb, 2 * w + ft0 + f, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 dzb = lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(wht[f], dzb, zero16());
+      }
+      drain_fence();
+      backward_in_place<NF>(img2, acc, gb1, w, ft0, lane);
+    }
+    __syncthreads();
+
+    // ---- phase 6a: dW1 += D2^T A1 over the chunk's 128 rows (8 k-steps of 16 rows, the next
+    //      k-step's fragments read under the current one's MFMAs); the next chunk's states
+    //      prefetched and parked in the (now free) dz region ----
+    OPAQUE_LANE();
+    {
+      uint4 xn[2];
+      load_x(chunk + G, xn);
+#pragma unroll
+      for (int ks = 0; ks < RR / 16; ++ks) {
+        bf16x8 fa[2], fb[8];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) fa[a] = tr_frag(img2, PITCH, 16 * ks, 64 * w + 32 * a, lane);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) fb[b] = tr_frag(img1, PITCH, 16 * ks, 32 * b, lane);
+        if (ks == RR / 16 - 2) ring_prime4<NF>(w_frag_base<H>(N.w1bt, 2 * w, lane), ring);  // for 6b
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) mfma_agpr(gw1[a][b], fa[a], fb[b]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      store_x(xnimg, xn);
+    }
+
+    // ---- phase 6b: d1 = (W1^T d2) * ReLU'(a1) -> bias grad, D1 over A1 in place (after every
+    //      wave's dW1 reads of A1) ----
+#pragma unroll
+    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+      OPAQUE_LANE();
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
+      pass4<NF>(w_frag_base<H>(N.w1bt, 2 * w + ft0, lane), img2, r, h, ring, acc);
+      if (ft0 + NF < 2) ring_prime4<NF>(w_frag_base<H>(N.w1bt, 2 * w + ft0 + NF, lane), ring);
+      if (ft0 == 0) __syncthreads();  // every wave's dW1 reads of A1 done before D1 overwrites it
+      OPAQUE_LANE();
+      backward_in_place<NF>(img1, acc, gb0, w, ft0, lane);
+    }
+
+    // ---- phase 7: dW0 += D1^T X (the wave's own D1 columns; X staged in phase 5) ----
+    OPAQUE_LANE();
+#pragma unroll
+    for (int ks = 0; ks < RR / 16; ++ks) {
+      const bf16x8 xb = tr_frag_x(simg, 16 * ks, lane);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+        gw0[ft] = mfma_v(tr_frag(img1, PITCH, 16 * ks, 64 * w + 32 * ft, lane), xb, gw0[ft]);
+    }
+    __syncthreads();
+  }
+
+#undef OPAQUE_LANE
+  // ================= epilogue: one partial-gradient slab per workgroup =================
+  tid = tid0;
+  lane = tid & 63;
+  r = lane & 31;
+  h = lane >> 5;
+  float *slab = q.slabs + static_cast<int64_t>(blockIdx.x) * q.slab_stride;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int o0 = 32 * (2 * w + a), i0 = 32 * b;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        slab[N.off_w1 + static_cast<int64_t>(o0 + reg_feature(e, h)) * H + i0 + r] = gw1[a][b][e];
+    }
+  if (r < q.din) {
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        slab[N.off_w0 + static_cast<int64_t>(64 * w + 32 * ft + reg_feature(e, h)) * q.din + r] = gw0[ft][e];
+  }
+  if ((lane & 1) == 0) {
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) {
+      const int f = 64 * w + 32 * ft + rs16_feature(lane);
+      if (N.b1) slab[N.off_b1 + f] = gb1[ft];
+      if (N.b0) slab[N.off_b0 + f] = gb0[ft];
+    }
+  }
+  const int na = ACTOR ? A : 1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = 4 * (lane >> 4) + i;
+      if (a < na) slab[N.off_wh + static_cast<int64_t>(a) * H + 64 * w + 16 * j + (lane & 15)] = ghw[j][i];
+    }
+  // head bias / log-std / loss partials: the 4 lane groups of a wave in a fixed xor order, then
+  // waves 0..3 in order through LDS
+  float *red = reinterpret_cast<float *>(lds + L::RED);
+  g_bh += __shfl_xor(g_bh, 16, 64);
+  g_bh += __shfl_xor(g_bh, 32, 64);
+  g_ls += __shfl_xor(g_ls, 16, 64);
+  g_ls += __shfl_xor(g_ls, 32, 64);
+  g_loss += __shfl_xor(g_loss, 16, 64);
+  g_loss += __shfl_xor(g_loss, 32, 64);
+  if (lane < 16) {
+    float *dst = red + (w * 16 + lane) * 4;
+    dst[0] = g_bh;
+    dst[1] = g_ls;
+    dst[2] = g_loss;
+  }
+  __syncthreads();
+  if (tid < na) {
+    float sb = 0.f, sl = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW4; ++v) {
+      sb += red[(v * 16 + tid) * 4];
+      sl += red[(v * 16 + tid) * 4 + 1];
+    }
+    if (N.bh) slab[N.off_bh + tid] = sb;
+    if (ACTOR) slab[q.off_logstd + tid] = sl;
+  }
+  if (tid == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW4; ++v) s += red[(v * 16) * 4 + 2];
+    q.loss_part[2 * blockIdx.x + z] = s;
+  }
+}
+
+#ifndef F4_NF
+#define F4_NF 1
+#endif
+template <int NA>
+__global__ __launch_bounds__(NT4, 1) void fused_update4_kernel(FusedArgs q) {
+  __shared__ __attribute__((aligned(16))) char lds[Lds4::TOTAL];
+  if (blockIdx.y == 0) body4<NA, true, F4_NF>(q, q.net[0], lds);
+  else body4<1, false, F4_NF>(q, q.net[1], lds);
+}
+
+}  // namespace f4
+
+bool fused_update4_ok(const FusedArgs &q) {
+  return q.hidden == f4::H && q.act == PPO_ACT_RELU && q.act_dim >= 1 && q.act_dim <= kFusedMaxAct;
+}
+
+int fused_update4_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  PPO_REQUIRE(fused_update4_ok(q), "fused update (4 waves): ReLU, H = 256, act_dim <= 8 only");
+  PPO_REQUIRE(q.G >= 1 && q.G <= kFusedMaxWG, "fused update: bad workgroup count %d", q.G);
+  const dim3 grid(q.G, 2), block(f4::NT4);
+  if (q.act_dim <= 2) launch_k(rec, f4::fused_update4_kernel<2>, grid, block, 0, st, q);
+  else if (q.act_dim <= 4) launch_k(rec, f4::fused_update4_kernel<4>, grid, block, 0, st, q);
+  else if (q.act_dim <= 6) launch_k(rec, f4::fused_update4_kernel<6>, grid, block, 0, st, q);
+  else launch_k(rec, f4::fused_update4_kernel<8>, grid, block, 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+}  // namespace ppo

@@ -688,6 +688,8 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
 }
 
 static const int g_fused_enabled = env_knob("PPO_FUSED", 1);
+// PPO_FUSED4=1: the 4-wave / 128-row fused update (fused_update4.hip) for ReLU nets
+static const int g_fused4 = env_knob("PPO_FUSED4", 0);
 
 // Pointers of both nets for the fused kernels (bf16 images from ctx->fw, f32 masters in params).
 static void fused_nets(const ppo_ctx *ctx, FusedNet (&out)[2]) {
@@ -754,8 +756,11 @@ static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *ac
   q.slabs = ctx->fslabs;
   q.slab_stride = ctx->total_params;
   q.loss_part = ctx->floss;
-  q.G = std::min(kFusedMaxWG, ceil_div(b, kFusedRows));
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
+  // the 4-wave kernel when enabled (not with the phase-stamp diagnostics or the in-launch fold,
+  // which only the 8-wave kernel implements)
+  q.v4 = ctx->fused4 && !q.stamps && !ctx->fold_on && fused_update4_ok(q);
+  q.G = std::min(kFusedMaxWG, ceil_div(b, q.v4 ? kFused4Rows : kFusedRows));
   return q;
 }
 
@@ -788,12 +793,14 @@ static int fused_forward_backward(ppo_ctx *ctx, const FusedArgs &q, hipStream_t 
   // them from L2, which is not HBM traffic) and one partial-gradient slab per workgroup
   const double by = static_cast<double>(b) * (2.0 * kFusedKX + 4.0 * kFusedSP) +
                     4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
+  const int na = A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8;
   const TimRec rec{KC_FUSED,
-                   tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act,
-                                              A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8)
+                   tim_active() ? (q.v4 ? intern_name("ppo::f4::fused_update4_kernel<%d>", na)
+                                        : intern_name("fused_update_kernel<%d, %d, %d, false>", H,
+                                                      q.act, na))
                                 : nullptr,
                    fl, by};
-  return fused_update_launch(q, rec, st);
+  return q.v4 ? fused_update4_launch(q, rec, st) : fused_update_launch(q, rec, st);
 }
 
 static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, float *grad_d,
@@ -1082,6 +1089,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
         return PPO_EHIP;
       }
       ctx->fold_on = env_knob("PPO_FUSED_FOLD", 0);
+      ctx->fused4 = g_fused4 != 0;
     }
   }
   *out = ctx;
@@ -1831,6 +1839,14 @@ extern "C" int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable) {
   PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_fold: null ctx");
   if (enable < 0) return ctx->fold_on && ctx->fsync ? 1 : 0;
   ctx->fold_on = enable != 0;
+  return 0;
+}
+
+extern "C" int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_variant: null ctx");
+  if (variant < 0) return ctx->fused4 ? 4 : 8;
+  PPO_REQUIRE(variant == 4 || variant == 8, "ppo_ctx_fused_variant: variant %d (4 or 8)", variant);
+  ctx->fused4 = variant == 4;
   return 0;
 }
 

@@ -215,6 +215,13 @@ class Engine:
             check(self.lib.ppo_ctx_fused_fold(self._ctx, int(bool(enable))))
         return bool(self.lib.ppo_ctx_fused_fold(self._ctx, -1))
 
+    def fused_variant(self, variant: Optional[int] = None) -> int:
+        """The fused bf16 update kernel (ppo_ctx_fused_variant): 8 = 8 waves / 64-row chunks,
+        4 = one wave per SIMD / 128-row chunks (ReLU); set it with variant, return the current."""
+        if variant is not None:
+            check(self.lib.ppo_ctx_fused_variant(self._ctx, int(variant)))
+        return int(self.lib.ppo_ctx_fused_variant(self._ctx, -1))
+
     def check_device_errors(self) -> None:
         """Raise EngineError if a device-side failure was flagged since the last check (the
         fold's grid barrier timing out).  Synchronises the host."""

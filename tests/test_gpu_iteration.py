@@ -61,7 +61,8 @@ def test_single_minibatch_update_tight(gpu):
                         cfg.learning_rate, label="single minibatch")
 
 
-def test_bf16_iteration_matches_bf16_emulation(gpu):
+@pytest.mark.parametrize("variant", [8, 4])
+def test_bf16_iteration_matches_bf16_emulation(gpu, variant):
     """precision="bf16" (BASELINE configs[1], fused kernels at 2x256): one full iteration
     against the oracle with the same bf16 operand rounding (oracle.use_bf16_gemms) on the
     same torch RNG streams.  Residual: f32 summation order, which occasionally flips the bf16
@@ -72,6 +73,7 @@ def test_bf16_iteration_matches_bf16_emulation(gpu):
     algo, agent, ref, env, cfg = _setup(gpu, n=256, t=32, b=2048, epochs=2, hidden=(256, 256),
                                         precision="bf16", p_term=0.02)
     assert agent.engine.fused
+    agent.engine.fused_variant(variant)  # 8: fused_update_kernel, 4: fused_update4_kernel
     R.use_bf16_gemms(ref)
     p0 = R.flat_params(ref).clone()
     mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg)
@@ -151,36 +153,45 @@ def test_bf16_wide_iteration_matches_bf16_emulation(gpu):
     adv_own, vt_own = own_gae(mem, cfg)
     assert torch.equal(mem["advantage"].cpu(), adv_own)
     assert torch.equal(mem["current_state_value_target"].cpu(), vt_own)
+    roll_bad = []
     for key in ("current_state_value", "action", "action_log_prob"):
         a, r = mem[key].cpu(), ref_mem[key]
         err = float((a - r).abs().max()) / (float(r.abs().max()) + 1e-6)
         print(f"wide bf16 rollout {key}: max err {err:.3e} of scale")
-        assert err <= 2e-3, (key, err)
+        if err > 2e-3:
+            roll_bad.append((key, err))
     rows0 = replay_rows(99, n, t, b, 2, 17)[0]
     g64 = _first_step_grad_f64(ref0, mem, rows0, n, t, cfg)
-    worst, worst_l2 = 0.0, 0.0
+    worst, worst_l2, bad = 0.0, 0.0, []
     for name, lo, hi in tensor_slices(ref):
         ge, gr = g_eng[0][lo:hi].double(), g64[lo:hi]
         err = float((ge - gr).abs().max()) / (float(gr.abs().max()) + 1e-30)
         l2 = float((ge - gr).norm() / (gr.norm() + 1e-30))
+        print(f"wide bf16 first-step grad {name}: err {err:.3e} of max, rel L2 {l2:.3e}")
         worst, worst_l2 = max(worst, err), max(worst_l2, l2)
-        assert err <= 1e-2 and l2 <= 5e-3, (name, err, l2)
+        if not (err <= 1e-2 and l2 <= 5e-3):
+            bad.append((name, err, l2))
     print(f"wide bf16 first-step grad vs f64 emulation: worst {worst:.3e} of max, rel L2 "
           f"{worst_l2:.3e}")
+    grad_bad = bad
     p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
     steps = len(g_ref)
     assert steps == 8
     dmax = float((p_eng - p_ref).abs().max())
     print(f"wide bf16 params: max |diff| {dmax:.3e} (bound {2 * cfg.learning_rate * steps:.1e})")
     assert dmax <= 2 * cfg.learning_rate * steps
-    worst_u = 0.0
+    worst_u, bad = 0.0, []
     for name, lo, hi in tensor_slices(ref):
         du_e, du_r = p_eng[lo:hi] - p0[lo:hi], p_ref[lo:hi] - p0[lo:hi]
         rel = float((du_e - du_r).norm() / (du_r.norm() + 1e-20))
         worst_u = max(worst_u, rel)
         print(f"wide bf16 update {name}: rel L2 {rel:.3e}")
-        assert rel <= 5e-3, (name, rel)
+        if rel > 5e-3:
+            bad.append((name, rel))
     print(f"wide bf16 update: worst rel L2 {worst_u:.3e}")
+    assert not bad, bad
+    assert not roll_bad, roll_bad
+    assert not grad_bad, grad_bad
 
 
 def test_philox_mode_runs_and_is_reproducible(gpu):
@@ -195,9 +206,10 @@ def test_philox_mode_runs_and_is_reproducible(gpu):
     assert torch.equal(outs[0], outs[1]), "philox mode must be bit-reproducible"
 
 
-@pytest.mark.parametrize("prec,hidden,n,b", [("f32", (64, 64), 64, 256),
-                                             ("bf16", (256, 256), 128, 512)])
-def test_graphs_match_eager(gpu, prec, hidden, n, b):
+@pytest.mark.parametrize("prec,hidden,n,b,variant", [("f32", (64, 64), 64, 256, 8),
+                                                     ("bf16", (256, 256), 128, 512, 8),
+                                                     ("bf16", (256, 256), 128, 512, 4)])
+def test_graphs_match_eager(gpu, prec, hidden, n, b, variant):
     """rollout_graph / train_graph (each captured once, replayed with the device Philox counter,
     the pre-drawn minibatch rows and the device Adam schedule) produce the same buffers and
     parameters, bit for bit, as the eager launch sequence over 3 iterations (iteration 0 eager
@@ -206,6 +218,8 @@ def test_graphs_match_eager(gpu, prec, hidden, n, b):
     for graph in (False, True):
         algo, agent, *_ = _setup(gpu, n=n, t=16, b=b, epochs=2, hidden=hidden, rng="philox",
                                  seed=4, rollout_graph=graph, train_graph=graph, precision=prec)
+        if prec == "bf16":
+            agent.engine.fused_variant(variant)
         snaps = []
         for _ in range(3):
             algo.iterate(verbose=False)

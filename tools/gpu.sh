@@ -35,7 +35,7 @@ for S in $STEPS; do
   echo "=== $S ($(date +%T))"
   case $S in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu ${NOX:--x} -v --timeout 300 --timeout-method thread \
         ${K:+-k "$K"} -s > gpurun_out/gpu_tests_${TAG}.log 2>&1 || fail tests gpurun_out/gpu_tests_${TAG}.log
       grep -E "passed|failed" gpurun_out/gpu_tests_${TAG}.log | tail -2 ;;
     smoke)
@@ -142,6 +142,13 @@ for S in $STEPS; do
       timeout -k 10 500 python bench.py --model lstm --steps 2 --warmup 1 \
         > gpurun_out/bench_${TAG}_lstm.json 2> gpurun_out/bench_${TAG}_lstm.err || fail lstm gpurun_out/bench_${TAG}_lstm.err
       for c in ant hum8k cnn lstm; do cut -c1-200 gpurun_out/bench_${TAG}_$c.json; done ;;
+    ab4)
+      # the fused update kernel variants on the headline line: 8 waves / 64 rows vs 4 waves / 128
+      for V in 0 1; do
+        PPO_FUSED4=$V timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $BENCH_ARGS \
+          > gpurun_out/bench_${TAG}_f4_$V.json 2> gpurun_out/bench_${TAG}_f4_$V.err || fail ab4 gpurun_out/bench_${TAG}_f4_$V.err
+        cut -c1-600 gpurun_out/bench_${TAG}_f4_$V.json
+      done ;;
     wbench)
       timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
       cat gpurun_out/wbench_${TAG}.txt ;;
