@@ -21,6 +21,9 @@
 // product with f32 accumulation; biases, ReLU', the loss heads and every bias gradient in f32.
 // Summation orders differ from fused_update_kernel (the head z is one K=256 chain here), so the
 // two kernels agree to f32 rounding, not bitwise; each is bitwise deterministic run to run.
+#include <cstdlib>
+#include <type_traits>
+
 #include "fused_common.h"
 
 namespace ppo {
@@ -36,9 +39,15 @@ constexpr int NT4 = 64 * NW4;
 constexpr int PITCH = 2 * H;       // A1 / A2 image row pitch (bytes)
 constexpr int DZTP = 2 * (RR + 8); // head-major dz image pitch (bytes)
 constexpr int KS = H / 16;         // k-steps of a 32x32x16 pass over H
-constexpr int PD4 = 3;             // weight-ring prefetch distance (k-steps)
-constexpr int P4 = PD4 + 1;        // ring period (divides KS)
-static_assert(KS % P4 == 0, "ring period must divide the k-steps");
+// Latency hiding with one wave per SIMD: PD = weight-ring prefetch distance (k-steps), BD =
+// B-operand lookahead (k-steps).  Compiled configurations (ppo_ctx_fused_variant / PPO_F4_CFG):
+// 0 = (7, 1), 1 = (3, 4), 2 = (7, 2).
+template <int PD_, int BD_>
+struct Cfg4 {
+  static constexpr int PD = PD_, P = PD_ + 1, BD = BD_;
+  static_assert(KS % P == 0, "ring period must divide the k-steps");
+  static_assert(P % BD == 0, "B slots must cycle within a ring period");
+};
 
 struct Lds4 {
   static constexpr int WHB = 0;                              // bf16 head image [16][H + 8]
@@ -99,63 +108,67 @@ __device__ __forceinline__ void drain8(f32x16 (&)[2][NACC]) { drain_fence(); }
 // acc[f][rt] += W[64w + 32(ft0 + f) + r][:] . img[32rt + r][:] over k = 0..H-1 for f < NF: A
 // operands from the fragment-major bf16 weight image (wf = the first tile's base for this lane),
 // B operands 16-B row reads of the LDS image (row tile t's next k-step read issued as soon as its
-// MFMAs have issued); weights PD4 k-steps ahead through the ring.
-template <int NF>
+// MFMAs have issued); weights C::PD k-steps ahead through the ring.
+template <int NF, class C>
 __device__ __forceinline__ void pass4(const __bf16 *wf, const char *img, int r, int h,
-                                      bf16x8 (&ring)[P4][NF], f32x16 (&acc)[NF][4]) {
+                                      bf16x8 (&ring)[C::P][NF], f32x16 (&acc)[NF][4]) {
   const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
   const char *rowp = img + r * PITCH;
   constexpr int64_t STEP = 16 * H;  // elements per k-step of the fragment-major image
   constexpr int64_t TILE = 64 * 8;  // elements per 32-feature tile of one k-step
-  bf16x8 bc[4];
+  // B operands BD k-steps ahead: slot s % BD holds k-step s; row tile t's read of step s + BD is
+  // issued right after its MFMAs of step s (one wave per SIMD: nothing else hides LDS latency)
+  bf16x8 bq[C::BD][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * (h ^ swz));
+  for (int j = 0; j < C::BD; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bq[j][t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * j + h) ^ swz));
 #pragma unroll 1
-  for (int s0 = 0; s0 < KS - P4; s0 += P4) {
+  for (int s0 = 0; s0 < KS - C::P; s0 += C::P) {
 #pragma unroll
-    for (int u = 0; u < P4; ++u) {
+    for (int u = 0; u < C::P; ++u) {
       const int s = s0 + u;
       bf16x8 a[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         a[f] = ring[u][f];
-        ring[(u + PD4) % P4][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + PD4) + TILE * f);
+        ring[(u + C::PD) % C::P][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + C::PD) + TILE * f);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
-        for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bc[t], acc[f][t]);
-        bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * s + 2 + h) ^ swz));
+        for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bq[u % C::BD][t], acc[f][t]);
+        bq[u % C::BD][t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * (s + C::BD) + h) ^ swz));
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
   // last period peeled: no weight prefetch past the end, no B read past the last k-step
 #pragma unroll
-  for (int u = 0; u < P4; ++u) {
-    const int s = KS - P4 + u;
+  for (int u = 0; u < C::P; ++u) {
+    const int s = KS - C::P + u;
     bf16x8 a[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       a[f] = ring[u][f];
-      if (s + PD4 < KS)
-        ring[(u + PD4) % P4][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + PD4) + TILE * f);
+      if (s + C::PD < KS)
+        ring[(u + C::PD) % C::P][f] = *reinterpret_cast<const bf16x8 *>(wf + STEP * (s + C::PD) + TILE * f);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bc[t], acc[f][t]);
-      if (s + 1 < KS) bc[t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * s + 2 + h) ^ swz));
+      for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(a[f], bq[u % C::BD][t], acc[f][t]);
+      if (s + C::BD < KS) bq[u % C::BD][t] = lds_b128(rowp + t * 32 * PITCH + 16 * ((2 * (s + C::BD) + h) ^ swz));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   drain_fence();
 }
 
-template <int NF>
-__device__ __forceinline__ void ring_prime4(const __bf16 *wf, bf16x8 (&ring)[P4][NF]) {
+template <int NF, class C>
+__device__ __forceinline__ void ring_prime4(const __bf16 *wf, bf16x8 (&ring)[C::P][NF]) {
 #pragma unroll
-  for (int s = 0; s < PD4; ++s)
+  for (int s = 0; s < C::PD; ++s)
 #pragma unroll
     for (int f = 0; f < NF; ++f)
       ring[s][f] = *reinterpret_cast<const bf16x8 *>(wf + static_cast<int64_t>(16 * H) * s + 64 * 8 * f);
@@ -216,7 +229,7 @@ __device__ __forceinline__ void backward_in_place(char *img, f32x16 (&acc)[NF][4
 }
 
 // One net's workgroup.  NH: head width (actor A padded, or 1), ACTOR selects the loss head.
-template <int NH, bool ACTOR, int NF>
+template <int NH, bool ACTOR, int NF, class C, bool STAMP>
 __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, char *lds) {
   using L = Lds4;
   constexpr int z = ACTOR ? 0 : 1;
@@ -243,6 +256,22 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
   lane = tid & 63;              \
   r = lane & 31;                \
   h = lane >> 5
+  // STAMP (diagnostic build, ppo_ctx_phase_stamps): s_memtime deltas per phase segment summed over
+  // the chunks (wave 0's view; a segment ending at a barrier includes the wait for the others)
+  uint64_t t_prev = 0, t_real0 = 0, t_acc[kStampSlots];
+  if constexpr (STAMP) {
+#pragma unroll
+    for (int k = 0; k < kStampSlots; ++k) t_acc[k] = 0;
+    t_prev = __builtin_amdgcn_s_memtime();
+    t_real0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+#define STAMP4(k)                                         \
+  if constexpr (STAMP) {                                  \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();  \
+    t_acc[k] += t_now - t_prev;                           \
+    t_prev = t_now;                                       \
+  }
   const int A = q.act_dim;
   const int G = q.G;
   const int nchunks = (q.b + RR - 1) / RR;
@@ -317,8 +346,9 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     store_x(xnimg, xv);
   }
   __syncthreads();
+  STAMP4(0);
 
-  bf16x8 ring[P4][NF];
+  bf16x8 ring[C::P][NF];
   f32x16 acc[NF][4];
   for (; chunk < nchunks; chunk += G) {
     // ---- phase 1: a1 = relu(W0 x + b0) -> A1 image; the row scalars issued; W1 ring primed ----
@@ -345,11 +375,13 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
 #pragma unroll
           for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(w0f[f][s], xb, acc[f][t]);
         }
-      if (ft0 + NF >= 2) ring_prime4<NF>(w_frag_base<H>(N.w1b, 2 * w, lane), ring);  // for phase 2
+      if (ft0 + NF >= 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1b, 2 * w, lane), ring);  // for phase 2
       drain_fence();
       store_act<NF>(img1, b0s, acc, w, ft0, r, h);
     }
+    STAMP4(1);
     __syncthreads();
+    STAMP4(2);
 
     // ---- phase 2: a2 = W1 a1; the row scalars staged (the S region is free) ----
     OPAQUE_LANE();
@@ -361,13 +393,15 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
       for (int f = 0; f < NF; ++f)
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
-      pass4<NF>(w_frag_base<H>(N.w1b, 2 * w + ft0, lane), img1, r, h, ring, acc);
-      if (ft0 + NF < 2) ring_prime4<NF>(w_frag_base<H>(N.w1b, 2 * w + ft0 + NF, lane), ring);
+      pass4<NF, C>(w_frag_base<H>(N.w1b, 2 * w + ft0, lane), img1, r, h, ring, acc);
+      if (ft0 + NF < 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1b, 2 * w + ft0 + NF, lane), ring);
       // ---- phase 3: bias + ReLU -> A2 image ----
       OPAQUE_LANE();
       store_act<NF>(img2, b1s, acc, w, ft0, r, h);
     }
+    STAMP4(3);
     __syncthreads();
+    STAMP4(4);
 
     // ---- phase 4: head z = a2 . W_h^T (16x16x32 MFMA), the per-(row, action) loss head -> dz
     //      images.  Wave w: rows 32w..32w+31 as two 16-row tiles; lane -> head n = lane & 15,
@@ -453,7 +487,9 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
             make_uint2(pack2(dz[0], dz[1]), pack2(dz[2], dz[3]));
       }
     }
+    STAMP4(5);
     __syncthreads();
+    STAMP4(6);
 
     // ---- phase 5: the X image for dW0; head dW += dz^T a2 (own features); d2 = (dz . W_h) *
     //      ReLU'(a2) -> bias grad, D2 written over A2 in place (own columns: this wave's reads of
@@ -481,7 +517,9 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
       drain_fence();
       backward_in_place<NF>(img2, acc, gb1, w, ft0, lane);
     }
+    STAMP4(7);
     __syncthreads();
+    STAMP4(8);
 
     // ---- phase 6a: dW1 += D2^T A1 over the chunk's 128 rows (8 k-steps of 16 rows, the next
     //      k-step's fragments read under the current one's MFMAs); the next chunk's states
@@ -490,22 +528,30 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     {
       uint4 xn[2];
       load_x(chunk + G, xn);
+      // fragments of k-step ks + 1 read under k-step ks's 16 MFMAs
+      bf16x8 fa[2][2], fb[2][8];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) fa[0][a] = tr_frag(img2, PITCH, 0, 64 * w + 32 * a, lane);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) fb[0][b] = tr_frag(img1, PITCH, 0, 32 * b, lane);
 #pragma unroll
       for (int ks = 0; ks < RR / 16; ++ks) {
-        bf16x8 fa[2], fb[8];
+        const int cu = ks & 1, nx = cu ^ 1;
+        if (ks == RR / 16 - 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1bt, 2 * w, lane), ring);  // for 6b
 #pragma unroll
-        for (int a = 0; a < 2; ++a) fa[a] = tr_frag(img2, PITCH, 16 * ks, 64 * w + 32 * a, lane);
+        for (int b = 0; b < 8; ++b) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) fb[b] = tr_frag(img1, PITCH, 16 * ks, 32 * b, lane);
-        if (ks == RR / 16 - 2) ring_prime4<NF>(w_frag_base<H>(N.w1bt, 2 * w, lane), ring);  // for 6b
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-#pragma unroll
-          for (int a = 0; a < 2; ++a) mfma_agpr(gw1[a][b], fa[a], fb[b]);
+          for (int a = 0; a < 2; ++a) mfma_agpr(gw1[a][b], fa[cu][a], fb[cu][b]);
+          if (ks + 1 < RR / 16) {
+            if (b < 2) fa[nx][b] = tr_frag(img2, PITCH, 16 * (ks + 1), 64 * w + 32 * b, lane);
+            fb[nx][b] = tr_frag(img1, PITCH, 16 * (ks + 1), 32 * b, lane);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       store_x(xnimg, xn);
     }
+    STAMP4(9);
 
     // ---- phase 6b: d1 = (W1^T d2) * ReLU'(a1) -> bias grad, D1 over A1 in place (after every
     //      wave's dW1 reads of A1) ----
@@ -516,8 +562,8 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
       for (int f = 0; f < NF; ++f)
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
-      pass4<NF>(w_frag_base<H>(N.w1bt, 2 * w + ft0, lane), img2, r, h, ring, acc);
-      if (ft0 + NF < 2) ring_prime4<NF>(w_frag_base<H>(N.w1bt, 2 * w + ft0 + NF, lane), ring);
+      pass4<NF, C>(w_frag_base<H>(N.w1bt, 2 * w + ft0, lane), img2, r, h, ring, acc);
+      if (ft0 + NF < 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1bt, 2 * w + ft0 + NF, lane), ring);
       if (ft0 == 0) __syncthreads();  // every wave's dW1 reads of A1 done before D1 overwrites it
       OPAQUE_LANE();
       backward_in_place<NF>(img1, acc, gb0, w, ft0, lane);
@@ -533,6 +579,7 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
         gw0[ft] = mfma_v(tr_frag(img1, PITCH, 16 * ks, 64 * w + 32 * ft, lane), xb, gw0[ft]);
     }
     __syncthreads();
+    STAMP4(10);
   }
 
 #undef OPAQUE_LANE
@@ -606,16 +653,30 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     for (int v = 0; v < NW4; ++v) s += red[(v * 16) * 4 + 2];
     q.loss_part[2 * blockIdx.x + z] = s;
   }
+  if constexpr (STAMP) {  // after every wave's slab stores have drained
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    STAMP4(11);
+    t_acc[12] = __builtin_amdgcn_s_memrealtime() - t_real0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (tid0 == 0) {
+      uint64_t *dst = q.stamps + (static_cast<int64_t>(z) * gridDim.x + blockIdx.x) * kStampSlots;
+#pragma unroll
+      for (int k = 0; k < kStampSlots; ++k) dst[k] = t_acc[k];
+    }
+  }
+#undef STAMP4
 }
 
-#ifndef F4_NF
-#define F4_NF 1
-#endif
-template <int NA>
+template <int CFG>
+using CfgOf = typename std::conditional<CFG == 0, Cfg4<7, 1>,
+                                        typename std::conditional<CFG == 1, Cfg4<3, 4>, Cfg4<7, 2>>::type>::type;
+
+template <int NA, int CFG, bool STAMP>
 __global__ __launch_bounds__(NT4, 1) void fused_update4_kernel(FusedArgs q) {
   __shared__ __attribute__((aligned(16))) char lds[Lds4::TOTAL];
-  if (blockIdx.y == 0) body4<NA, true, F4_NF>(q, q.net[0], lds);
-  else body4<1, false, F4_NF>(q, q.net[1], lds);
+  if (blockIdx.y == 0) body4<NA, true, 1, CfgOf<CFG>, STAMP>(q, q.net[0], lds);
+  else body4<1, false, 1, CfgOf<CFG>, STAMP>(q, q.net[1], lds);
 }
 
 }  // namespace f4
@@ -624,14 +685,32 @@ bool fused_update4_ok(const FusedArgs &q) {
   return q.hidden == f4::H && q.act == PPO_ACT_RELU && q.act_dim >= 1 && q.act_dim <= kFusedMaxAct;
 }
 
+template <int CFG>
+static void launch4_cfg(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  const dim3 grid(q.G, 2), block(f4::NT4);
+  if (q.stamps) {  // diagnostic build: the headline head width only
+    launch_k(rec, f4::fused_update4_kernel<6, CFG, true>, grid, block, 0, st, q);
+    return;
+  }
+  if (q.act_dim <= 2) launch_k(rec, f4::fused_update4_kernel<2, CFG, false>, grid, block, 0, st, q);
+  else if (q.act_dim <= 4) launch_k(rec, f4::fused_update4_kernel<4, CFG, false>, grid, block, 0, st, q);
+  else if (q.act_dim <= 6) launch_k(rec, f4::fused_update4_kernel<6, CFG, false>, grid, block, 0, st, q);
+  else launch_k(rec, f4::fused_update4_kernel<8, CFG, false>, grid, block, 0, st, q);
+}
+
+static const int g_f4_cfg = [] {
+  const char *v = getenv("PPO_F4_CFG");
+  return v ? atoi(v) : 0;
+}();
+
 int fused_update4_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   PPO_REQUIRE(fused_update4_ok(q), "fused update (4 waves): ReLU, H = 256, act_dim <= 8 only");
   PPO_REQUIRE(q.G >= 1 && q.G <= kFusedMaxWG, "fused update: bad workgroup count %d", q.G);
-  const dim3 grid(q.G, 2), block(f4::NT4);
-  if (q.act_dim <= 2) launch_k(rec, f4::fused_update4_kernel<2>, grid, block, 0, st, q);
-  else if (q.act_dim <= 4) launch_k(rec, f4::fused_update4_kernel<4>, grid, block, 0, st, q);
-  else if (q.act_dim <= 6) launch_k(rec, f4::fused_update4_kernel<6>, grid, block, 0, st, q);
-  else launch_k(rec, f4::fused_update4_kernel<8>, grid, block, 0, st, q);
+  PPO_REQUIRE(!q.stamps || (q.act_dim > 4 && q.act_dim <= 6),
+              "fused update (4 waves): phase stamps only for act_dim 5-6");
+  if (g_f4_cfg == 1) launch4_cfg<1>(q, rec, st);
+  else if (g_f4_cfg == 2) launch4_cfg<2>(q, rec, st);
+  else launch4_cfg<0>(q, rec, st);
   PPO_LAUNCHED();
   return 0;
 }

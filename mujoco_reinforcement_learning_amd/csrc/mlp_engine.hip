@@ -759,7 +759,8 @@ static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *ac
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
   // the 4-wave kernel when enabled (not with the phase-stamp diagnostics or the in-launch fold,
   // which only the 8-wave kernel implements)
-  q.v4 = ctx->fused4 && !q.stamps && !ctx->fold_on && fused_update4_ok(q);
+  q.v4 = ctx->fused4 && !ctx->fold_on && fused_update4_ok(q) &&
+         (!q.stamps || (q.act_dim > 4 && q.act_dim <= 6));
   q.G = std::min(kFusedMaxWG, ceil_div(b, q.v4 ? kFused4Rows : kFusedRows));
   return q;
 }

@@ -144,10 +144,15 @@ for S in $STEPS; do
       for c in ant hum8k cnn lstm; do cut -c1-200 gpurun_out/bench_${TAG}_$c.json; done ;;
     ab4)
       # the fused update kernel variants on the headline line: 8 waves / 64 rows vs 4 waves / 128
-      for V in 0 1; do
-        PPO_FUSED4=$V timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $BENCH_ARGS \
-          > gpurun_out/bench_${TAG}_f4_$V.json 2> gpurun_out/bench_${TAG}_f4_$V.err || fail ab4 gpurun_out/bench_${TAG}_f4_$V.err
-        cut -c1-600 gpurun_out/bench_${TAG}_f4_$V.json
+      for V in ${AB4:-"0:0 1:0 1:1 1:2"}; do
+        PPO_FUSED4=${V%%:*} PPO_F4_CFG=${V##*:} timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $BENCH_ARGS \
+          > gpurun_out/bench_${TAG}_f4_${V/:/_}.json 2> gpurun_out/bench_${TAG}_f4_${V/:/_}.err || fail ab4 gpurun_out/bench_${TAG}_f4_${V/:/_}.err
+        python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value']/1e6,2), 'M', round(d['ms_per_step'],3), 'ms', r['kernel'], round(r['avg_launch_us'],2), 'us', round(r['frac'],4))" gpurun_out/bench_${TAG}_f4_${V/:/_}.json $V
+      done ;;
+    phases4)
+      for C in ${F4CFGS:-0 1 2}; do
+        PPO_F4_CFG=$C timeout -k 10 200 python tools/fused_phases.py 4 > gpurun_out/phases4_${TAG}_$C.txt 2>&1 || fail phases4 gpurun_out/phases4_${TAG}_$C.txt
+        echo "cfg $C"; cat gpurun_out/phases4_${TAG}_$C.txt
       done ;;
     wbench)
       timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
