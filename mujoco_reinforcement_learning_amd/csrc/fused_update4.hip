@@ -355,29 +355,34 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     OPAQUE_LANE();
     uint4 sv[2];
     load_srow(chunk, sv);
+    {
+      // every operand issued up front (one wave per SIMD: no partner hides a load's latency)
+      bf16x8 w0f[2][2], xb[2][4];
 #pragma unroll
-    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
-      bf16x8 w0f[NF][2];
-#pragma unroll
-      for (int f = 0; f < NF; ++f)
+      for (int ft = 0; ft < 2; ++ft)
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-          w0f[f][s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (64 * w + 32 * (ft0 + f) + r) * kFusedKX + 16 * s + 8 * h);
-#pragma unroll
-      for (int f = 0; f < NF; ++f)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
+          w0f[ft][s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (64 * w + 32 * ft + r) * kFusedKX + 16 * s + 8 * h);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const bf16x8 xb = lds_b128(xnimg + x_off(32 * t + r, 2 * s + h));
+        for (int t = 0; t < 4; ++t) xb[s][t] = lds_b128(xnimg + x_off(32 * t + r, 2 * s + h));
 #pragma unroll
-          for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(w0f[f][s], xb, acc[f][t]);
-        }
-      if (ft0 + NF >= 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1b, 2 * w, lane), ring);  // for phase 2
-      drain_fence();
-      store_act<NF>(img1, b0s, acc, w, ft0, r, h);
+      for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[f][t] = zero16();
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(w0f[ft0 + f][s], xb[s][t], acc[f][t]);
+        if (ft0 + NF >= 2) ring_prime4<NF, C>(w_frag_base<H>(N.w1b, 2 * w, lane), ring);  // for phase 2
+        drain_fence();
+        store_act<NF>(img1, b0s, acc, w, ft0, r, h);
+      }
     }
     STAMP4(1);
     __syncthreads();
@@ -413,12 +418,18 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
       const int n = lane & 15, qg = lane >> 4;
       const float *const srl = reinterpret_cast<const float *>(simg);
       f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      {
+        bf16x8 bh[H / 32], za[2][H / 32];
 #pragma unroll
-      for (int s = 0; s < H / 32; ++s) {
-        const bf16x8 bh = lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg));
+        for (int s = 0; s < H / 32; ++s) {
+          bh[s] = lds_b128(whb + n * HeadImg<H>::PITCH + 2 * (32 * s + 8 * qg));
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-          zacc[u] = mfma16_v(lds_b128(img2 + img_off(32 * w + 16 * u + n, 4 * s + qg, PITCH)), bh, zacc[u]);
+          for (int u = 0; u < 2; ++u) za[u][s] = lds_b128(img2 + img_off(32 * w + 16 * u + n, 4 * s + qg, PITCH));
+        }
+#pragma unroll
+        for (int s = 0; s < H / 32; ++s)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) zacc[u] = mfma16_v(za[u][s], bh[s], zacc[u]);
       }
       drain_fence();
       const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
@@ -496,26 +507,33 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     //      them above precede the writes in its LDS order) ----
     OPAQUE_LANE();
     store_x(simg, xc);
+    {
+      // head dW and d2 operands all issued up front (the head dW MFMAs hide the d2 reads)
+      bf16x8 af[RR / 32], bt[RR / 32][4], wht[2], dzb[4];
 #pragma unroll
-    for (int ks = 0; ks < RR / 32; ++ks) {
-      const bf16x8 af = lds_b128(dztimg + (lane & 15) * DZTP + 2 * (32 * ks + 8 * (lane >> 4)));
+      for (int ks = 0; ks < RR / 32; ++ks) {
+        af[ks] = lds_b128(dztimg + (lane & 15) * DZTP + 2 * (32 * ks + 8 * (lane >> 4)));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ghw[j] = mfma16_v(af, tr_frag16(img2, PITCH, 32 * ks, 64 * w + 16 * j, lane), ghw[j]);
-    }
-    OPAQUE_LANE();
-#pragma unroll
-    for (int ft0 = 0; ft0 < 2; ft0 += NF) {
-      bf16x8 wht[NF];
-#pragma unroll
-      for (int f = 0; f < NF; ++f) wht[f] = head_t_frag<H>(whb, 2 * w + ft0 + f, lane);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 dzb = lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h);
-#pragma unroll
-        for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(wht[f], dzb, zero16());
+        for (int j = 0; j < 4; ++j) bt[ks][j] = tr_frag16(img2, PITCH, 32 * ks, 64 * w + 16 * j, lane);
       }
-      drain_fence();
-      backward_in_place<NF>(img2, acc, gb1, w, ft0, lane);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) wht[ft] = head_t_frag<H>(whb, 2 * w + ft, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dzb[t] = lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h);
+#pragma unroll
+      for (int ks = 0; ks < RR / 32; ++ks)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ghw[j] = mfma16_v(af[ks], bt[ks][j], ghw[j]);
+      OPAQUE_LANE();
+#pragma unroll
+      for (int ft0 = 0; ft0 < 2; ft0 += NF) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int f = 0; f < NF; ++f) acc[f][t] = mfma_v(wht[ft0 + f], dzb[t], zero16());
+        drain_fence();
+        backward_in_place<NF>(img2, acc, gb1, w, ft0, lane);
+      }
     }
     STAMP4(7);
     __syncthreads();
@@ -571,12 +589,18 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
 
     // ---- phase 7: dW0 += D1^T X (the wave's own D1 columns; X staged in phase 5) ----
     OPAQUE_LANE();
+    {
+      bf16x8 xb[RR / 16], d1f[RR / 16][2];
 #pragma unroll
-    for (int ks = 0; ks < RR / 16; ++ks) {
-      const bf16x8 xb = tr_frag_x(simg, 16 * ks, lane);
+      for (int ks = 0; ks < RR / 16; ++ks) {
+        xb[ks] = tr_frag_x(simg, 16 * ks, lane);
 #pragma unroll
-      for (int ft = 0; ft < 2; ++ft)
-        gw0[ft] = mfma_v(tr_frag(img1, PITCH, 16 * ks, 64 * w + 32 * ft, lane), xb, gw0[ft]);
+        for (int ft = 0; ft < 2; ++ft) d1f[ks][ft] = tr_frag(img1, PITCH, 16 * ks, 64 * w + 32 * ft, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < RR / 16; ++ks)
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft) gw0[ft] = mfma_v(d1f[ks][ft], xb[ks], gw0[ft]);
     }
     __syncthreads();
     STAMP4(10);
