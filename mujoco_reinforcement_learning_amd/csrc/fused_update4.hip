@@ -205,6 +205,14 @@ __device__ __forceinline__ void backward_in_place(char *img, f32x16 (&acc)[NF][4
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     const int ft = ft0 + f;
+    // every activation read issued before any write: the compiler cannot prove the swizzled
+    // addresses distinct, so interleaved read / write pairs would each wait out an LDS round trip
+    uint2 yv[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        yv[t][g] = *reinterpret_cast<const uint2 *>(img + img_off(32 * t + r, 8 * w + 4 * ft + g, PITCH) + 8 * h);
     float bsum[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
@@ -212,18 +220,21 @@ __device__ __forceinline__ void backward_in_place(char *img, f32x16 (&acc)[NF][4
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        char *p = img + img_off(32 * t + r, 8 * w + 4 * ft + g, PITCH) + 8 * h;
-        const uint2 yv = *reinterpret_cast<const uint2 *>(p);
-        const float d0 = act_backward(acc[f][t][4 * g], bf_lo(yv.x), PPO_ACT_RELU);
-        const float d1 = act_backward(acc[f][t][4 * g + 1], bf_hi(yv.x), PPO_ACT_RELU);
-        const float d2 = act_backward(acc[f][t][4 * g + 2], bf_lo(yv.y), PPO_ACT_RELU);
-        const float d3 = act_backward(acc[f][t][4 * g + 3], bf_hi(yv.y), PPO_ACT_RELU);
+        const float d0 = act_backward(acc[f][t][4 * g], bf_lo(yv[t][g].x), PPO_ACT_RELU);
+        const float d1 = act_backward(acc[f][t][4 * g + 1], bf_hi(yv[t][g].x), PPO_ACT_RELU);
+        const float d2 = act_backward(acc[f][t][4 * g + 2], bf_lo(yv[t][g].y), PPO_ACT_RELU);
+        const float d3 = act_backward(acc[f][t][4 * g + 3], bf_hi(yv[t][g].y), PPO_ACT_RELU);
         bsum[4 * g] += d0;
         bsum[4 * g + 1] += d1;
         bsum[4 * g + 2] += d2;
         bsum[4 * g + 3] += d3;
-        *reinterpret_cast<uint2 *>(p) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+        yv[t][g] = make_uint2(pack2(d0, d1), pack2(d2, d3));
       }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint2 *>(img + img_off(32 * t + r, 8 * w + 4 * ft + g, PITCH) + 8 * h) = yv[t][g];
     gb[ft] += rs16(bsum, lane);
   }
 }
@@ -336,7 +347,11 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
 #pragma unroll
   for (int j = 0; j < 4; ++j) ghw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float gb1[2] = {0.f, 0.f}, gb0[2] = {0.f, 0.f};   // rs16-scattered bias grads per feature tile
-  float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;       // head (lane & 15) partials
+  // loss-head partials of this lane's (row, head) pairs: heads 2k + (tid >> 7), k < KP
+  constexpr int KP = NH > 1 ? NH / 2 : 1;
+  float g_bh[KP], g_ls[KP], g_loss = 0.f;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) g_bh[k] = g_ls[k] = 0.f;
 
 
   int chunk = blockIdx.x;
@@ -408,15 +423,16 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
     __syncthreads();
     STAMP4(4);
 
-    // ---- phase 4: head z = a2 . W_h^T (16x16x32 MFMA), the per-(row, action) loss head -> dz
-    //      images.  Wave w: rows 32w..32w+31 as two 16-row tiles; lane -> head n = lane & 15,
-    //      rows 32w + 16u + 4 (lane >> 4) + i ----
+    // ---- phase 4: head z = a2 . W_h^T on the 16x16x32 MFMA (wave w: rows 32w..32w+31 as two
+    //      16-row tiles, lane -> head lane & 15), z staged in LDS, then the loss head over DENSE
+    //      (row, head) pairs: lane -> row tid & 127 and heads 2k + (tid >> 7), k < KP (no padded
+    //      head lanes, one row's scalar work once), the row sums on the row's lane of waves 0-1 ----
     OPAQUE_LANE();
     uint4 xc[2];
     load_x(chunk, xc);  // this chunk's states again, for the X image dW0 reads (phase 5)
+    float *const zb = reinterpret_cast<float *>(dzimg);  // [128][16] f32: z -> log-prob; col 8: dlogp
     {
       const int n = lane & 15, qg = lane >> 4;
-      const float *const srl = reinterpret_cast<const float *>(simg);
       f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       {
         bf16x8 bh[H / 32], za[2][H / 32];
@@ -432,70 +448,99 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
           for (int u = 0; u < 2; ++u) zacc[u] = mfma16_v(za[u][s], bh[s], zacc[u]);
       }
       drain_fence();
-      const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float dz[4];
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int lr = 32 * w + 16 * u + 4 * qg + i;
-          const bool valid = chunk * RR + lr < count;
-          const float *sp = srl + lr * kFusedSP;
-          dz[i] = 0.f;
-          if constexpr (ACTOR) {
-            const bool act_lane = n < A;
-            float y = 0.f, d = 0.f, lp = 0.f;
-            if (act_lane) {
-              float zz = zacc[u][i];
-              if (N.bh) zz += hbias[n];
-              y = tanhf(zz);
-              const float mu = q.omv * y;
-              const float x = valid ? sp[n] : mu;
-              d = x - mu;
-              lp = ((-(d * d)) * (0.5f * h_ivar) - h_lsd) - kLogSqrt2Pi;
-            }
-            const float logp = row16_sum(lp);
-            const float old_lp = valid ? sp[A] : logp;
-            const float adv = valid ? sp[A + 1] : 0.f;
-            const float ratio = expf(logp - old_lp);
-            const float s1 = ratio * adv;
-            const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
-            const float s2 = cl * adv;
-            const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
-            const float gg = -q.inv_b;
-            const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
-            const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
-            const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
-            const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
-            const float dlogp = valid ? dratio * ratio : 0.f;
-            if (act_lane) {
-              const float dmu = dlogp * (d * h_ivar);
-              dz[i] = (dmu * q.omv) * (1.f - y * y);
-              if (valid) {
-                g_ls += dlogp * ((d * d) * h_ivar - 1.f) - q.ent_coef * q.inv_ba;
-                g_bh += dz[i];
-              }
-            }
-            if (valid && n == 0) g_loss += mn;
-          } else {
-            if (n == 0) {
-              float v = zacc[u][i];
-              if (N.bh) v += hbias[0];
-              const float vt = valid ? sp[A + 2] : v;
-              const float diff = v - vt;
-              const float ad = fabsf(diff);
-              if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
-              dz[i] = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
-              g_bh += dz[i];
-            }
+        for (int i = 0; i < 4; ++i) zb[(32 * w + 16 * u + 4 * qg + i) * 16 + n] = zacc[u][i];
+    }
+    __syncthreads();
+    OPAQUE_LANE();
+    {
+      const int row = tid & 127, hb = tid >> 7;
+      const bool valid = chunk * RR + row < count;
+      const float *const sp = reinterpret_cast<const float *>(simg) + row * kFusedSP;
+      float dzv[KP];
+      if constexpr (ACTOR) {
+        float yk[KP], dk[KP], zk[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) zk[k] = zb[row * 16 + 2 * k + hb];  // all reads before the writes
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {  // (row, head a): y, x - mu, the Normal log-prob
+          const int a = 2 * k + hb;
+          const bool on = a < A;
+          float zz = zk[k];
+          if (N.bh) zz += hbias[a];
+          const float y = tanhf(zz);
+          const float mu = q.omv * y;
+          const float x = valid ? sp[a] : mu;
+          const float d = x - mu;
+          yk[k] = y;
+          dk[k] = on ? d : 0.f;
+          zb[row * 16 + a] = on ? ((-(d * d)) * (0.5f * hbias[48 + a]) - hbias[32 + a]) - kLogSqrt2Pi : 0.f;
+        }
+        __syncthreads();
+        if (tid < RR) {  // the row's log-prob (row16_sum's tree; heads >= NH are its zero pads)
+          float l[8];
+#pragma unroll
+          for (int a = 0; a < 8; ++a) l[a] = a < NH ? zb[row * 16 + a] : 0.f;
+          const float logp = ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
+          const float old_lp = valid ? sp[A] : logp;
+          const float adv = valid ? sp[A + 1] : 0.f;
+          const float ratio = expf(logp - old_lp);
+          const float s1 = ratio * adv;
+          const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
+          const float s2 = cl * adv;
+          const float mn = (s1 != s1 || s2 != s2) ? (s1 + s2) : (s2 < s1 ? s2 : s1);
+          const float gg = -q.inv_b;
+          const float g1 = (s1 < s2) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+          const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
+          const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
+          const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
+          zb[row * 16 + 8] = valid ? dratio * ratio : 0.f;
+          if (valid) g_loss += mn;
+        }
+        __syncthreads();
+        const float dlogp = zb[row * 16 + 8];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          const int a = 2 * k + hb;
+          const bool on = a < A;
+          const float h_ivar = hbias[48 + a];
+          const float dmu = dlogp * (dk[k] * h_ivar);
+          dzv[k] = on ? (dmu * q.omv) * (1.f - yk[k] * yk[k]) : 0.f;
+          if (on && valid) {
+            g_ls[k] += dlogp * ((dk[k] * dk[k]) * h_ivar - 1.f) - q.ent_coef * q.inv_ba;
+            g_bh[k] += dzv[k];
           }
         }
-        const int lr0 = 32 * w + 16 * u + 4 * qg;
+      } else {
+        float v = zb[row * 16];
+        if (N.bh) v += hbias[0];
+        const float vt = valid ? sp[A + 2] : v;
+        const float diff = v - vt;
+        const float ad = fabsf(diff);
+        dzv[0] = tid < RR ? q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff)) : 0.f;
+        if (tid < RR) {
+          if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+          g_bh[0] += dzv[0];
+        }
+      }
+      __syncthreads();  // every z / log-prob / dlogp read done: the dz images take the region
+      // dz images: row-major [128][16] and head-major [16][128 + 8], zeros in the padded heads
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          *reinterpret_cast<uint16_t *>(dzimg + (lr0 + i) * kDzRowBytes + 2 * n) = bf16_bits4(dz[i]);
-        *reinterpret_cast<uint2 *>(dztimg + n * DZTP + 2 * lr0) =
-            make_uint2(pack2(dz[0], dz[1]), pack2(dz[2], dz[3]));
+      for (int k = 0; k < KP; ++k) {
+        const int a = 2 * k + hb;
+        if (a < NH) {
+          *reinterpret_cast<uint16_t *>(dzimg + row * kDzRowBytes + 2 * a) = bf16_bits4(dzv[k]);
+          *reinterpret_cast<uint16_t *>(dztimg + a * DZTP + 2 * row) = bf16_bits4(dzv[k]);
+        }
+      }
+      if (tid < RR) {
+#pragma unroll
+        for (int a = NH; a < 16; ++a) {
+          *reinterpret_cast<uint16_t *>(dzimg + row * kDzRowBytes + 2 * a) = 0;
+          *reinterpret_cast<uint16_t *>(dztimg + a * DZTP + 2 * row) = 0;
+        }
       }
     }
     STAMP4(5);
@@ -645,36 +690,38 @@ __device__ __forceinline__ void body4(const FusedArgs &q, const FusedNet &N, cha
       const int a = 4 * (lane >> 4) + i;
       if (a < na) slab[N.off_wh + static_cast<int64_t>(a) * H + 64 * w + 16 * j + (lane & 15)] = ghw[j][i];
     }
-  // head bias / log-std / loss partials: the 4 lane groups of a wave in a fixed xor order, then
-  // waves 0..3 in order through LDS
-  float *red = reinterpret_cast<float *>(lds + L::RED);
-  g_bh += __shfl_xor(g_bh, 16, 64);
-  g_bh += __shfl_xor(g_bh, 32, 64);
-  g_ls += __shfl_xor(g_ls, 16, 64);
-  g_ls += __shfl_xor(g_ls, 32, 64);
-  g_loss += __shfl_xor(g_loss, 16, 64);
-  g_loss += __shfl_xor(g_loss, 32, 64);
-  if (lane < 16) {
-    float *dst = red + (w * 16 + lane) * 4;
-    dst[0] = g_bh;
-    dst[1] = g_ls;
-    dst[2] = g_loss;
+  // head bias / log-std / loss partials: each wave's 64 lanes in a fixed xor-butterfly order,
+  // then per head the two waves holding it (heads of parity hb on waves 2hb, 2hb + 1) in order
+  float *red = reinterpret_cast<float *>(lds + L::RED);  // [4 waves][KP + 1][2]
+  auto wsum = [](float v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+  };
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const float sb = wsum(g_bh[k]), sl = wsum(g_ls[k]);
+    if (lane == 0) {
+      red[(w * (KP + 1) + k) * 2] = sb;
+      red[(w * (KP + 1) + k) * 2 + 1] = sl;
+    }
+  }
+  {
+    const float s = wsum(g_loss);
+    if (lane == 0) red[(w * (KP + 1) + KP) * 2] = s;
   }
   __syncthreads();
   if (tid < na) {
-    float sb = 0.f, sl = 0.f;
-#pragma unroll
-    for (int v = 0; v < NW4; ++v) {
-      sb += red[(v * 16 + tid) * 4];
-      sl += red[(v * 16 + tid) * 4 + 1];
-    }
+    const int k = NH > 1 ? tid >> 1 : 0, hb = NH > 1 ? tid & 1 : 0;
+    const float sb = red[((2 * hb) * (KP + 1) + k) * 2] + red[((2 * hb + 1) * (KP + 1) + k) * 2];
+    const float sl = red[((2 * hb) * (KP + 1) + k) * 2 + 1] + red[((2 * hb + 1) * (KP + 1) + k) * 2 + 1];
     if (N.bh) slab[N.off_bh + tid] = sb;
     if (ACTOR) slab[q.off_logstd + tid] = sl;
   }
   if (tid == 0) {
     float s = 0.f;
 #pragma unroll
-    for (int v = 0; v < NW4; ++v) s += red[(v * 16) * 4 + 2];
+    for (int v = 0; v < NW4; ++v) s += red[(v * (KP + 1) + KP) * 2];
     q.loss_part[2 * blockIdx.x + z] = s;
   }
   if constexpr (STAMP) {  // after every wave's slab stores have drained
