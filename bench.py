@@ -546,8 +546,6 @@ def main():
     # PPO_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the data-parallel path
     if os.environ.get("PPO_BENCH_ONE_DEVICE") == "1":
         local = 0
-        if world > 1:  # the in-launch fold needs its whole grid resident: not with N ranks per GPU
-            os.environ.setdefault("PPO_FUSED_FOLD", "0")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -127,22 +127,11 @@ int ppo_pack_weights(ppo_ctx *ctx, void *stream);
  * `offset`.  (No reference counterpart: the reference draws from the host generator.) */
 int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
 
-/* The fused bf16 update's in-launch slab fold (default off; PPO_FUSED_FOLD=1 or enable=1 turns
- * it on): the partial-gradient slabs are folded -- and on ppo_update_step_staged, Adam, the
- * weight images and the next minibatch's gather run -- inside the fused kernel behind a bounded,
- * self-re-arming grid barrier, instead of in a separate reduce / tail launch.  Used only when the
- * (G, 2) grid is resident (one workgroup per CU).  enable < 0 queries.  Results are bitwise those
- * of the separate launches (same reduction order).  Off by default because it measured slower:
- * the fold adds 29 us to the fused launch against an 18 us standalone tail. */
-int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable);
 /* Which fused bf16 update kernel the ctx launches for ReLU 2x256 nets (A11-A13, ppo.py:109-135):
  * 8 = fused_update_kernel (8 waves, 64-row chunks; also tanh / ELU), 4 = fused_update4_kernel
  * (one wave per SIMD, 128-row chunks).  Default PPO_FUSED4 (1 -> 4, else 8);
  * variant < 0 queries.  The two agree to f32 rounding; each is bitwise deterministic. */
 int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant);
-/* Host check (synchronises): PPO_EHIP if a fold's grid barrier timed out since the last check
- * (its step's gradients are wrong), with the message in ppo_last_error(). */
-int ppo_ctx_check_device_errors(ppo_ctx *ctx);
 /* GEMM precision of every fc-layer GEMM the ctx launches (rollout forward, update forward,
  * dgrad, wgrad): PPO_PREC_F32 (default; parity with the f32 reference) or PPO_PREC_BF16 (bf16
  * operands on v_mfma_f32_32x32x16_bf16, f32 accumulation, f32 activations / params / Adam in

@@ -563,8 +563,6 @@ class PPOEngine:
         t0 = time.perf_counter()
         memory, loss_buf = self._iterate()
         self._finish_logging(loss_buf)
-        if hasattr(self.agent.engine, "check_device_errors"):
-            self.agent.engine.check_device_errors()  # after the loss readback's synchronisation
         self.last_mean_reward = float(memory.reward.mean())
         run = self.run
         if verbose:

@@ -58,10 +58,6 @@ struct ppo_ctx {
   int64_t frec_cap, frec_rows;
   uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
   int fstamp_on, fstamp_g;
-  uint32_t *fsync;              // the in-launch fold's arrival counter (zeroed per launch)
-  int *ffold_err;               // set by a fold whose grid barrier timed out
-  int fold_on;                  // ppo_ctx_fused_fold (default: PPO_FUSED_FOLD, 0)
-  int fold_g;                   // G the residency check last passed for (0: none)
   int fused4;                   // ppo_ctx_fused_variant: 1 -> fused_update4_kernel (ReLU)
   ppo::WideWork *wide;          // wide bf16-resident layered path (wide_path.h), or null
   ppo::Timing tim;

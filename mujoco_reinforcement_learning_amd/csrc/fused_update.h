@@ -111,19 +111,6 @@ struct FusedArgs {
   int G;                       // workgroups per net
   bool v4;                     // run fused_update4_kernel (4 waves, 128-row chunks)
   uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
-  // In-launch fold of the partial-gradient slabs (fold > 0; every workgroup must be resident,
-  // fused_fold_ok): after its slab is written, each workgroup publishes it (agent-scope
-  // release), arrives on *sync (zeroed before the launch) and waits -- bounded -- for all the
-  // others; then the workgroups fold the slabs in red's fixed order, workgroup w taking the
-  // parameter blocks w, w + 2G, ... (the step_tail_kernel arithmetic, so results are bitwise
-  // those of the separate launch).  fold = 1: the flat gradient (data parallel: the all-reduce
-  // follows); fold = 2: also Adam + the bf16 weight images and the next minibatch's gather
-  // (tail).  A barrier that times out sets *fold_err and skips the fold.
-  int fold;
-  uint32_t *sync;
-  int *fold_err;
-  ReduceArgs red;
-  TailArgs tail;
 };
 // Gather the minibatch (bf16 states + row scalars) and, with q.pack_w, refresh the bf16 weight
 // images.
@@ -137,8 +124,5 @@ bool fused_update4_ok(const FusedArgs &q);
 int fused_update4_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).
 bool fused_width_ok(int hidden);
-// True when a (G, 2) grid of the fused kernel for this activation / action width is fully
-// resident on the device (one workgroup per CU), i.e. the in-launch fold can wait on it.
-bool fused_fold_ok(int act, int act_dim, int G);
 
 }  // namespace ppo

@@ -349,161 +349,6 @@ __global__ __launch_bounds__(kRedThreads) void step_tail_kernel(ReduceArgs r, Ta
   tail_block(r, t, blockIdx.x, red_scratch(scratch));
 }
 
-// The in-launch fold (FusedArgs::fold): publish this workgroup's slab, a bounded grid-wide
-// barrier, then this workgroup's share of step_tail_kernel's work.  The protocol is the
-// placement-independent release / acquire hand-off of cdna_hip_programming.md (split-K
-// reduction recipe): plain slab stores drained, one agent-scope release before the relaxed
-// agent-scope arrival, one agent-scope acquire after the wait, then plain loads.
-//
-// After the barrier each workgroup owns parameter blocks me, me + nwg, ... (kRedParams each).
-// With one 512-thread workgroup per CU, folding them one after another leaves a single block's
-// loads in flight per CU (measured: the fold then cost 3x the standalone step_tail_kernel, which
-// runs ~4 blocks per CU at once).  So kFoldJ blocks are folded together: every thread issues
-// its (group, chunk) item's loads for all kFoldJ blocks before summing any, and the Adam
-// operands of the owned parameters are loaded up front.  Each item is summed in exactly
-// slab_item_sum's order and the chunks combine in chunk order, so the result is bitwise the
-// standalone kernels'.
-constexpr uint64_t kFoldTimeoutTicks = 20000000;  // s_memrealtime at 100 MHz: 200 ms
-constexpr int kFoldGenWord = 32;                  // sync[0] arrivals, sync[32] generation
-constexpr int kFoldJ = 5;                         // blocks folded together per round
-constexpr int kFoldNK = 8;                        // splits per chunk on the fast path (G = 128)
-
-struct FoldLds {  // carve-up of the fused kernel's LDS once the compute phase is over
-  static constexpr int SEG = 0;
-  static constexpr int PART = ((kMaxSegs * static_cast<int>(sizeof(ReduceSeg)) + 15) / 16) * 16;
-  static constexpr int LRED = PART + kFoldJ * kRedChunks * kRedGroups * 16;
-  static constexpr int FLAG = LRED + 2 * kRedThreads * 4;
-  static constexpr int TOTAL = FLAG + 16;
-};
-
-__device__ __forceinline__ void fused_fold(const FusedArgs &q, char *lds) {
-  const int tid = threadIdx.x;
-  const int nwg = static_cast<int>(gridDim.x * gridDim.y);
-  const int me = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
-  int *flag = reinterpret_cast<int *>(lds + FoldLds::FLAG);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    // sense-reversing barrier: the generation is read before arriving (it cannot advance until
-    // every workgroup has arrived); the last arriver re-arms the count and bumps the generation,
-    // so no per-launch reset (and no memset node in a captured graph) is needed
-    uint32_t *count = q.sync, *gen = q.sync + kFoldGenWord;
-    const uint32_t gen0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int ok = 1;
-    if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        static_cast<uint32_t>(nwg - 1)) {
-      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // acquire every arrival's release, then publish it (and the re-armed count) with the
-      // generation: a waiter that sees the new generation sees every slab
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kFoldTimeoutTicks) {
-          ok = 0;
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    *flag = ok;
-  }
-  __syncthreads();
-  if (!*flag) {  // the grid was not resident: leave the (wrong) outputs flagged
-    if (tid == 0) *q.fold_err = 1;
-    return;
-  }
-  const ReduceArgs &r = q.red;
-  const AdamPackArgs &a = q.tail.a;
-  ReduceSeg *sseg = reinterpret_cast<ReduceSeg *>(lds + FoldLds::SEG);
-  float4 *part = reinterpret_cast<float4 *>(lds + FoldLds::PART);
-  if (tid < r.nseg) sseg[tid] = r.seg[tid];
-  // the loss scalars first: their entropy term reads logstd (parameter block 0, workgroup 0's),
-  // which this workgroup's Adam below overwrites -- the standalone kernels' order
-  if (me == 0 && r.loss_out) reduce_loss_block(r, reinterpret_cast<float *>(lds + FoldLds::LRED));
-  __syncthreads();
-  const int grp = tid % kRedGroups, chunk = tid / kRedGroups;
-  const int64_t nred = (r.total + kRedParams - 1) / kRedParams;
-  const bool adam = q.fold == 2 && tid < kFoldJ * kRedGroups;  // owner of (block tid/32, grp)
-  for (int64_t base = me; base < nred; base += static_cast<int64_t>(kFoldJ) * nwg) {
-    // Adam operands of the owned parameters, in flight with the slab loads
-    const int64_t ia = (base + static_cast<int64_t>(tid / kRedGroups) * nwg) * kRedParams + 4 * grp;
-    const bool own = adam && ia < r.total;
-    float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f), m4 = p4, v4 = p4;
-    if (own) {
-      p4 = *reinterpret_cast<const float4 *>(a.p + ia);
-      m4 = *reinterpret_cast<const float4 *>(a.m + ia);
-      v4 = *reinterpret_cast<const float4 *>(a.v + ia);
-    }
-    // every item's slab loads first (fast items: aligned, kFoldNK splits in this chunk) ...
-    float4 v[kFoldJ][kFoldNK];
-    bool fast[kFoldJ];
-#pragma unroll
-    for (int j = 0; j < kFoldJ; ++j) {
-      const int64_t i = (base + static_cast<int64_t>(j) * nwg) * kRedParams + 4 * grp;
-      const float *src = r.seg[0].src;
-      int64_t stride = 0;
-      fast[j] = false;
-      if (i < r.total) {
-        const ReduceSeg &g = sseg[seg_find(sseg, r.nseg, i)];
-        const int64_t off = i - g.dst;
-        const int k0 = (g.nsplit * chunk) / kRedChunks, k1 = (g.nsplit * (chunk + 1)) / kRedChunks;
-        fast[j] = off >= 0 && off + 3 < g.len && g.stride % 4 == 0 &&
-                  reinterpret_cast<uintptr_t>(g.src) % 16 == 0 && k1 - k0 == kFoldNK;
-        if (fast[j]) {
-          src = g.src + off + k0 * g.stride;
-          stride = g.stride;
-        }
-      }
-      // a non-fast item reads one harmless (aligned, in-bounds) address kFoldNK times
-      if (!fast[j]) src = reinterpret_cast<const float *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(15));
-#pragma unroll
-      for (int e = 0; e < kFoldNK; ++e) v[j][e] = *reinterpret_cast<const float4 *>(src + e * stride);
-    }
-    // ... then the sums, in slab_item_sum's order
-#pragma unroll
-    for (int j = 0; j < kFoldJ; ++j) {
-      const int64_t i = (base + static_cast<int64_t>(j) * nwg) * kRedParams + 4 * grp;
-      float4 acc;
-      if (fast[j]) {
-        float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-#pragma unroll
-        for (int e = 0; e < kFoldNK; e += 2) {
-          s0 = make_float4(s0.x + v[j][e].x, s0.y + v[j][e].y, s0.z + v[j][e].z, s0.w + v[j][e].w);
-          s1 = make_float4(s1.x + v[j][e + 1].x, s1.y + v[j][e + 1].y, s1.z + v[j][e + 1].z,
-                           s1.w + v[j][e + 1].w);
-        }
-        acc = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
-      } else {
-        acc = slab_item_sum(r, sseg, i, chunk);
-      }
-      part[(j * kRedChunks + chunk) * kRedGroups + grp] = acc;
-    }
-    __syncthreads();
-    if (tid < kFoldJ * kRedGroups) {
-      const int j = tid / kRedGroups;
-      const int64_t i = (base + static_cast<int64_t>(j) * nwg) * kRedParams + 4 * grp;
-      if (i < r.total) {
-        const float4 g4 = chunk_combine(part + j * kRedChunks * kRedGroups, kRedGroups, grp);
-        *reinterpret_cast<float4 *>(r.grad + i) = g4;
-        if (own) adam_apply(a, i, g4, p4, m4, v4);
-      }
-    }
-    __syncthreads();  // part is reused by the next round
-  }
-  if (q.fold == 2 && q.tail.b > 0) {
-    const int64_t gblocks = (static_cast<int64_t>(q.tail.b) * 8 + 255) / 256;
-    for (int64_t g = 2 * static_cast<int64_t>(me) + (tid >> 8); g < gblocks; g += 2 * nwg)
-      tail_gather(q.tail, g, tid & 255);
-  }
-}
-
 // ============================================================================================
 // The fused update kernel
 // ============================================================================================
@@ -1091,40 +936,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 template <int H, int ACT, int NA, bool STAMP>
 __global__ __launch_bounds__(NT, 1) void fused_update_kernel(FusedArgs q, uint64_t *stamps) {
   __shared__ __attribute__((aligned(16))) char lds[Lds<H, ACT != PPO_ACT_RELU>::TOTAL];
-  static_assert(FoldLds::TOTAL <= Lds<H, ACT != PPO_ACT_RELU>::TOTAL, "fold scratch fits the LDS");
   if (blockIdx.y == 0) fused_body<H, ACT, NA, true, STAMP>(q, q.net[0], lds, stamps);
   else fused_body<H, ACT, 1, false, STAMP>(q, q.net[1], lds, stamps);
-  if (q.fold) fused_fold(q, lds);
 }
 
 bool fused_width_ok(int hidden) { return hidden == 256; }
-
-template <int ACT, int NA>
-static bool fold_ok_na(int G) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void *>(fused_update_kernel<256, ACT, NA, false>), NT,
-          0) != hipSuccess)
-    return false;
-  return per_cu >= 1 && static_cast<int64_t>(per_cu) * cus >= 2 * G;
-}
-
-template <int ACT>
-static bool fold_ok_act(int act_dim, int G) {
-  if (act_dim <= 2) return fold_ok_na<ACT, 2>(G);
-  if (act_dim <= 4) return fold_ok_na<ACT, 4>(G);
-  if (act_dim <= 6) return fold_ok_na<ACT, 6>(G);
-  return fold_ok_na<ACT, 8>(G);
-}
-
-bool fused_fold_ok(int act, int act_dim, int G) {
-  if (act == PPO_ACT_RELU) return fold_ok_act<PPO_ACT_RELU>(act_dim, G);
-  if (act == PPO_ACT_TANH) return fold_ok_act<PPO_ACT_TANH>(act_dim, G);
-  return fold_ok_act<PPO_ACT_ELU>(act_dim, G);
-}
 
 int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   const int row_blocks = q.rec ? static_cast<int>(ceil_div(static_cast<int64_t>(q.b) * 8, 256))
@@ -1223,8 +1039,6 @@ int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   PPO_REQUIRE(q.G >= 1 && q.G <= kFusedMaxWG, "fused update: bad workgroup count %d", q.G);
   PPO_REQUIRE(q.act_dim >= 1 && q.act_dim <= kFusedMaxAct, "fused update: act_dim %d", q.act_dim);
   PPO_REQUIRE(!q.stamps || q.act == PPO_ACT_RELU, "fused update: phase stamps only for ReLU");
-  PPO_REQUIRE(!q.fold || (q.sync && q.fold_err && q.red.nseg > 0),
-              "fused update: the in-launch fold needs its counter, error word and reduction");
   if (q.act == PPO_ACT_RELU) launch_act<PPO_ACT_RELU>(q, rec, st);
   else if (q.act == PPO_ACT_TANH) launch_act<PPO_ACT_TANH>(q, rec, st);
   else launch_act<PPO_ACT_ELU>(q, rec, st);

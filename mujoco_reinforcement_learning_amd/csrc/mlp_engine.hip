@@ -757,10 +757,8 @@ static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *ac
   q.slab_stride = ctx->total_params;
   q.loss_part = ctx->floss;
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
-  // the 4-wave kernel when enabled (not with the phase-stamp diagnostics or the in-launch fold,
-  // which only the 8-wave kernel implements)
-  q.v4 = ctx->fused4 && !ctx->fold_on && fused_update4_ok(q) &&
-         (!q.stamps || (q.act_dim > 4 && q.act_dim <= 6));
+  // the 4-wave kernel when selected (its phase-stamp build covers act_dim 5-6 only)
+  q.v4 = ctx->fused4 && fused_update4_ok(q) && (!q.stamps || (q.act_dim > 4 && q.act_dim <= 6));
   q.G = std::min(kFusedMaxWG, ceil_div(b, q.v4 ? kFused4Rows : kFusedRows));
   return q;
 }
@@ -840,26 +838,6 @@ static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, floa
   return r;
 }
 
-// The in-launch fold (FusedArgs::fold) is used when enabled and the (G, 2) grid is resident
-// (one workgroup per CU); the residency check runs once per G.
-static bool fold_usable(ppo_ctx *ctx, int G) {
-  if (!ctx->fold_on || !ctx->fsync) return false;
-  if (ctx->fold_g == G) return true;
-  if (!fused_fold_ok(ctx->cfg.activation, ctx->cfg.act_dim, G)) return false;
-  ctx->fold_g = G;
-  return true;
-}
-
-static int fold_prepare(ppo_ctx *ctx, FusedArgs &q, int mode, const ReduceArgs &r,
-                        hipStream_t st) {
-  q.fold = mode;
-  q.sync = ctx->fsync;
-  q.fold_err = ctx->ffold_err;
-  q.red = r;
-  (void)st;  // the barrier re-arms itself (fused_fold): nothing to reset per launch
-  return 0;
-}
-
 static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
                                 const float *old_logp_d, const float *adv_d,
                                 const float *vtarget_d, const int32_t *rows_d, int b,
@@ -876,11 +854,6 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
     if (int rc = fused_prep(ctx, p, st)) return rc;
   }
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
-  if (fold_usable(ctx, q.G)) {  // the slab fold inside the fused launch: no reduce launch
-    FusedArgs f = q;
-    if (int rc = fold_prepare(ctx, f, 1, r, st)) return rc;
-    return fused_forward_backward(ctx, f, st);
-  }
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const int64_t P = ctx->total_params;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(q.G) * P,
@@ -1079,17 +1052,6 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       c += static_cast<int64_t>(kFusedMaxWG) * off * 4;
       ctx->floss = reinterpret_cast<float *>(c);
       c += kFusedMaxWG * 2 * 4;
-      ctx->fsync = reinterpret_cast<uint32_t *>(c);  // [0] arrivals, [32] generation
-      ctx->ffold_err = reinterpret_cast<int *>(c + 64);
-      e = hipMemset(c, 0, 256);
-      if (e != hipSuccess) {
-        (void)hipFree(arena);
-        (void)hipFree(fa);
-        delete ctx;
-        set_error("ppo_ctx_create: hipMemset failed: %s", hipGetErrorString(e));
-        return PPO_EHIP;
-      }
-      ctx->fold_on = env_knob("PPO_FUSED_FOLD", 0);
       ctx->fused4 = g_fused4 != 0;
     }
   }
@@ -1449,11 +1411,6 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.srow = ctx->fsrow;
   t.b = next_b;
   t.reduce = true;
-  if (fold_usable(ctx, q.G)) {  // the whole optimizer step in ONE launch
-    if (int rc = fold_prepare(ctx, q, 2, r, st)) return rc;
-    q.tail = t;
-    return fused_forward_backward(ctx, q, st);
-  }
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
@@ -1836,34 +1793,11 @@ extern "C" int ppo_ctx_set_precision(ppo_ctx *ctx, int prec) {
   return 0;
 }
 
-extern "C" int ppo_ctx_fused_fold(ppo_ctx *ctx, int enable) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_fold: null ctx");
-  if (enable < 0) return ctx->fold_on && ctx->fsync ? 1 : 0;
-  ctx->fold_on = enable != 0;
-  return 0;
-}
-
 extern "C" int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant) {
   PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_variant: null ctx");
   if (variant < 0) return ctx->fused4 ? 4 : 8;
   PPO_REQUIRE(variant == 4 || variant == 8, "ppo_ctx_fused_variant: variant %d (4 or 8)", variant);
   ctx->fused4 = variant == 4;
-  return 0;
-}
-
-extern "C" int ppo_ctx_check_device_errors(ppo_ctx *ctx) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_check_device_errors: null ctx");
-  if (!ctx->ffold_err) return 0;
-  int err = 0;
-  PPO_HIP_TRY(hipMemcpy(&err, ctx->ffold_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (err) {
-    // a timed-out barrier leaves the arrival count mid-generation: re-arm it with the flag
-    PPO_HIP_TRY(hipMemset(ctx->fsync, 0, 256));
-    set_error("fused update: the in-launch slab fold's grid barrier timed out (workgroups not "
-              "co-resident); the gradients of that step are wrong -- disable it with "
-              "ppo_ctx_fused_fold(ctx, 0) / PPO_FUSED_FOLD=0 (the default)");
-    return PPO_EHIP;
-  }
   return 0;
 }
 

@@ -46,8 +46,7 @@ constexpr int kRedChunks = 16;
 constexpr int kRedThreads = kRedGroups * kRedChunks;
 constexpr int kRedParams = 4 * kRedGroups;  // parameters per block
 // LDS scratch of one block reduction: part [kRedChunks][kRedGroups], lred [2][kRedThreads],
-// sseg [kMaxSegs] (the standalone kernels declare it; the fused kernel's in-launch fold lends
-// its own LDS, free once the compute phase is over).
+// sseg [kMaxSegs] (the kernels declare it as one __shared__ array).
 struct RedScratch {
   float4 *part;
   float *lred;

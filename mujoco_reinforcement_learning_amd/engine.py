@@ -208,24 +208,12 @@ class Engine:
         check(self.lib.ppo_ctx_set_rng_counter(self._ctx, ptr(counter)))
         self._rng_counter = counter  # keep the buffer alive while the ctx may read it
 
-    def fused_fold(self, enable: Optional[bool] = None) -> bool:
-        """The fused update's in-launch slab fold (ppo_ctx_fused_fold): set it with enable,
-        return whether it is on."""
-        if enable is not None:
-            check(self.lib.ppo_ctx_fused_fold(self._ctx, int(bool(enable))))
-        return bool(self.lib.ppo_ctx_fused_fold(self._ctx, -1))
-
     def fused_variant(self, variant: Optional[int] = None) -> int:
         """The fused bf16 update kernel (ppo_ctx_fused_variant): 8 = 8 waves / 64-row chunks,
         4 = one wave per SIMD / 128-row chunks (ReLU); set it with variant, return the current."""
         if variant is not None:
             check(self.lib.ppo_ctx_fused_variant(self._ctx, int(variant)))
         return int(self.lib.ppo_ctx_fused_variant(self._ctx, -1))
-
-    def check_device_errors(self) -> None:
-        """Raise EngineError if a device-side failure was flagged since the last check (the
-        fold's grid barrier timing out).  Synchronises the host."""
-        check(self.lib.ppo_ctx_check_device_errors(self._ctx))
 
     # ---- measurement ---------------------------------------------------------------------
     def timing(self, enable: bool, capacity: int = 65536) -> None:

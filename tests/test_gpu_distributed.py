@@ -119,8 +119,7 @@ def _local_worker(rank, world, port, q, shape="fused"):
     torch.cuda.synchronize()
     kernels = sorted(agent.engine.timing_kernels())
     agent.engine.timing(False)
-    q.put((rank, agent.packed_params().cpu(), (kernels, agent.engine.fused_fold()),
-           algo.last_losses))
+    q.put((rank, agent.packed_params().cpu(), kernels, algo.last_losses))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -146,18 +145,18 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu, shape):
     # replicas bit-identical (same all-reduced gradient, same Adam), and they moved
     assert torch.equal(got[0][0], got[1][0])
     assert all(abs(x) < 1e6 for x in got[0][2])
-    kernels, fold = got[0][1]
+    kernels = got[0][1]
     if shape == "wide":  # layered bf16-resident GEMMs, the fixed-order slab fold, Adam
         assert any(k.startswith("wide_gemm_kernel") for k in kernels), kernels
         assert "wide_reduce_kernel" in kernels and "wide_policy_fused_kernel" in kernels, kernels
         assert not any(k.startswith("fused_update_kernel") for k in kernels), kernels
         return
-    # the data-parallel optimizer step: the fused kernel (slabs folded to the flat gradient in
-    # the same launch, or by reduce_slabs_kernel without the in-launch fold), the all-reduce,
+    # the data-parallel optimizer step: the fused kernel, reduce_slabs_kernel folding its slabs
+    # into the flat gradient, the all-reduce,
     # then ONE tail launch: Adam + weight images + the next minibatch's gather
     assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
     assert "step_tail_kernel" in kernels, kernels
-    assert ("reduce_slabs_kernel" in kernels) == (not fold), (fold, kernels)
+    assert "reduce_slabs_kernel" in kernels, kernels
 
 
 def _ckpt_worker(rank, world, port, q, exp):

@@ -12,14 +12,13 @@
 #   phases    fused-update phase stamps (tools/fused_phases.py)
 #   wbench    tools/wide_bench.py: the wide-path bf16 GEMMs at Humanoid shapes vs torch's matmul
 #   micro     tools/micro_fused.py timing of the fused update kernel alone
-#   fold      the bench line with PPO_FUSED_FOLD=1 (in-launch slab fold) -> bench_${TAG}_fold.json
 #   cnn       bench.py --model cnn (pixel cheetah-run) -> bench_${TAG}_cnn.json
 #   cnntrace  rocprofv3 --kernel-trace --stats over the CNN bench
 #   dp2       2-rank data-parallel rehearsal on the one GPU (gloo) -> bench_${TAG}_dp2.json
 #   hum       Humanoid configs[3] shard (1024 envs, O=376, A=17, 3x512) -> bench_${TAG}_hum.json
 #   configs   bench lines of Ant, Humanoid 8192 on one GPU, the pixel CNN and the BiLSTM
 #   humtrace  rocprofv3 --kernel-trace --stats over the Humanoid shard bench (graph replay, no events)
-#   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1; fold off and on)
+#   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
@@ -92,10 +91,6 @@ for S in $STEPS; do
         -- python3 bench.py --model lstm --steps 1 --warmup 1 $LSTM_ARGS > gpurun_out/rp_${TAG}_lstm.json \
         2> gpurun_out/rp_${TAG}_lstm.log || fail lstmtrace gpurun_out/rp_${TAG}_lstm.log
       head -12 $(find gpurun_out/rp_${TAG}_lstm -name "*kernel_stats.csv") ;;
-    fold)
-      PPO_FUSED_FOLD=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs > gpurun_out/bench_${TAG}_fold.json \
-        2> gpurun_out/bench_${TAG}_fold.err || fail fold gpurun_out/bench_${TAG}_fold.err
-      cat gpurun_out/bench_${TAG}_fold.json ;;
     cnn)
       timeout -k 10 600 python bench.py --model cnn $CNN_ARGS > gpurun_out/bench_${TAG}_cnn.json \
         2> gpurun_out/bench_${TAG}_cnn.err || fail cnn gpurun_out/bench_${TAG}_cnn.err
@@ -114,10 +109,7 @@ for S in $STEPS; do
     dp1)
       PPO_DP_REHEARSE=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs > gpurun_out/bench_${TAG}_dp1.json \
         2> gpurun_out/bench_${TAG}_dp1.err || fail dp1 gpurun_out/bench_${TAG}_dp1.err
-      PPO_DP_REHEARSE=1 PPO_FUSED_FOLD=1 timeout -k 10 400 python bench.py --no-cpu-baseline --no-legs \
-        > gpurun_out/bench_${TAG}_dp1fold.json 2> gpurun_out/bench_${TAG}_dp1fold.err \
-        || fail dp1fold gpurun_out/bench_${TAG}_dp1fold.err
-      cat gpurun_out/bench_${TAG}_dp1.json gpurun_out/bench_${TAG}_dp1fold.json ;;
+      cat gpurun_out/bench_${TAG}_dp1.json ;;
     hum)
       timeout -k 10 500 python bench.py --num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 \
         --steps 3 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
