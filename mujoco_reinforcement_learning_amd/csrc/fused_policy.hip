@@ -120,6 +120,14 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   // hs[0..7] head bias, hs[8..15] the actor's log-std (wave 0)
   const float hraw = gptr(wu == 0 && (lane & 8) ? (q.logstd ? q.logstd : fb)
                                                 : (N.bh ? N.bh : fb))[tid & 7];
+  // the L0 weight fragments and the first W1 ring fragments: in flight under the observation
+  // loads and the f64 statistics instead of at the start of their passes
+  bf16x8 w0f[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    w0f[s] = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
+  bf16x8 ring[PD + 1];
+  wring_prime<H>(w_frag_base<H>(N.w1b, w, lane), ring);
   float epsv = 0.f;
   if (ACTOR && !q.eps && ea < A && erow < nrow)
     epsv = philox_normal_at(q.seed, q.offset + (q.offset_base ? obraw : 0) + eidx);
@@ -199,8 +207,6 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   PSTAMP(4);
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----
-  bf16x8 ring[PD + 1];
-  wring_prime<H>(w_frag_base<H>(N.w1b, w, lane), ring);
   {
     f32x16 acc[NTP];
 #pragma unroll
@@ -209,10 +215,9 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8 *>(N.w0b + (32 * w + r) * kFusedKX + 16 * s + 8 * h);
 #pragma unroll
       for (int t = 0; t < NTP; ++t)
-        acc[t] = mfma(af, lds_b128(ximg + x_off(32 * t + r, 2 * s + h)), acc[t]);
+        acc[t] = mfma(w0f[s], lds_b128(ximg + x_off(32 * t + r, 2 * s + h)), acc[t]);
     }
     mfma_drain(acc);
 #pragma unroll
