@@ -25,6 +25,7 @@
 
 #include "common.h"
 #include "conv.h"
+#include "conv_pixel.h"
 #include "gemm.h"
 #include "gemm_ops.h"
 #include "reduce_slabs.h"
@@ -394,6 +395,50 @@ int run_conv(const ConvArgs &a, int nets, hipStream_t st) {
   }
 }
 
+// The bf16 pixel layer through the space-to-depth kernels (conv_pixel.h); PPO_PIXEL_S2D=0 keeps
+// it on the implicit-GEMM conv_kernel (the A/B baseline).
+static const int g_pix_s2d = [] {
+  const char *v = getenv("PPO_PIXEL_S2D");
+  return v ? atoi(v) : 1;
+}();
+
+PixArgs pix_args(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows, int b) {
+  PixArgs p{};
+  p.frames = frames;
+  p.rows = rows;
+  p.nimg = b;
+  for (int z = 0; z < 2; ++z) {
+    p.w[z] = x->params + x->conv[z][0].w;
+    p.bias[z] = x->params + x->conv[z][0].b;
+  }
+  return p;
+}
+
+int pixel_forward(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows, int b, hipStream_t st) {
+  if (b == 0) return 0;
+  PixArgs p = pix_args(x, frames, rows, b);
+  for (int z = 0; z < 2; ++z) p.out[z] = static_cast<__bf16 *>(x->a1[z]);
+  launch_k(conv_rec<L1, MODE_FWD>("pixel_fwd_kernel", b, 2), pixel_fwd_kernel,
+           dim3(std::min(b, 512)), dim3(kPixFwdThreads), 0, st, p);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+int pixel_wgrad(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows, int b, int splits,
+                hipStream_t st) {
+  PixArgs p = pix_args(x, frames, rows, b);
+  for (int z = 0; z < 2; ++z) {
+    p.dz[z] = x->dz1[z];
+    p.slab[z] = x->cslab[z][0];
+  }
+  p.slab_stride = x->cslab_stride[0];
+  p.splits = splits;
+  launch_k(conv_rec<L1, MODE_WGRAD>("pixel_wgrad_kernel", b, 2), pixel_wgrad_kernel,
+           dim3(splits), dim3(kPixWgThreads), 0, st, p);
+  PPO_LAUNCHED();
+  return 0;
+}
+
 int pack_conv(ppo_cnn_ctx *x, hipStream_t st) {
   PackArgs p{};
   const int co[3] = {L1::cout, L2::cout, L3::cout}, ci[3] = {L1::cin, L2::cin, L3::cin},
@@ -427,7 +472,11 @@ int encoder_forward_t(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows
     a.net[z].out = x->a1[z];
   }
   a.rows = rows;
-  if (int rc = run_conv<L1, MODE_FWD, uint8_t, TACT, BF, false, false>(a, 2, st)) return rc;
+  if (BF && g_pix_s2d) {
+    if (int rc = pixel_forward(x, frames, rows, b, st)) return rc;
+  } else if (int rc = run_conv<L1, MODE_FWD, uint8_t, TACT, BF, false, false>(a, 2, st)) {
+    return rc;
+  }
   a.rows = nullptr;
   for (int z = 0; z < 2; ++z) {
     a.net[z].in = x->a1[z];
@@ -492,7 +541,11 @@ int encoder_backward_t(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *row
   a.rows = rows;
   a.splits = splits_for(static_cast<int64_t>(b) * L1::P);
   a.slab_stride = x->cslab_stride[0];
-  if (int rc = run_conv<L1, MODE_WGRAD, uint8_t, TACT, BF, false, false>(a, 2, st)) return rc;
+  if (BF && g_pix_s2d) {
+    if (int rc = pixel_wgrad(x, frames, rows, b, a.splits, st)) return rc;
+  } else if (int rc = run_conv<L1, MODE_WGRAD, uint8_t, TACT, BF, false, false>(a, 2, st)) {
+    return rc;
+  }
   // remember the split counts for the reduction
   x->cslab_splits_last[0] = a.splits;
   x->cslab_splits_last[1] = s2;
