@@ -136,9 +136,11 @@ def roofline(name, c, traffic, force_hbm=False):
     (bytes / 8 TB/s); achieved = that work per launch / mean launch duration."""
     launches = max(c["launches"], 1)
     avg_s = c["ms"] * 1e-3 / launches
-    # the fused update kernel and the wide path's GEMMs are bf16-only; the layered GEMMs carry
-    # their dtype in the name
-    bf16 = "bf16" in name or "wide_gemm" in name or c["class"] == "fused_update"
+    # the fused update kernel, the wide path's GEMMs and the pixel encoder's LDS-staged
+    # convolutions (conv_pixel.h, conv_lds.h) are bf16-only; the layered GEMMs and conv_kernel
+    # carry their dtype in the name
+    bf16 = ("bf16" in name or "wide_gemm" in name or c["class"] == "fused_update"
+            or "_lds_kernel" in name or name.startswith("pixel_"))
     peak_f = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     t_mfma = c["flops"] / (peak_f * 1e12)
     t_hbm = c["bytes"] / (PEAK_HBM_GBS * 1e9)

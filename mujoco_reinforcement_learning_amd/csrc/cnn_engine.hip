@@ -26,6 +26,7 @@
 #include "common.h"
 #include "conv.h"
 #include "conv_pixel.h"
+#include "conv_lds.h"
 #include "gemm.h"
 #include "gemm_ops.h"
 #include "reduce_slabs.h"
@@ -269,6 +270,8 @@ struct ppo_cnn_ctx {
   int64_t rows;
   // workspace views (per net z)
   float *wpack[2][3];                 // packed conv weights [co][(ky kx) ci]
+  __bf16 *wdg[2][2];                  // bf16 W'^T of L2 / L3 for dgrad_lds_kernel (conv_lds.h)
+  __bf16 *wfw[2][2];                  // bf16 W' of L2 / L3 for fwd_lds_kernel
   void *a1[2], *a2[2];                // encoder activations (bf16 or f32, HWC)
   float *feat[2];                     // [rows][3136] CHW
   float *act[2][PPO_MAX_LAYERS + 1];  // MLP layer outputs [rows][out]
@@ -347,6 +350,25 @@ TimRec conv_rec(const char *name, int nimg, int nets) {
   return TimRec{KC_CONV, tim_active() ? name : nullptr, fl, by};
 }
 
+// The LDS-staged bf16 kernels (conv_pixel.h, conv_lds.h): their algorithmic bytes per image, both
+// nets -- every tensor once at its stored width (u8 frames read once for both nets, bf16
+// activations, f32 gradients); the frame / input of a product read once.
+template <class G, int MODE>
+TimRec lds_rec(const char *name, int nimg) {
+  TimRec r = conv_rec<G, MODE>(name, nimg, 2);
+  const double in = static_cast<double>(G::PIN) * G::cin, out = static_cast<double>(G::P) * G::cout;
+  const bool pixel = G::cin == 3;
+  double per;
+  if (MODE == MODE_FWD)
+    per = pixel ? in + 2 * 2 * out : 2 * (2 * in + (G::P == L3::P ? 4 : 2) * out);
+  else if (MODE == MODE_WGRAD)
+    per = pixel ? in + 2 * 4 * out : 2 * (2 * in + 4 * out);
+  else
+    per = 2 * (4 * out + 2 * in + 4 * in);  // dz, relu' operand, the input gradient
+  r.bytes = static_cast<double>(nimg) * per;
+  return r;
+}
+
 template <class G, int MODE, typename TIN, typename TOUT, bool BF, bool DZCHW, bool OUTCHW, int WM,
           int WN, int TM, int TN>
 int launch_conv(const ConvArgs &a, int nets, hipStream_t st) {
@@ -418,7 +440,7 @@ int pixel_forward(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows, in
   if (b == 0) return 0;
   PixArgs p = pix_args(x, frames, rows, b);
   for (int z = 0; z < 2; ++z) p.out[z] = static_cast<__bf16 *>(x->a1[z]);
-  launch_k(conv_rec<L1, MODE_FWD>("pixel_fwd_kernel", b, 2), pixel_fwd_kernel,
+  launch_k(lds_rec<L1, MODE_FWD>("pixel_fwd_kernel", b), pixel_fwd_kernel,
            dim3(std::min(b, 512)), dim3(kPixFwdThreads), 0, st, p);
   PPO_LAUNCHED();
   return 0;
@@ -433,13 +455,105 @@ int pixel_wgrad(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows, int 
   }
   p.slab_stride = x->cslab_stride[0];
   p.splits = splits;
-  launch_k(conv_rec<L1, MODE_WGRAD>("pixel_wgrad_kernel", b, 2), pixel_wgrad_kernel,
+  launch_k(lds_rec<L1, MODE_WGRAD>("pixel_wgrad_kernel", b), pixel_wgrad_kernel,
            dim3(splits), dim3(kPixWgThreads), 0, st, p);
   PPO_LAUNCHED();
   return 0;
 }
 
+// The bf16 input gradients of L2 / L3 through dgrad_lds_kernel (conv_lds.h); PPO_CONV_LDS=0
+// keeps them on the implicit-GEMM conv_kernel.
+static const int g_conv_lds = [] {
+  const char *v = getenv("PPO_CONV_LDS");
+  return v ? atoi(v) : 1;
+}();
+
+template <class D>
+int dgrad_lds(ppo_cnn_ctx *x, int l, const float *const dz[2], const void *const xin[2],
+              float *const dout[2], int b, hipStream_t st) {
+  // W'^T of both nets: packed by lds_pack (the weights of this minibatch's forward)
+  if (b == 0) return 0;
+  DgArgs q{};
+  for (int z = 0; z < 2; ++z) {
+    q.wt[z] = x->wdg[z][l - 1];
+    q.dz[z] = dz[z];
+    q.xin[z] = static_cast<const __bf16 *>(xin[z]);
+    q.dout[z] = dout[z];
+  }
+  q.nimg = b;
+  using G = std::conditional_t<D::S == 2, L2, L3>;
+  launch_k(lds_rec<G, MODE_DGRAD>(D::S == 2 ? "dgrad_lds_kernel<L2>" : "dgrad_lds_kernel<L3>", b),
+           dgrad_lds_kernel<D>, dim3(std::min(b, 256)), dim3(512), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+template <class D>
+int pack_fw(ppo_cnn_ctx *x, int l, hipStream_t st) {
+  launch_k(TimRec{KC_CONV, "fw_pack_kernel", 0.0, 0.0}, fw_pack_kernel<D>,
+           dim3(ceil_div(2LL * D::CO * D::KD, 256)), dim3(256), 0, st,
+           x->params + x->conv[0][l].w, x->params + x->conv[1][l].w, x->wfw[0][l - 1],
+           x->wfw[1][l - 1]);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+template <class D>
+int pack_dg(ppo_cnn_ctx *x, int l, hipStream_t st) {
+  launch_k(TimRec{KC_CONV, "dg_pack_kernel", 0.0, 0.0}, dg_pack_kernel<D>,
+           dim3(ceil_div(2LL * D::N * D::KD, 256)), dim3(256), 0, st,
+           x->params + x->conv[0][l].w, x->params + x->conv[1][l].w, x->wdg[0][l - 1],
+           x->wdg[1][l - 1]);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+template <class D>
+int fwd_lds(ppo_cnn_ctx *x, int l, const void *const xin[2], void *const out[2], int b,
+            hipStream_t st) {
+  if (b == 0) return 0;
+  FwArgs q{};
+  for (int z = 0; z < 2; ++z) {
+    q.wp[z] = x->wfw[z][l - 1];
+    q.bias[z] = x->params + x->conv[z][l].b;
+    q.xin[z] = static_cast<const __bf16 *>(xin[z]);
+    q.out[z] = out[z];
+  }
+  q.nimg = b;
+  using G = std::conditional_t<D::S == 2, L2, L3>;
+  launch_k(lds_rec<G, MODE_FWD>(D::S == 2 ? "fwd_lds_kernel<L2>" : "fwd_lds_kernel<L3>", b),
+           fwd_lds_kernel<D>, dim3(std::min(b, 256)), dim3(512), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+template <class D>
+int wgrad_lds(ppo_cnn_ctx *x, int l, const void *const xin[2], const float *const dz[2], int b,
+              int splits, hipStream_t st) {
+  FwArgs q{};
+  for (int z = 0; z < 2; ++z) {
+    q.xin[z] = static_cast<const __bf16 *>(xin[z]);
+    q.dz[z] = dz[z];
+    q.slab[z] = x->cslab[z][l];
+  }
+  q.slab_stride = x->cslab_stride[l];
+  q.splits = splits;
+  q.nimg = b;
+  using G = std::conditional_t<D::S == 2, L2, L3>;
+  launch_k(lds_rec<G, MODE_WGRAD>(D::S == 2 ? "wgrad_lds_kernel<L2>" : "wgrad_lds_kernel<L3>", b),
+           wgrad_lds_kernel<D>, dim3(splits), dim3(512), 0, st, q);
+  PPO_LAUNCHED();
+  return 0;
+}
+
 int pack_conv(ppo_cnn_ctx *x, hipStream_t st) {
+  if (x->prec == PPO_PREC_BF16 && g_conv_lds) {
+    if (int rc = pack_fw<L2F>(x, 1, st)) return rc;
+    if (int rc = pack_fw<L3F>(x, 2, st)) return rc;
+    if (int rc = pack_dg<L2D>(x, 1, st)) return rc;
+    if (int rc = pack_dg<L3D>(x, 2, st)) return rc;
+    if (g_pix_s2d) return 0;  // no conv_kernel reads the f32 pack
+  }
   PackArgs p{};
   const int co[3] = {L1::cout, L2::cout, L3::cout}, ci[3] = {L1::cin, L2::cin, L3::cin},
             ks[3] = {L1::k, L2::k, L3::k};
@@ -484,12 +598,23 @@ int encoder_forward_t(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *rows
     a.net[z].bias = x->params + x->conv[z][1].b;
     a.net[z].out = x->a2[z];
   }
-  if (int rc = run_conv<L2, MODE_FWD, TACT, TACT, BF, false, false>(a, 2, st)) return rc;
+  if (BF && g_conv_lds) {
+    const void *xin[2] = {x->a1[0], x->a1[1]};
+    void *const out[2] = {x->a2[0], x->a2[1]};
+    if (int rc = fwd_lds<L2F>(x, 1, xin, out, b, st)) return rc;
+  } else if (int rc = run_conv<L2, MODE_FWD, TACT, TACT, BF, false, false>(a, 2, st)) {
+    return rc;
+  }
   for (int z = 0; z < 2; ++z) {
     a.net[z].in = x->a2[z];
     a.net[z].w = x->wpack[z][2];
     a.net[z].bias = x->params + x->conv[z][2].b;
     a.net[z].out = x->feat[z];
+  }
+  if (BF && g_conv_lds) {
+    const void *xin[2] = {x->a2[0], x->a2[1]};
+    void *const out[2] = {x->feat[0], x->feat[1]};
+    return fwd_lds<L3F>(x, 2, xin, out, b, st);
   }
   return run_conv<L3, MODE_FWD, TACT, float, BF, false, true>(a, 2, st);
 }
@@ -514,8 +639,22 @@ int encoder_backward_t(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *row
   }
   a.splits = splits_for(static_cast<int64_t>(b) * L3::P);
   a.slab_stride = x->cslab_stride[2];
-  if (int rc = run_conv<L3, MODE_WGRAD, TACT, TACT, BF, true, false>(a, 2, st)) return rc;
-  if (int rc = run_conv<L3, MODE_DGRAD, TACT, TACT, BF, true, false>(a, 2, st)) return rc;
+  if (BF && g_conv_lds) {
+    a.splits = std::max(1, std::min(kConvMaxSplits, b));
+    const void *xin[2] = {x->a2[0], x->a2[1]};
+    const float *dz[2] = {x->dfeat[0], x->dfeat[1]};
+    if (int rc = wgrad_lds<L3F>(x, 2, xin, dz, b, a.splits, st)) return rc;
+  } else if (int rc = run_conv<L3, MODE_WGRAD, TACT, TACT, BF, true, false>(a, 2, st)) {
+    return rc;
+  }
+  if (BF && g_conv_lds) {
+    const float *dz[2] = {x->dfeat[0], x->dfeat[1]};
+    const void *xin[2] = {x->a2[0], x->a2[1]};
+    float *const dout[2] = {x->dz2[0], x->dz2[1]};
+    if (int rc = dgrad_lds<L3D>(x, 2, dz, xin, dout, b, st)) return rc;
+  } else if (int rc = run_conv<L3, MODE_DGRAD, TACT, TACT, BF, true, false>(a, 2, st)) {
+    return rc;
+  }
   const int s3 = a.splits;
   // L2: dz = dz2 (HWC)
   for (int z = 0; z < 2; ++z) {
@@ -527,8 +666,22 @@ int encoder_backward_t(ppo_cnn_ctx *x, const uint8_t *frames, const int32_t *row
   }
   a.splits = splits_for(static_cast<int64_t>(b) * L2::P);
   a.slab_stride = x->cslab_stride[1];
-  if (int rc = run_conv<L2, MODE_WGRAD, TACT, TACT, BF, false, false>(a, 2, st)) return rc;
-  if (int rc = run_conv<L2, MODE_DGRAD, TACT, TACT, BF, false, false>(a, 2, st)) return rc;
+  if (BF && g_conv_lds) {
+    a.splits = std::max(1, std::min(kConvMaxSplits, b));
+    const void *xin[2] = {x->a1[0], x->a1[1]};
+    const float *dz[2] = {x->dz2[0], x->dz2[1]};
+    if (int rc = wgrad_lds<L2F>(x, 1, xin, dz, b, a.splits, st)) return rc;
+  } else if (int rc = run_conv<L2, MODE_WGRAD, TACT, TACT, BF, false, false>(a, 2, st)) {
+    return rc;
+  }
+  if (BF && g_conv_lds) {
+    const float *dz[2] = {x->dz2[0], x->dz2[1]};
+    const void *xin[2] = {x->a1[0], x->a1[1]};
+    float *const dout[2] = {x->dz1[0], x->dz1[1]};
+    if (int rc = dgrad_lds<L2D>(x, 1, dz, xin, dout, b, st)) return rc;
+  } else if (int rc = run_conv<L2, MODE_DGRAD, TACT, TACT, BF, false, false>(a, 2, st)) {
+    return rc;
+  }
   const int s2 = a.splits;
   // L1: pixels through the minibatch rows, dz = dz1
   for (int z = 0; z < 2; ++z) {
@@ -723,13 +876,17 @@ extern "C" int ppo_cnn_ctx_create(const ppo_cnn_cfg *cfg, int device, ppo_cnn_ct
     need = align_up(need + n, kWsAlign);
     return at;
   };
-  int64_t o_pack[2][3], o_a1[2], o_a2[2], o_feat[2], o_act[2][PPO_MAX_LAYERS + 1], o_dz[2][2],
+  int64_t o_wdg[2][2], o_wfw[2][2], o_pack[2][3], o_a1[2], o_a2[2], o_feat[2], o_act[2][PPO_MAX_LAYERS + 1], o_dz[2][2],
       o_dfeat[2], o_dz2[2], o_dz1[2], o_cslab[2][3];
   const int64_t ksz[3] = {static_cast<int64_t>(L1::cout) * L1::kdim,
                           static_cast<int64_t>(L2::cout) * L2::kdim,
                           static_cast<int64_t>(L3::cout) * L3::kdim};
   for (int z = 0; z < 2; ++z) {
     for (int l = 0; l < 3; ++l) o_pack[z][l] = take(ksz[l]);
+    o_wdg[z][0] = take(L2D::N * L2D::KD / 2);  // bf16
+    o_wdg[z][1] = take(L3D::N * L3D::KD / 2);
+    o_wfw[z][0] = take(L2F::CO * L2F::KD / 2);
+    o_wfw[z][1] = take(L3F::CO * L3F::KD / 2);
     o_a1[z] = take(R * L1::P * L1::cout);  // f32-sized (bf16 uses half)
     o_a2[z] = take(R * L2::P * L2::cout);
     o_feat[z] = take(R * kFeatures);
@@ -758,6 +915,8 @@ extern "C" int ppo_cnn_ctx_create(const ppo_cnn_cfg *cfg, int device, ppo_cnn_ct
   for (int z = 0; z < 2; ++z) {
     for (int l = 0; l < 3; ++l) {
       x->wpack[z][l] = w + o_pack[z][l];
+      if (l < 2) x->wdg[z][l] = reinterpret_cast<__bf16 *>(w + o_wdg[z][l]);
+      if (l < 2) x->wfw[z][l] = reinterpret_cast<__bf16 *>(w + o_wfw[z][l]);
       x->cslab[z][l] = w + o_cslab[z][l];
     }
     x->a1[z] = w + o_a1[z];

@@ -105,6 +105,17 @@ __device__ __forceinline__ int pix_block(int p) {
   return oy * kS2dSide + (p - oy * L1::wout);
 }
 
+// Workgroup barrier for the per-image LDS hand-offs: waits for this wave's LDS operations only.
+// __syncthreads() is a workgroup-scope release / acquire, which also waits for every global load
+// and store the wave has in flight -- the next image's prefetch and this image's output stores --
+// and serialised one memory round trip per image.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -160,13 +171,13 @@ __global__ __launch_bounds__(kPixFwdThreads) void pixel_fwd_kernel(PixArgs q) {
   int img = blockIdx.x;
   if (img < q.nimg) prefetch(img);
   for (; img < q.nimg; img += gridDim.x) {
-    __syncthreads();  // every wave is done reading the previous frame
+    lds_barrier();  // every wave is done reading the previous frame
 #pragma unroll
     for (int i = 0; i < kPixFwdUnits; ++i) {
       const int u = tid + i * kPixFwdThreads;
       if (u < kPixUnits) pix_unit_store(fs, u, pre[i]);
     }
-    __syncthreads();
+    lds_barrier();
     if (img + static_cast<int>(gridDim.x) < q.nimg) prefetch(img + gridDim.x);
 
 #pragma unroll 1
@@ -278,7 +289,7 @@ __global__ __launch_bounds__(kPixWgThreads) void pixel_wgrad_kernel(PixArgs q) {
 
   if (i0 < i1) prefetch(i0);
   for (int img = i0; img < i1; ++img) {
-    __syncthreads();  // every wave is done reading the previous frame's images
+    lds_barrier();  // every wave is done reading the previous frame's images
 #pragma unroll
     for (int i = 0; i < kPixWgDzIters; ++i) {
       const int e = tid + i * kPixWgThreads;
@@ -299,7 +310,7 @@ __global__ __launch_bounds__(kPixWgThreads) void pixel_wgrad_kernel(PixArgs q) {
       const int u = tid + i * kPixWgThreads;
       if (u < kPixUnits) pix_unit_store(fs, u, pf[i]);
     }
-    __syncthreads();
+    lds_barrier();
     if (img + 1 < i1) prefetch(img + 1);
 
 #pragma unroll 1
