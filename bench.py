@@ -107,7 +107,6 @@ def apply_model_defaults(args, default_of) -> None:
         if getattr(args, k) == default_of(k):
             setattr(args, k, v)
     if args.model == "lstm":
-        args.no_timing = True  # the BiLSTM context has no per-kernel events: end-to-end roofline
         args.no_legs = True
         args.cpu_baseline = False
     if args.model == "cnn":
@@ -457,8 +456,8 @@ CONFIG_LEGS = {
 
 def config_leg(args, name, dev, steps=None, **over) -> dict:
     """One BASELINE-config leg on this GPU: its own workload, metric string, ms_per_step and
-    roofline (the leg's dominant kernel from live events, or -- for the BiLSTM context, which has
-    no per-kernel events -- the whole iteration's algorithmic FLOPs against the bf16 peak)."""
+    roofline (the leg's dominant kernel from live events; the whole iteration's algorithmic FLOPs
+    against the bf16 peak only if an engine recorded no per-kernel events)."""
     spec = dict(CONFIG_LEGS[name], **over)
     baseline = spec.pop("baseline")
     ns = argparse.Namespace(**vars(args))

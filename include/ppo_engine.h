@@ -420,6 +420,10 @@ int ppo_lstm_minibatch_grad(ppo_lstm_ctx *ctx, const float *states_d, const floa
                             const int32_t *rows_d, int b, float *grad_d, float *loss_d,
                             float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                             float inv_ba, void *stream);
+/* Per-launch event timing of this context (as ppo_ctx_timing / ppo_ctx_timing_kernel). */
+int ppo_lstm_timing(ppo_lstm_ctx *ctx, int enable, int capacity);
+int ppo_lstm_timing_kernel(ppo_lstm_ctx *ctx, int index, const char **name, int *kclass,
+                           double *total_ms, int64_t *launches, double *flops, double *bytes);
 
 /* ---- Pixel-observation actor-critic (BASELINE.json configs[4]) ----------------------------
  * dm_control cheetah-run pixel observations: u8 frames (H, W, C) = (84, 84, 3), HWC.  The

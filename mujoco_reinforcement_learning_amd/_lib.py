@@ -179,6 +179,10 @@ _SIGNATURES = {
                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_lstm_minibatch_grad": (c_int, [c_void_p] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]
                                 + [ctypes.c_float] * 5 + [c_void_p]),
+    "ppo_lstm_timing": (c_int, [c_void_p, c_int, c_int]),
+    "ppo_lstm_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
+                                       POINTER(c_double), POINTER(c_int64), POINTER(c_double),
+                                       POINTER(c_double)]),
     # pixel-observation actor-critic (cnn_engine.hip, conv.h)
     "ppo_cnn_ctx_create": (c_int, [POINTER(CnnCfg), c_int, POINTER(c_void_p)]),
     "ppo_cnn_ctx_destroy": (c_int, [c_void_p]),

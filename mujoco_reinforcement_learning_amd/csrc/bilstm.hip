@@ -80,39 +80,55 @@ struct CellArgs {
   int b, w, h, s;
 };
 
+// One thread per (row, direction, 4 consecutive units): every tensor is read and written as
+// float4 (H % 4 == 0, 16-B aligned buffers); per element the arithmetic of torch's LSTM cell.
 __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int H = q.h, W = q.w;
-  if (i >= static_cast<int64_t>(q.b) * 2 * H) return;
-  const int j = static_cast<int>(i % H);
-  const int d = static_cast<int>((i / H) & 1);
-  const int64_t b = i / (2 * H);
+  const int H = q.h, W = q.w, H4 = H / 4;
+  if (i >= static_cast<int64_t>(q.b) * 2 * H4) return;
+  const int j = 4 * static_cast<int>(i % H4);
+  const int d = static_cast<int>((i / H4) & 1);
+  const int64_t b = i / (2 * H4);
   const bool first = q.s == 0;
   const int t = d == 0 ? q.s : W - 1 - q.s;
   const int tp = d == 0 ? t - 1 : t + 1;
   float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
-  float pre[4];
+  float4 pre[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float hg = first ? q.b_hh[d][k * H + j] : q.gh[b * (8 * H) + d * (4 * H) + k * H + j];
-    pre[k] = hg + g[k * H + j];
+    const float4 hg = first ? *reinterpret_cast<const float4 *>(q.b_hh[d] + k * H + j)
+                            : *reinterpret_cast<const float4 *>(q.gh + b * (8 * H) + d * (4 * H) + k * H + j);
+    const float4 gx = *reinterpret_cast<const float4 *>(g + k * H + j);
+    pre[k] = make_float4(hg.x + gx.x, hg.y + gx.y, hg.z + gx.z, hg.w + gx.w);
   }
-  const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
-              og = sigmoidf_(pre[3]);
   const int64_t o = (b * W + t) * (2 * H) + d * H + j;
   const int64_t op = (b * W + tp) * (2 * H) + d * H + j;
-  const float cp = first ? 0.f : q.c[op];
-  const float c = fg * cp + ig * gg;  // (forgetgate * cx).add_(ingate * cellgate)
-  const float h = og * tanhf(c);
-  g[j] = ig;
-  g[H + j] = fg;
-  g[2 * H + j] = gg;
-  g[3 * H + j] = og;
-  q.c[o] = c;
-  q.y[o] = h;
-  q.hp[o] = first ? 0.f : q.y[op];
-  if (q.feat_mode == 1) q.feat[o] = act_forward(h, q.act);
-  else if (q.feat_mode == 2 && t == W - 1) q.feat[b * (2 * H) + d * H + j] = act_forward(h, q.act);
+  const float4 cp4 = first ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4 *>(q.c + op);
+  const float4 hp4 = first ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4 *>(q.y + op);
+  const float *pr[4] = {&pre[0].x, &pre[1].x, &pre[2].x, &pre[3].x};
+  const float cpv[4] = {cp4.x, cp4.y, cp4.z, cp4.w};
+  float ig[4], fg[4], gg[4], og[4], c[4], h[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ig[e] = sigmoidf_(pr[0][e]);
+    fg[e] = sigmoidf_(pr[1][e]);
+    gg[e] = tanhf(pr[2][e]);
+    og[e] = sigmoidf_(pr[3][e]);
+    c[e] = fg[e] * cpv[e] + ig[e] * gg[e];  // (forgetgate * cx).add_(ingate * cellgate)
+    h[e] = og[e] * tanhf(c[e]);
+  }
+  *reinterpret_cast<float4 *>(g + j) = make_float4(ig[0], ig[1], ig[2], ig[3]);
+  *reinterpret_cast<float4 *>(g + H + j) = make_float4(fg[0], fg[1], fg[2], fg[3]);
+  *reinterpret_cast<float4 *>(g + 2 * H + j) = make_float4(gg[0], gg[1], gg[2], gg[3]);
+  *reinterpret_cast<float4 *>(g + 3 * H + j) = make_float4(og[0], og[1], og[2], og[3]);
+  *reinterpret_cast<float4 *>(q.c + o) = make_float4(c[0], c[1], c[2], c[3]);
+  *reinterpret_cast<float4 *>(q.y + o) = make_float4(h[0], h[1], h[2], h[3]);
+  *reinterpret_cast<float4 *>(q.hp + o) = hp4;
+  if (q.feat_mode == 1 || (q.feat_mode == 2 && t == W - 1)) {
+    float *f = q.feat_mode == 1 ? q.feat + o : q.feat + b * (2 * H) + d * H + j;
+    *reinterpret_cast<float4 *>(f) = make_float4(act_forward(h[0], q.act), act_forward(h[1], q.act),
+                                                 act_forward(h[2], q.act), act_forward(h[3], q.act));
+  }
 }
 
 struct CellBwdArgs {
@@ -128,35 +144,56 @@ struct CellBwdArgs {
 
 __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int H = q.h, W = q.w;
-  if (i >= static_cast<int64_t>(q.b) * 2 * H) return;
-  const int j = static_cast<int>(i % H);
-  const int d = static_cast<int>((i / H) & 1);
-  const int64_t b = i / (2 * H);
+  const int H = q.h, W = q.w, H4 = H / 4;
+  if (i >= static_cast<int64_t>(q.b) * 2 * H4) return;
+  const int j = 4 * static_cast<int>(i % H4);
+  const int d = static_cast<int>((i / H4) & 1);
+  const int64_t b = i / (2 * H4);
   const int t = d == 0 ? W - 1 - q.s : q.s;          // reverse of the forward processing order
   const bool first_fwd = d == 0 ? t == 0 : t == W - 1;
   const int tp = d == 0 ? t - 1 : t + 1;
   const int64_t o = (b * W + t) * (2 * H) + d * H + j;
   const int64_t r = b * (2 * H) + d * H + j;
-  float dh = 0.f;
-  if (q.dy_mode == 1) dh = q.dy[o];
-  else if (t == W - 1) dh = q.dy_last[r];
-  if (q.s > 0) dh += q.dh_rec[r];
-  const float dc_in = q.s > 0 ? q.dcarry[r] : 0.f;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 dh4 = z4;
+  if (q.dy_mode == 1) dh4 = *reinterpret_cast<const float4 *>(q.dy + o);
+  else if (t == W - 1) dh4 = *reinterpret_cast<const float4 *>(q.dy_last + r);
+  const float4 dr4 = q.s > 0 ? *reinterpret_cast<const float4 *>(q.dh_rec + r) : z4;
+  const float4 dc4 = q.s > 0 ? *reinterpret_cast<const float4 *>(q.dcarry + r) : z4;
   float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
-  const float ig = g[j], fg = g[H + j], gg = g[2 * H + j], og = g[3 * H + j];
-  const float c = q.c[o];
-  const float cp = first_fwd ? 0.f : q.c[(b * W + tp) * (2 * H) + d * H + j];
-  const float tc = tanhf(c);
-  const float d_o = dh * tc;                          // hy = outgate * cy.tanh()
-  const float d_tc = dh * og;
-  const float dc = d_tc * (1.f - tc * tc) + dc_in;    // tanh_backward, + the next step's dcx
-  const float d_f = dc * cp, d_i = dc * gg, d_g = dc * ig;
-  q.dcarry[r] = dc * fg;
-  g[j] = (d_i * (1.f - ig)) * ig;                     // sigmoid_backward: g * (1 - y) * y
-  g[H + j] = (d_f * (1.f - fg)) * fg;
-  g[2 * H + j] = d_g * (1.f - gg * gg);               // tanh_backward
-  g[3 * H + j] = (d_o * (1.f - og)) * og;
+  const float4 ig4 = *reinterpret_cast<const float4 *>(g + j);
+  const float4 fg4 = *reinterpret_cast<const float4 *>(g + H + j);
+  const float4 gg4 = *reinterpret_cast<const float4 *>(g + 2 * H + j);
+  const float4 og4 = *reinterpret_cast<const float4 *>(g + 3 * H + j);
+  const float4 c4 = *reinterpret_cast<const float4 *>(q.c + o);
+  const float4 cp4 = first_fwd ? z4 : *reinterpret_cast<const float4 *>(q.c + (b * W + tp) * (2 * H) + d * H + j);
+  const float dhv[4] = {dh4.x, dh4.y, dh4.z, dh4.w}, drv[4] = {dr4.x, dr4.y, dr4.z, dr4.w};
+  const float dcv[4] = {dc4.x, dc4.y, dc4.z, dc4.w};
+  const float igv[4] = {ig4.x, ig4.y, ig4.z, ig4.w}, fgv[4] = {fg4.x, fg4.y, fg4.z, fg4.w};
+  const float ggv[4] = {gg4.x, gg4.y, gg4.z, gg4.w}, ogv[4] = {og4.x, og4.y, og4.z, og4.w};
+  const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, cpv[4] = {cp4.x, cp4.y, cp4.z, cp4.w};
+  float carry[4], di[4], df[4], dg[4], dout[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float dh = dhv[e];
+    if (q.s > 0) dh += drv[e];
+    const float dc_in = q.s > 0 ? dcv[e] : 0.f;
+    const float tc = tanhf(cv[e]);
+    const float d_o = dh * tc;                          // hy = outgate * cy.tanh()
+    const float d_tc = dh * ogv[e];
+    const float dc = d_tc * (1.f - tc * tc) + dc_in;    // tanh_backward, + the next step's dcx
+    const float d_f = dc * cpv[e], d_i = dc * ggv[e], d_g = dc * igv[e];
+    carry[e] = dc * fgv[e];
+    di[e] = (d_i * (1.f - igv[e])) * igv[e];            // sigmoid_backward: g * (1 - y) * y
+    df[e] = (d_f * (1.f - fgv[e])) * fgv[e];
+    dg[e] = d_g * (1.f - ggv[e] * ggv[e]);              // tanh_backward
+    dout[e] = (d_o * (1.f - ogv[e])) * ogv[e];
+  }
+  *reinterpret_cast<float4 *>(q.dcarry + r) = make_float4(carry[0], carry[1], carry[2], carry[3]);
+  *reinterpret_cast<float4 *>(g + j) = make_float4(di[0], di[1], di[2], di[3]);
+  *reinterpret_cast<float4 *>(g + H + j) = make_float4(df[0], df[1], df[2], df[3]);
+  *reinterpret_cast<float4 *>(g + 2 * H + j) = make_float4(dg[0], dg[1], dg[2], dg[3]);
+  *reinterpret_cast<float4 *>(g + 3 * H + j) = make_float4(dout[0], dout[1], dout[2], dout[3]);
 }
 
 __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) {
@@ -329,9 +366,15 @@ struct ppo_lstm_ctx {
   float *slabs;                      // [kSplits][total]
   float *row_part;                   // [rows][3]
   int maxw;
+  Timing tim;
 };
 
 namespace {
+
+struct TimingScope {
+  explicit TimingScope(ppo_lstm_ctx *x) { g_tim = x->tim.on ? &x->tim : nullptr; }
+  ~TimingScope() { g_tim = nullptr; }
+};
 
 void add_mlp(Mlp &m, int in, const ppo_lstm_cfg &c, int out, int final_act, int64_t &off,
              std::vector<int64_t> &offs) {
@@ -466,7 +509,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st
       a.h = H;
       a.s = s;
       launch_k(TimRec{KC_LSTM, "lstm_cell_fwd_kernel", 0.0, 0.0}, lstm_cell_fwd_kernel,
-               dim3(ceil_div(static_cast<int64_t>(b) * 2 * H, 256)), dim3(256), 0, st, a);
+               dim3(ceil_div(static_cast<int64_t>(b) * 2 * (H / 4), 256)), dim3(256), 0, st, a);
       PPO_LAUNCHED();
     }
   }
@@ -596,7 +639,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
       a.h = H;
       a.s = s;
       launch_k(TimRec{KC_LSTM, "lstm_cell_bwd_kernel", 0.0, 0.0}, lstm_cell_bwd_kernel,
-               dim3(ceil_div(static_cast<int64_t>(b) * 2 * H, 256)), dim3(256), 0, st, a);
+               dim3(ceil_div(static_cast<int64_t>(b) * 2 * (H / 4), 256)), dim3(256), 0, st, a);
       PPO_LAUNCHED();
     }
     const float *in = l == 0 ? xin : x->y[z][l - 1];
@@ -784,6 +827,13 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
 
 extern "C" int ppo_lstm_ctx_destroy(ppo_lstm_ctx *x) {
   if (!x) return 0;
+  (void)timing_enable(x->tim, 0, 0);
+  for (int i = 0; i < 2 * x->tim.capacity; ++i) (void)hipEventDestroy(x->tim.ev[i]);
+  delete[] x->tim.ev;
+  delete[] x->tim.cls;
+  delete[] x->tim.kname;
+  delete[] x->tim.flops;
+  delete[] x->tim.bytes;
   if (x->ws) (void)hipFree(x->ws);
   delete x;
   return 0;
@@ -822,6 +872,7 @@ extern "C" int ppo_lstm_forward(ppo_lstm_ctx *x, const float *state_d, int n, fl
   if (int rc = check_rows(x, n)) return rc;
   if (n == 0) return 0;
   PPO_HIP_TRY(hipSetDevice(x->device));
+  TimingScope ts(x);
   hipStream_t st = as_stream(stream);
   if (int rc = forward_all(x, state_d, n, st)) return rc;
   const int A = x->cfg.act_dim, W = x->cfg.window;
@@ -858,6 +909,7 @@ extern "C" int ppo_lstm_policy_step(ppo_lstm_ctx *x, const float *state_d, int n
   if (int rc = check_rows(x, n)) return rc;
   if (n == 0) return 0;
   PPO_HIP_TRY(hipSetDevice(x->device));
+  TimingScope ts(x);
   hipStream_t st = as_stream(stream);
   if (int rc = forward_all(x, state_d, n, st)) return rc;
   const int nl = x->cfg.n_hidden;
@@ -890,6 +942,7 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   if (int rc = check_rows(x, b)) return rc;
   PPO_REQUIRE(b > 0, "ppo_lstm_minibatch_grad: empty minibatch");
   PPO_HIP_TRY(hipSetDevice(x->device));
+  TimingScope ts(x);
   hipStream_t st = as_stream(stream);
   const ppo_lstm_cfg &c = x->cfg;
   const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
@@ -963,4 +1016,16 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
            dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);
   PPO_LAUNCHED();
   return 0;
+}
+
+extern "C" int ppo_lstm_timing(ppo_lstm_ctx *x, int enable, int capacity) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_timing: null ctx");
+  return timing_enable(x->tim, enable, capacity);
+}
+
+extern "C" int ppo_lstm_timing_kernel(ppo_lstm_ctx *x, int index, const char **name, int *kclass,
+                                      double *total_ms, int64_t *launches, double *flops,
+                                      double *bytes) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_timing_kernel: null ctx");
+  return timing_read_kernel(x->tim, index, name, kclass, total_ms, launches, flops, bytes);
 }

@@ -73,6 +73,11 @@ __device__ __forceinline__ void pix_unit_load(const uint8_t *frame, int u, uint3
   w[2] = p[2];
 }
 
+// bf16(x * fl(1/255)) == bf16(x / 255) for every u8 x (tests/test_pixel_scale.py checks all 256;
+// the f32 products differ from the quotients in 126 of them, never after the bf16 rounding), so
+// the bf16 staging multiplies instead of running the IEEE divide sequence per byte.
+constexpr float kInv255 = 1.f / 255.f;
+
 // unit u = (y, bx) -> 12 bf16 at block (y / 4, bx), offset (y % 4) * 12
 __device__ __forceinline__ void pix_unit_store(__bf16 *s, int u, const uint32_t (&w)[3]) {
   const int y = u / kS2dSide, bx = u - y * kS2dSide;
@@ -82,8 +87,8 @@ __device__ __forceinline__ void pix_unit_store(__bf16 *s, int u, const uint32_t 
   for (int j = 0; j < 6; ++j) {
     const uint32_t word = w[j >> 1];
     const int sh = 16 * (j & 1);
-    const float lo = static_cast<float>((word >> sh) & 255u) / 255.f;
-    const float hi = static_cast<float>((word >> (sh + 8)) & 255u) / 255.f;
+    const float lo = static_cast<float>((word >> sh) & 255u) * kInv255;
+    const float hi = static_cast<float>((word >> (sh + 8)) & 255u) * kInv255;
     o[j] = pack_bf16x2(lo, hi);
   }
 #pragma unroll

@@ -61,18 +61,13 @@ class DataParallel:
         return self.world > 1 or self.rehearse
 
     def allreduce_grad(self, flat_grad: torch.Tensor) -> None:
-        """SUM of the flat gradient over ranks, in place, ordered on the current stream."""
+        """SUM of the flat gradient over ranks, in place, ordered on the current stream (RCCL
+        runs it on its own stream; the compute stream waits on it, the host does not).  There is
+        no asynchronous form: nothing independent sits between the gradient and its use -- Adam
+        consumes the sum and the next minibatch's forward consumes Adam's weights."""
         if self.world > 1:
             torch.distributed.all_reduce(flat_grad, op=torch.distributed.ReduceOp.SUM,
                                          group=self.pg)
-
-    def allreduce_grad_async(self, flat_grad: torch.Tensor):
-        """Start the SUM all-reduce and return its work handle (None on one rank); the caller
-        issues independent work on the compute stream, then ``wait()``s before using the sum."""
-        if self.world > 1:
-            return torch.distributed.all_reduce(flat_grad, op=torch.distributed.ReduceOp.SUM,
-                                                group=self.pg, async_op=True)
-        return None
 
     def broadcast_params(self, flat: torch.Tensor, src: int = 0) -> None:
         """Start every replica from rank ``src``'s parameters."""

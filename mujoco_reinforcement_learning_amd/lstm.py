@@ -172,6 +172,35 @@ class LSTMEngine:
             ptr(rows), int(b), ptr(grad), ptr(loss), clip_lo, clip_hi, entropy_coef, inv_b,
             inv_ba, _stream(self.device)))
 
+    # ---- measurement (the Engine.timing* contract of bench.py) ----------------------------------
+    def timing(self, enable: bool, capacity: int = 65536) -> None:
+        check(self.lib.ppo_lstm_timing(self._ctx, int(enable), int(capacity)))
+
+    def timing_kernels(self) -> dict:
+        out = {}
+        n_k = self.lib.ppo_lstm_timing_kernel(self._ctx, -1, None, None, None, None, None, None)
+        check(min(n_k, 0))
+        for i in range(n_k):
+            name, cls = ctypes.c_char_p(), ctypes.c_int()
+            ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            cnt = ctypes.c_int64()
+            check(self.lib.ppo_lstm_timing_kernel(self._ctx, i, ctypes.byref(name),
+                                                  ctypes.byref(cls), ctypes.byref(ms),
+                                                  ctypes.byref(cnt), ctypes.byref(fl),
+                                                  ctypes.byref(by)))
+            out[name.value.decode()] = {
+                "class": self.lib.ppo_kernel_class_name(cls.value).decode(), "ms": ms.value,
+                "launches": cnt.value, "flops": fl.value, "bytes": by.value}
+        return out
+
+    def timing_read(self) -> dict:
+        out = {}
+        for name, k in self.timing_kernels().items():
+            c = out.setdefault(k["class"], {"ms": 0.0, "launches": 0, "flops": 0.0, "bytes": 0.0})
+            for key in ("ms", "launches", "flops", "bytes"):
+                c[key] += k[key]
+        return out
+
 
 class EngineLSTMActor(nn.Module):
     """models/lstm/lstm_actor.py:9-38 (parameters only; forward through the engine)."""

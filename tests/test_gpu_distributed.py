@@ -235,9 +235,9 @@ def _rccl_worker(q):
     x = torch.arange(142605, dtype=torch.float32, device=dev) * 0.5  # the 2x256 flat gradient size
     want = x.clone()
     torch.distributed.all_reduce(x, op=torch.distributed.ReduceOp.SUM)
-    work = DataParallel().allreduce_grad_async(x)  # world 1: no collective, no handle
+    DataParallel().allreduce_grad(x)  # world 1: no collective
     torch.cuda.synchronize()
-    q.put((torch.equal(x.cpu(), want.cpu()), work is None, torch.distributed.get_backend()))
+    q.put((torch.equal(x.cpu(), want.cpu()), torch.distributed.get_backend()))
     torch.distributed.destroy_process_group()
 
 
@@ -256,9 +256,9 @@ def test_rccl_allreduce_known_answer(gpu):
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(q,))
     p.start()
-    ok, no_handle, backend = q.get(timeout=300)
+    ok, backend = q.get(timeout=300)
     p.join(timeout=60)
-    assert p.exitcode == 0 and ok and no_handle and backend == "nccl"
+    assert p.exitcode == 0 and ok and backend == "nccl"
 
 
 def test_bench_self_launches_two_ranks_on_one_gpu(gpu):

@@ -8,6 +8,7 @@
 #   host      bench --env host (PCIe-inclusive) -> gpurun_out/bench_${TAG}_host.json
 #   trace     rocprofv3 --kernel-trace --stats over the bench + timing agreement
 #   traffic   FETCH_SIZE / WRITE_SIZE PMC passes over the bench -> traffic per launch
+#   trafficall  the same over the bench with its config legs (every leg's roofline.traffic)
 #   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
 #   phases    fused-update phase stamps (tools/fused_phases.py)
 #   wbench    tools/wide_bench.py: the wide-path bf16 GEMMs at Humanoid shapes vs torch's matmul
@@ -21,6 +22,7 @@
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
+#   cnnpmc    SQ counter passes over one pixel-CNN iteration (LDS-staged conv kernels)
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -68,6 +70,17 @@ for S in $STEPS; do
         > gpurun_out/rp_${TAG}_write.log 2>&1 || fail write gpurun_out/rp_${TAG}_write.log
       python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_fetch -name "*counter_collection.csv") \
         $(find gpurun_out/rp_${TAG}_write -name "*counter_collection.csv") gpurun_out/traffic_${TAG}.json ;;
+    trafficall)
+      # FETCH_SIZE / WRITE_SIZE passes over the bench INCLUDING its config legs (Ant, Humanoid
+      # shard, pixel CNN, BiLSTM): per-kernel traffic for every leg's roofline -> bench_traffic.json
+      timeout -s KILL 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/rp_${TAG}_fetchall -o fetch --output-format csv \
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --leg-steps 1 \
+        > gpurun_out/rp_${TAG}_fetchall.log 2>&1 || fail fetchall gpurun_out/rp_${TAG}_fetchall.log
+      timeout -s KILL 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/rp_${TAG}_writeall -o write --output-format csv \
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --leg-steps 1 \
+        > gpurun_out/rp_${TAG}_writeall.log 2>&1 || fail writeall gpurun_out/rp_${TAG}_writeall.log
+      python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_fetchall -name "*counter_collection.csv") \
+        $(find gpurun_out/rp_${TAG}_writeall -name "*counter_collection.csv") gpurun_out/trafficall_${TAG}.json ;;
     pmc)
       i=0
       # one pass per space-separated word (at most 8 SQ_ counters each)
@@ -79,6 +92,20 @@ for S in $STEPS; do
       done
       python3 tools/pmc_summary.py gpurun_out/pmc_${TAG} fused_update > gpurun_out/pmc_${TAG}.txt
       cat gpurun_out/pmc_${TAG}.txt ;;
+    cnnpmc)
+      # SQ counter passes over one pixel-CNN iteration (the LDS-staged conv kernels)
+      i=0
+      PASSES=${PASSES:-"SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_INSTS_VALU,SQ_INSTS_LDS SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_BUSY_CYCLES,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,GRBM_GUI_ACTIVE"}
+      for P in $PASSES; do
+        i=$((i+1))
+        timeout -s KILL 300 rocprofv3 --pmc ${P//,/ } -d gpurun_out/cpmc_${TAG}/p$i -o pmc --output-format csv \
+          -- python3 bench.py --model cnn --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs \
+          > gpurun_out/cpmc_${TAG}_p$i.log 2>&1 || fail cnnpmc$i gpurun_out/cpmc_${TAG}_p$i.log
+      done
+      for KN in fwd_lds_kernel dgrad_lds_kernel wgrad_lds_kernel pixel_fwd pixel_wgrad; do
+        echo "--- $KN"; python3 tools/pmc_summary.py gpurun_out/cpmc_${TAG} $KN
+      done > gpurun_out/cpmc_${TAG}.txt
+      cat gpurun_out/cpmc_${TAG}.txt ;;
     phases)
       timeout -k 10 200 python tools/fused_phases.py > gpurun_out/phases_${TAG}.txt 2>&1 || fail phases gpurun_out/phases_${TAG}.txt
       cat gpurun_out/phases_${TAG}.txt ;;

@@ -30,13 +30,30 @@ def kernel_key(name: str) -> str:
     return name[5:] if name.startswith("ppo::") else name
 
 
+_LAYER = {"32, 20,": "L2", "64, 9,": "L3"}
+
+
+def bench_key(key: str) -> str:
+    """The name bench.py's event records use: namespaces dropped ('conv::pixel_wgrad_kernel' ->
+    'pixel_wgrad_kernel'), and the LDS-staged conv kernels named by layer
+    ('conv::dgrad_lds_kernel<ppo::conv::DgGeo<32, 20, ...>>' -> 'dgrad_lds_kernel<L2>')."""
+    head, sep, rest = key.partition("<")
+    head = head.split("::")[-1]
+    if head in ("fwd_lds_kernel", "dgrad_lds_kernel", "wgrad_lds_kernel", "dg_pack_kernel",
+                "fw_pack_kernel"):
+        for sig, layer in _LAYER.items():
+            if sig in rest:
+                return f"{head}<{layer}>" if "lds" in head else head
+    return head + sep + rest
+
+
 def per_kernel(path: str, counter: str) -> dict:
     tot, cnt = defaultdict(float), defaultdict(int)
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
                 continue
-            k = kernel_key(row["Kernel_Name"])
+            k = bench_key(kernel_key(row["Kernel_Name"]))
             tot[k] += float(row["Counter_Value"])
             cnt[k] += 1
     return {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
