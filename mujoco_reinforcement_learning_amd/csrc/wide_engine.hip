@@ -22,6 +22,7 @@
 #include <new>
 
 #include "common.h"
+#include "fused_common.h"
 #include "reduce_slabs.h"
 #include "timing.h"
 #include "wide_gemm.h"
@@ -34,7 +35,15 @@ using wide::WideBatch;
 using wide::WideProblem;
 
 static inline int64_t rup(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
-constexpr int kWideSplits = 16;      // WGRAD split-K slabs of the hidden layers
+constexpr int kWideSplits = 16;      // WGRAD split-K slabs of the hidden layers (at most)
+// Split-K slabs of the hidden-layer WGRAD: PPO_WIDE_SPLITS (1 .. 16, default 16).  Every slab is
+// a full f32 copy of the layer's gradient written by WGRAD and read by wide_reduce_kernel, so at
+// small minibatches (8,192 rows per rank) fewer, longer splits move fewer bytes.
+static const int g_wide_splits = [] {
+  const char *v = getenv("PPO_WIDE_SPLITS");
+  const int n = v ? atoi(v) : kWideSplits;
+  return n < 1 ? 1 : (n > kWideSplits ? kWideSplits : n);
+}();
 constexpr int kWideHeadSplits = 64;  // ... of the heads (few output tiles)
 static const int g_wide_enabled = [] {
   const char *v = getenv("PPO_WIDE");
@@ -1090,46 +1099,43 @@ struct WideLossArgs {
   float *part, *loss_part;
 };
 
-// Block partials: per action a, the wave's butterfly sums of d loss / d logstd_a and of dz_a go
-// to LDS, then waves 0..3 are added in order; the same for the critic bias gradient and the two
-// loss terms.  The per-action values are recomputed in a second pass (tanh again) rather than
-// kept in per-lane arrays.
-__device__ __forceinline__ float wave_bfly(float s) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-  return s;
+// One thread per (row, action): 32 lanes per row, kWideLossRows = 8 rows per 256-thread block, so
+// an 8,192-row minibatch is 1,024 blocks (the first form ran one thread per row over the actions
+// in a serial loop: 32 blocks, each lane a chain of 2 x 17 tanh / divide steps). The row's
+// log-prob is the sum of its 32 lanes (DPP within 16-lane rows + v_permlane16_swap); the block
+// partials per action (d loss / d logstd_a, dz_a), the critic bias gradient and the two loss terms
+// are added over the block's 8 rows in row order.
+__device__ __forceinline__ float half_sum32(float s) {  // sum over each 32-lane half, every lane
+  s = fu::row16_sum(s);
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
 
-__global__ __launch_bounds__(kWideLossRows) void wide_loss_kernel(WideLossArgs q) {
-  constexpr int NWV = kWideLossRows / 64;
-  __shared__ float red[NWV][kWidePart];
-  __shared__ float lred[NWV][2];
-  __shared__ float s_sd[32], s_logsd[32], s_var[32], s_b[32];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+__global__ __launch_bounds__(256) void wide_loss_kernel(WideLossArgs q) {
+  static_assert(kWideLossRows * 32 == 256, "32 lanes per row");
+  __shared__ float rls[kWideLossRows][32], rdz[kWideLossRows][32], rrow[kWideLossRows][3];
+  __shared__ float s_logsd[32], s_var[32], s_b[32];
+  const int tid = threadIdx.x, a = tid & 31, r = tid >> 5;
   const int A = q.act_dim;
   if (tid < 32) {
     const float sd = tid < A ? expf(q.logstd[tid]) : 1.f;
-    s_sd[tid] = sd;
     s_logsd[tid] = logf(sd);
     s_var[tid] = sd * sd;
     s_b[tid] = (q.ba && tid < A) ? q.ba[tid] : 0.f;
   }
   __syncthreads();
   const int count = q.rows_n ? *q.rows_n : q.b;
-  const int j = blockIdx.x * kWideLossRows + tid;
+  const int j = blockIdx.x * kWideLossRows + r;
   const bool valid = j < count;
+  const bool act = a < A;
   const int64_t sr = valid ? q.rows[j] : 0;
-  const float *zr = q.za + static_cast<int64_t>(j) * 32;
-  const float *xr = q.actions + sr * A;
-  const bool has_b = q.ba != nullptr;
-  float logp = 0.f;
-  for (int a = 0; a < A; ++a) {
-    const float z = has_b ? zr[a] + s_b[a] : zr[a];
-    const float mu = q.omv * tanhf(z);
-    const float x = valid ? xr[a] : mu;
-    const float d = x - mu;
-    logp += ((-(d * d)) / (2.f * s_var[a]) - s_logsd[a]) - kLogSqrt2Pi;
-  }
+  const float var = s_var[a];
+  const float z = q.za[static_cast<int64_t>(j) * 32 + a] + s_b[a];
+  const float y = tanhf(z);
+  const float mu = q.omv * y;
+  const float x = (valid && act) ? q.actions[sr * A + a] : mu;
+  const float d = x - mu;
+  const float logp = half_sum32(act ? ((-(d * d)) / (2.f * var) - s_logsd[a]) - kLogSqrt2Pi : 0.f);
   const float old_lp = valid ? q.old_logp[sr] : logp;
   const float adv = valid ? q.adv[sr] : 0.f;
   const float ratio = expf(logp - old_lp);
@@ -1143,61 +1149,45 @@ __global__ __launch_bounds__(kWideLossRows) void wide_loss_kernel(WideLossArgs q
   const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
   const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
   const float dlogp = valid ? dratio * ratio : 0.f;
-  uint32_t *dzrow = reinterpret_cast<uint32_t *>(q.dza + static_cast<int64_t>(j) * 64);
-  for (int a0 = 0; a0 < A; a0 += 2) {
-    float dzp[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int a = a0 + h;
-      float dz = 0.f, ls = 0.f;
-      if (a < A) {
-        const float z = has_b ? zr[a] + s_b[a] : zr[a];
-        const float y = tanhf(z);
-        const float mu = q.omv * y;
-        const float x = valid ? xr[a] : mu;
-        const float d = x - mu;
-        const float dmu = dlogp * (d / s_var[a]);
-        dz = valid ? (dmu * q.omv) * (1.f - y * y) : 0.f;
-        ls = valid ? dlogp * ((d * d) / s_var[a] - 1.f) - q.ent_coef * q.inv_ba : 0.f;
-        const float sl = wave_bfly(ls), sz = wave_bfly(dz);
-        if (lane == 0) {
-          red[wid][a] = sl;
-          red[wid][32 + a] = sz;
-        }
-      }
-      dzp[h] = dz;
-    }
-    dzrow[a0 >> 1] = wide::pack2(dzp[0], dzp[1]);  // columns >= A stay zero (never written)
-  }
-  // critic
-  const float zc0 = q.zc[static_cast<int64_t>(j) * 32];
-  const float v = q.bc ? zc0 + q.bc[0] : zc0;
-  const float vt = valid ? q.vtarget[sr] : v;
-  const float diff = v - vt;
-  const float ad = fabsf(diff);
-  const float dv = valid ? q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff)) : 0.f;
-  reinterpret_cast<uint32_t *>(q.dzc + static_cast<int64_t>(j) * 64)[0] = wide::pack2(dv, 0.f);
-  const float sdv = wave_bfly(dv);
-  const float sla = wave_bfly(valid ? mn : 0.f);
-  const float slc = wave_bfly(valid ? ((ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f)) : 0.f);
-  if (lane == 0) {
-    red[wid][64] = sdv;
-    lred[wid][0] = sla;
-    lred[wid][1] = slc;
+  const bool live = valid && act;
+  const float dmu = dlogp * (d / var);
+  const float dz = live ? (dmu * q.omv) * (1.f - y * y) : 0.f;
+  const float ls = live ? dlogp * ((d * d) / var - 1.f) - q.ent_coef * q.inv_ba : 0.f;
+  // dz row: column pairs (a, a + 1) packed by the even lane (columns >= A are zero)
+  const float dz_next = fu::dpp_f<fu::kDppXor1>(dz);
+  if ((a & 1) == 0)
+    reinterpret_cast<uint32_t *>(q.dza + static_cast<int64_t>(j) * 64)[a >> 1] = wide::pack2(dz, dz_next);
+  rls[r][a] = ls;
+  rdz[r][a] = dz;
+  if (a == 0) {  // critic and the row's loss terms
+    const float zc0 = q.zc[static_cast<int64_t>(j) * 32];
+    const float v = q.bc ? zc0 + q.bc[0] : zc0;
+    const float vt = valid ? q.vtarget[sr] : v;
+    const float diff = v - vt;
+    const float ad = fabsf(diff);
+    const float dv = valid ? q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff)) : 0.f;
+    reinterpret_cast<uint32_t *>(q.dzc + static_cast<int64_t>(j) * 64)[0] = wide::pack2(dv, 0.f);
+    rrow[r][0] = dv;
+    rrow[r][1] = valid ? mn : 0.f;
+    rrow[r][2] = valid ? ((ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f)) : 0.f;
   }
   __syncthreads();
   float *part = q.part + static_cast<int64_t>(blockIdx.x) * kWidePart;
-  if (tid < 65 && (tid >= 64 || (tid & 31) < A)) {
-    float s = red[0][tid];
+  if (tid < 64) {  // logstd grads [0, 32), actor head bias [32, 64): rows in order
+    const int col = tid & 31;
+    if (col < A) {
+      float s = 0.f;
 #pragma unroll
-    for (int w = 1; w < NWV; ++w) s += red[w][tid];
-    part[tid] = s;
-  } else if (tid == 65 || tid == 66) {
-    const int k = tid - 65;
-    float s = lred[0][k];
+      for (int k = 0; k < kWideLossRows; ++k) s += tid < 32 ? rls[k][col] : rdz[k][col];
+      part[tid] = s;
+    }
+  } else if (tid < 67) {  // critic bias [64], then the actor / critic loss partials
+    const int c = tid - 64;
+    float s = 0.f;
 #pragma unroll
-    for (int w = 1; w < NWV; ++w) s += lred[w][k];
-    q.loss_part[2 * blockIdx.x + k] = s;
+    for (int k = 0; k < kWideLossRows; ++k) s += rrow[k][c];
+    if (c == 0) part[64] = s;
+    else q.loss_part[2 * blockIdx.x + c - 1] = s;
   }
 }
 
@@ -1254,7 +1244,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
     q.loss_part = W.loss_part;
     launch_k(TimRec{KC_UPDATE_HEAD, "wide_loss_kernel", 0.0,
                     static_cast<double>(b) * (4.0 * 64 + 4.0 * A + 16.0 + 256.0)},
-             wide_loss_kernel, dim3(blocks), dim3(kWideLossRows), 0, st, q);
+             wide_loss_kernel, dim3(blocks), dim3(256), 0, st, q);
     PPO_LAUNCHED();
   }
 
@@ -1288,7 +1278,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
       max_n = std::max(max_n, L.in);
     }
     if (np) {
-      wg.splits = s == 0 ? kWideHeadSplits : kWideSplits;
+      wg.splits = s == 0 ? kWideHeadSplits : g_wide_splits;
       for (int z = 0; z < 2; ++z)
         if (ctx->net[z].n_hidden - s >= 0) splits_of[z][ctx->net[z].n_hidden - s] = wg.splits;
       if (int rc = wide::run(wide::WK_WGRAD, wg, np, max_m, max_n, b, st)) return rc;

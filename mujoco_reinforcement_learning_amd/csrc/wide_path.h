@@ -42,7 +42,7 @@ struct WideWork {
   void *arena;
 };
 
-constexpr int kWideLossRows = 256;  // rows per loss-kernel block
+constexpr int kWideLossRows = 8;    // rows per loss-kernel block (32 lanes per row)
 constexpr int kWidePart = 96;       // per block: logstd grads [0,32), actor head bias [32,64),
                                     // critic head bias [64]
 

@@ -22,6 +22,7 @@
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
+#   abhum     Humanoid shard line per value of one env knob (ABVAR, ABVALS)
 #   cnnpmc    SQ counter passes over one pixel-CNN iteration (LDS-staged conv kernels)
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
 set -o pipefail
@@ -118,6 +119,16 @@ for S in $STEPS; do
         -- python3 bench.py --model lstm --steps 1 --warmup 1 $LSTM_ARGS > gpurun_out/rp_${TAG}_lstm.json \
         2> gpurun_out/rp_${TAG}_lstm.log || fail lstmtrace gpurun_out/rp_${TAG}_lstm.log
       head -12 $(find gpurun_out/rp_${TAG}_lstm -name "*kernel_stats.csv") ;;
+    abhum)
+      # A/B of one environment knob on the Humanoid shard line: ABVAR=NAME ABVALS="v1 v2 ..."
+      for V in $ABVALS; do
+        env $ABVAR=$V timeout -k 10 500 python bench.py --num-envs 1024 --obs-dim 376 --act-dim 17 \
+          --hidden 512,512,512 --batch ${HUM_BATCH:-8192} --steps 3 --warmup 2 --no-legs --no-cpu-baseline \
+          > gpurun_out/bench_${TAG}_hum_$V.json 2> gpurun_out/bench_${TAG}_hum_$V.err \
+          || fail abhum gpurun_out/bench_${TAG}_hum_$V.err
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['ms_per_step'])" \
+          gpurun_out/bench_${TAG}_hum_$V.json
+      done ;;
     cnn)
       timeout -k 10 600 python bench.py --model cnn $CNN_ARGS > gpurun_out/bench_${TAG}_cnn.json \
         2> gpurun_out/bench_${TAG}_cnn.err || fail cnn gpurun_out/bench_${TAG}_cnn.err
@@ -139,7 +150,7 @@ for S in $STEPS; do
       cat gpurun_out/bench_${TAG}_dp1.json ;;
     hum)
       timeout -k 10 500 python bench.py --num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 \
-        --steps 3 --warmup 1 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
+        --batch ${HUM_BATCH:-8192} --steps 3 --warmup 2 --no-legs --no-cpu-baseline > gpurun_out/bench_${TAG}_hum.json \
         2> gpurun_out/bench_${TAG}_hum.err || fail hum gpurun_out/bench_${TAG}_hum.err
       cat gpurun_out/bench_${TAG}_hum.json ;;
     humtrace)
