@@ -9,6 +9,7 @@
 #   trace     rocprofv3 --kernel-trace --stats over the bench + timing agreement
 #   traffic   FETCH_SIZE / WRITE_SIZE PMC passes over the bench -> traffic per launch
 #   trafficall  the same over the bench with its config legs (every leg's roofline.traffic)
+#   trafficlegs the same per workload in separate processes (LEGS="main ant hum cnn lstm"), merged
 #   pmc       SQ wait / issue / LDS / MFMA counter passes over tools/micro_fused.py
 #   phases    fused-update phase stamps (tools/fused_phases.py)
 #   wbench    tools/wide_bench.py: the wide-path bf16 GEMMs at Humanoid shapes vs torch's matmul
@@ -82,6 +83,30 @@ for S in $STEPS; do
         > gpurun_out/rp_${TAG}_writeall.log 2>&1 || fail writeall gpurun_out/rp_${TAG}_writeall.log
       python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_fetchall -name "*counter_collection.csv") \
         $(find gpurun_out/rp_${TAG}_writeall -name "*counter_collection.csv") gpurun_out/trafficall_${TAG}.json ;;
+    trafficlegs)
+      # FETCH_SIZE / WRITE_SIZE passes per workload (LEGS="main ant hum cnn lstm"), one process each,
+      # merged into gpurun_out/trafficlegs_${TAG}.json (copy it to bench_traffic.json)
+      BASE="--steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs"
+      outs=""
+      for L in ${LEGS:-main ant hum lstm cnn}; do
+        case $L in
+          main) A="" ;;
+          ant) A="--num-envs 4096 --obs-dim 27 --act-dim 8" ;;
+          hum) A="--num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 --batch 8192" ;;
+          cnn) A="--model cnn" ;;
+          lstm) A="--model lstm" ;;
+        esac
+        for C in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 300 rocprofv3 --pmc $C -d gpurun_out/rp_${TAG}_${L}_$C -o pmc --output-format csv \
+            -- python3 bench.py $BASE $A > gpurun_out/rp_${TAG}_${L}_$C.log 2>&1 \
+            || fail "traffic $L $C" gpurun_out/rp_${TAG}_${L}_$C.log
+        done
+        python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_${L}_FETCH_SIZE -name "*counter_collection.csv") \
+          $(find gpurun_out/rp_${TAG}_${L}_WRITE_SIZE -name "*counter_collection.csv") gpurun_out/traffic_${TAG}_$L.json \
+          > /dev/null
+        outs="$outs gpurun_out/traffic_${TAG}_$L.json"
+      done
+      python tools/merge_traffic.py gpurun_out/trafficlegs_${TAG}.json $outs ;;
     pmc)
       i=0
       # one pass per space-separated word (at most 8 SQ_ counters each)
