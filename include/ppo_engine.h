@@ -420,6 +420,11 @@ int ppo_lstm_minibatch_grad(ppo_lstm_ctx *ctx, const float *states_d, const floa
                             const int32_t *rows_d, int b, float *grad_d, float *loss_d,
                             float clip_lo, float clip_hi, float entropy_coef, float inv_b,
                             float inv_ba, void *stream);
+/* bf16 forward steps s > 0 as one launch per step (the recurrent projection h W_hh^T on MFMA with
+ * the cell in its epilogue: lstm_step_fwd_kernel; latent a multiple of 64) instead of the
+ * projection GEMM + lstm_cell_fwd_kernel pair; bitwise the same results.  enable < 0 queries;
+ * default PPO_LSTM_FUSED_STEP (1). */
+int ppo_lstm_fused_step(ppo_lstm_ctx *ctx, int enable);
 /* Per-launch event timing of this context (as ppo_ctx_timing / ppo_ctx_timing_kernel). */
 int ppo_lstm_timing(ppo_lstm_ctx *ctx, int enable, int capacity);
 int ppo_lstm_timing_kernel(ppo_lstm_ctx *ctx, int index, const char **name, int *kclass,

@@ -179,6 +179,7 @@ _SIGNATURES = {
                                      c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_lstm_minibatch_grad": (c_int, [c_void_p] + [c_void_p] * 6 + [c_int, c_void_p, c_void_p]
                                 + [ctypes.c_float] * 5 + [c_void_p]),
+    "ppo_lstm_fused_step": (c_int, [c_void_p, c_int]),
     "ppo_lstm_timing": (c_int, [c_void_p, c_int, c_int]),
     "ppo_lstm_timing_kernel": (c_int, [c_void_p, c_int, POINTER(ctypes.c_char_p), POINTER(c_int),
                                        POINTER(c_double), POINTER(c_int64), POINTER(c_double),

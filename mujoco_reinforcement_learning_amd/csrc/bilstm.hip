@@ -131,6 +131,132 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
   }
 }
 
+// ---- one forward step s > 0 in one launch (bf16 mode) ----------------------------------------
+// The recurrent projection gh = h_prev W_hh^T + b_hh on MFMA with lstm_cell_fwd_kernel's cell in
+// the epilogue, for both directions (blockIdx.z): the layered form writes gh ([B][2][4H] f32) in a
+// GEMM and reads it back in the cell kernel.  A workgroup owns 64 rows x 64 hidden units and all
+// four gates of them (a lane's accumulators hold i, f, g, o of the same (row, unit), so the cell
+// needs no exchange).  Bitwise the layered result: the operands rounded to bf16 (RNE) as staged,
+// the K order of gemm_bf16_kernel (k-steps of 16 in order into one v_mfma_f32_32x32x16_bf16
+// accumulator), gh = acc + b_hh, then pre = gh + Gx and the same cell arithmetic.
+constexpr int kStepRows = 64, kStepUnits = 64, kStepBK = 32;
+struct StepArgs {
+  CellArgs cell;
+  const float *whh[2];  // W_hh per direction, [4H][H] f32 (torch layout)
+};
+
+typedef __bf16 lstm_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
+  constexpr int AP = kStepBK + 8;                 // bf16 image row pitch (16 B of padding)
+  constexpr int AIMG = kStepRows * AP, BIMG = 4 * kStepUnits * AP;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * (AIMG + BIMG)];
+  const CellArgs &c = q.cell;
+  const int H = c.h, W = c.w;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int mt = wv & 1, ug = wv >> 1;
+  const int r0 = blockIdx.x * kStepRows, j0 = blockIdx.y * kStepUnits, d = blockIdx.z;
+  const int t = d == 0 ? c.s : W - 1 - c.s;
+  const int tp = d == 0 ? t - 1 : t + 1;
+  const float *arow = c.y + static_cast<int64_t>(tp) * 2 * H + d * H;  // + row * W * 2H + k
+  const int64_t lda = static_cast<int64_t>(W) * 2 * H;
+  const float *wb = q.whh[d];
+
+  // staging: A 64 rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63) x
+  // 32 k (8 float4 per thread); rows past b load row b-1 (clamped, results discarded)
+  float4 va[2], vb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
+      const int row = min(r0 + rr, c.b - 1);
+      va[u] = *reinterpret_cast<const float4 *>(arow + row * lda + k0 + kk);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
+      vb[u] = *reinterpret_cast<const float4 *>(wb + static_cast<int64_t>(gate * H + j0 + jj) * H + k0 + kk);
+    }
+  };
+  auto lstore = [&](int buf) {
+    __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
+      *reinterpret_cast<uint2 *>(ai + rr * AP + kk) =
+          make_uint2(pack_bf16x2(va[u].x, va[u].y), pack_bf16x2(va[u].z, va[u].w));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
+      *reinterpret_cast<uint2 *>(bi + nn * AP + kk) =
+          make_uint2(pack_bf16x2(vb[u].x, vb[u].y), pack_bf16x2(vb[u].z, vb[u].w));
+    }
+  };
+
+  lstm_f32x16 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[g][e] = 0.f;
+  const int nk = H / kStepBK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * kStepBK);
+    const __bf16 *ai = lds + cur * (AIMG + BIMG), *bi = ai + AIMG;
+#pragma unroll
+    for (int ks = 0; ks < kStepBK / 16; ++ks) {
+      const lstm_bf16x8 a = *reinterpret_cast<const lstm_bf16x8 *>(
+          ai + (32 * mt + (lane & 31)) * AP + 16 * ks + 8 * (lane >> 5));
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const lstm_bf16x8 bv = *reinterpret_cast<const lstm_bf16x8 *>(
+            bi + (g * kStepUnits + 32 * ug + (lane & 31)) * AP + 16 * ks + 8 * (lane >> 5));
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue: C row (r&3) + 8 (r>>2) + 4 (lane>>5) of the wave's 32 rows, unit j = lane & 31
+  const int j = j0 + 32 * ug + (lane & 31);
+  float bh[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bh[g] = c.b_hh[d][g * H + j];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int64_t bb = r0 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+    if (bb >= c.b) continue;
+    float *g = c.g + (bb * W + t) * (8 * H) + d * (4 * H);
+    float pre[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pre[k] = (acc[k][e] + bh[k]) + g[k * H + j];  // gh.add_(igates)
+    const int64_t o = (bb * W + t) * (2 * H) + d * H + j;
+    const int64_t op = (bb * W + tp) * (2 * H) + d * H + j;
+    const float cp = c.c[op], hprev = c.y[op];
+    const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
+                og = sigmoidf_(pre[3]);
+    const float cn = fg * cp + ig * gg;  // (forgetgate * cx).add_(ingate * cellgate)
+    const float h = og * tanhf(cn);
+    g[j] = ig;
+    g[H + j] = fg;
+    g[2 * H + j] = gg;
+    g[3 * H + j] = og;
+    c.c[o] = cn;
+    c.y[o] = h;
+    c.hp[o] = hprev;
+    if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
+    else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
+  }
+}
+
 struct CellBwdArgs {
   float *g;            // gate activations in, dG out
   const float *c;
@@ -366,10 +492,18 @@ struct ppo_lstm_ctx {
   float *slabs;                      // [kSplits][total]
   float *row_part;                   // [rows][3]
   int maxw;
+  int fused_step;  // bf16 forward steps as lstm_step_fwd_kernel (ppo_lstm_fused_step)
   Timing tim;
 };
 
 namespace {
+
+// bf16 forward steps s > 0 as one recurrent-GEMM + cell launch (lstm_step_fwd_kernel);
+// PPO_LSTM_FUSED_STEP=0 keeps the layered GEMM + cell pair
+const int g_lstm_fused_step = [] {
+  const char *v = getenv("PPO_LSTM_FUSED_STEP");
+  return v ? atoi(v) : 1;
+}();
 
 struct TimingScope {
   explicit TimingScope(ppo_lstm_ctx *x) { g_tim = x->tim.on ? &x->tim : nullptr; }
@@ -475,7 +609,37 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st
       p[d].n = 4 * H;
     }
     if (int rc = gemm_fwd(x, p, 2, L.in, b * W, 4 * H, PPO_ACT_IDENTITY, false, st)) return rc;
+    const bool fused_step = x->prec == PPO_PREC_BF16 && x->fused_step && H % kStepUnits == 0;
     for (int s = 0; s < W; ++s) {
+      if (s > 0 && fused_step) {
+        StepArgs a{};
+        a.cell.g = x->g[z][l];
+        a.cell.b_hh[0] = P + L.b_hh[0];
+        a.cell.b_hh[1] = P + L.b_hh[1];
+        a.cell.c = x->c[z][l];
+        a.cell.y = x->y[z][l];
+        a.cell.hp = x->hp[z][l];
+        const bool top = l == N.layers - 1;
+        a.cell.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
+        a.cell.feat = z == 0 ? x->feat_a : x->feat_c;
+        a.cell.act = x->cfg.activation;
+        a.cell.b = b;
+        a.cell.w = W;
+        a.cell.h = H;
+        a.cell.s = s;
+        a.whh[0] = P + L.w_hh[0];
+        a.whh[1] = P + L.w_hh[1];
+        TimRec rec{KC_LSTM, "lstm_step_fwd_kernel", 0.0, 0.0};
+        if (tim_active()) {
+          rec.flops = 2.0 * 2 * b * 4.0 * H * H;
+          // W_hh and h_prev once, Gx / c_prev / h_prev in, gates / c / h / h_prev out (f32)
+          rec.bytes = 4.0 * (2 * 4.0 * H * H + 2.0 * b * H * (1 + 4 + 2 + 4 + 3));
+        }
+        launch_k(rec, lstm_step_fwd_kernel, dim3(ceil_div(b, kStepRows), H / kStepUnits, 2),
+                 dim3(256), 0, st, a);
+        PPO_LAUNCHED();
+        continue;
+      }
       if (s > 0) {
         GemmProblem q[2] = {};
         for (int d = 0; d < 2; ++d) {
@@ -731,6 +895,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   x->cfg = c;
   x->device = device;
   x->prec = PPO_PREC_F32;
+  x->fused_step = g_lstm_fused_step;
   const int H = c.latent, W = c.window, O = c.obs_dim, A = c.act_dim;
   int64_t off = 0;
   // LSTMActor.parameters(): feature_extractor, actor, actor_logstd (lstm_actor.py:12-38)
@@ -1028,4 +1193,11 @@ extern "C" int ppo_lstm_timing_kernel(ppo_lstm_ctx *x, int index, const char **n
                                       double *bytes) {
   PPO_REQUIRE(x != nullptr, "ppo_lstm_timing_kernel: null ctx");
   return timing_read_kernel(x->tim, index, name, kclass, total_ms, launches, flops, bytes);
+}
+
+extern "C" int ppo_lstm_fused_step(ppo_lstm_ctx *x, int enable) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_fused_step: null ctx");
+  if (enable < 0) return x->fused_step;
+  x->fused_step = enable != 0;
+  return 0;
 }

@@ -172,6 +172,13 @@ class LSTMEngine:
             ptr(rows), int(b), ptr(grad), ptr(loss), clip_lo, clip_hi, entropy_coef, inv_b,
             inv_ba, _stream(self.device)))
 
+    def fused_step(self, enable: Optional[bool] = None) -> bool:
+        """bf16 forward steps as one recurrent-GEMM + cell launch (ppo_lstm_fused_step); set it
+        with enable, return the current setting."""
+        if enable is not None:
+            check(self.lib.ppo_lstm_fused_step(self._ctx, int(bool(enable))))
+        return bool(self.lib.ppo_lstm_fused_step(self._ctx, -1))
+
     # ---- measurement (the Engine.timing* contract of bench.py) ----------------------------------
     def timing(self, enable: bool, capacity: int = 65536) -> None:
         check(self.lib.ppo_lstm_timing(self._ctx, int(enable), int(capacity)))

@@ -172,6 +172,32 @@ def test_minibatch_grad_deterministic_and_bf16_close(gpu):
         assert rel <= 6e-2, (i, rel)
 
 
+def test_fused_forward_step_bitwise_equals_layered(gpu):
+    """bf16 mode: the forward steps s > 0 as one lstm_step_fwd_kernel launch (recurrent projection
+    on MFMA, the cell in its epilogue) reproduce the layered projection GEMM + cell kernel bitwise
+    -- forward outputs and the whole minibatch gradient -- on the main.py network (latent 256,
+    W = 5); 200 rows, so the last 64-row block is partial."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    b = 200
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=24)
+    agent.engine.set_precision("bf16")
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    old_logp = torch.randn(b, generator=gen) - 10.0
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    out = {}
+    for fused in (False, True):
+        agent.engine.fused_step(fused)
+        assert agent.engine.fused_step() == fused
+        out[fused] = (_forward(agent, x), _grad(agent, x, actions, old_logp, adv, vt))
+    for k in out[True][0]:
+        assert torch.equal(out[True][0][k], out[False][0][k]), k
+    assert torch.equal(out[True][1][0], out[False][1][0])
+    assert torch.equal(out[True][1][1], out[False][1][1])
+
+
 @pytest.mark.parametrize("kw", [{"latent": 8, "window": 3, "hidden": (32, 32)},
                                 {"latent": 12, "window": 2, "hidden": (24, 16), "extractor_layers": 2,
                                  "activation": "tanh"}])

@@ -23,6 +23,7 @@
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
+#   abmodel   one model's line (MODEL) per environment setting (ABSETS="A=0,B=1 ...")
 #   abhum     Humanoid shard line per value of one env knob (ABVAR, ABVALS)
 #   cnnpmc    SQ counter passes over one pixel-CNN iteration (LDS-staged conv kernels)
 # usage: gpurun --timeout 1200 -- 'TAG=r02 STEPS="tests bench trace traffic" bash tools/gpu.sh'
@@ -96,17 +97,22 @@ for S in $STEPS; do
           cnn) A="--model cnn" ;;
           lstm) A="--model lstm" ;;
         esac
-        for C in FETCH_SIZE WRITE_SIZE; do
-          timeout -s KILL 300 rocprofv3 --pmc $C -d gpurun_out/rp_${TAG}_${L}_$C -o pmc --output-format csv \
-            -- python3 bench.py $BASE $A > gpurun_out/rp_${TAG}_${L}_$C.log 2>&1 \
-            || fail "traffic $L $C" gpurun_out/rp_${TAG}_${L}_$C.log
+        for C in ${COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
+          # the profiled run writes only to its log: a heartbeat on stdout keeps the call alive
+          timeout -s KILL 600 rocprofv3 --pmc $C -d gpurun_out/rp_${TAG}_${L}_$C -o pmc --output-format csv \
+            -- python3 bench.py $BASE $A > gpurun_out/rp_${TAG}_${L}_$C.log 2>&1 &
+          pid=$!
+          while kill -0 $pid 2>/dev/null; do sleep 20; echo "  $L $C running ($(date +%T))"; done
+          wait $pid || fail "traffic $L $C" gpurun_out/rp_${TAG}_${L}_$C.log
         done
-        python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_${L}_FETCH_SIZE -name "*counter_collection.csv") \
-          $(find gpurun_out/rp_${TAG}_${L}_WRITE_SIZE -name "*counter_collection.csv") gpurun_out/traffic_${TAG}_$L.json \
-          > /dev/null
-        outs="$outs gpurun_out/traffic_${TAG}_$L.json"
+        if [ -z "$COUNTERS" ]; then
+          python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_${L}_FETCH_SIZE -name "*counter_collection.csv") \
+            $(find gpurun_out/rp_${TAG}_${L}_WRITE_SIZE -name "*counter_collection.csv") gpurun_out/traffic_${TAG}_$L.json \
+            > /dev/null
+          outs="$outs gpurun_out/traffic_${TAG}_$L.json"
+        fi
       done
-      python tools/merge_traffic.py gpurun_out/trafficlegs_${TAG}.json $outs ;;
+      [ -n "$outs" ] && python tools/merge_traffic.py gpurun_out/trafficlegs_${TAG}.json $outs ;;
     pmc)
       i=0
       # one pass per space-separated word (at most 8 SQ_ counters each)
@@ -153,6 +159,17 @@ for S in $STEPS; do
           || fail abhum gpurun_out/bench_${TAG}_hum_$V.err
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['ms_per_step'])" \
           gpurun_out/bench_${TAG}_hum_$V.json
+      done ;;
+    abmodel)
+      # A/B of environment settings on one model's line: MODEL=lstm|cnn ABSETS="X=0,Y=1 X=1,Y=1 ..."
+      i=0
+      for SET in $ABSETS; do
+        i=$((i+1))
+        env ${SET//,/ } timeout -k 10 500 python bench.py --model ${MODEL:-lstm} --steps 3 --warmup 2 \
+          --no-cpu-baseline > gpurun_out/bench_${TAG}_ab$i.json 2> gpurun_out/bench_${TAG}_ab$i.err \
+          || fail "abmodel $SET" gpurun_out/bench_${TAG}_ab$i.err
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'])" \
+          gpurun_out/bench_${TAG}_ab$i.json "$SET"
       done ;;
     cnn)
       timeout -k 10 600 python bench.py --model cnn $CNN_ARGS > gpurun_out/bench_${TAG}_cnn.json \

@@ -38,7 +38,8 @@ def bench_key(key: str) -> str:
     'pixel_wgrad_kernel'), and the LDS-staged conv kernels named by layer
     ('conv::dgrad_lds_kernel<ppo::conv::DgGeo<32, 20, ...>>' -> 'dgrad_lds_kernel<L2>')."""
     head, sep, rest = key.partition("<")
-    head = head.split("::")[-1]
+    if head.split("::")[0] in ("conv", "lstm", "f4", "cnn", "wide", "fu"):  # the engine's namespaces
+        head = head.split("::")[-1]
     if head in ("fwd_lds_kernel", "dgrad_lds_kernel", "wgrad_lds_kernel", "dg_pack_kernel",
                 "fw_pack_kernel"):
         for sig, layer in _LAYER.items():
