@@ -89,6 +89,9 @@ struct DgStage {
 };
 
 typedef __bf16 dg_bf16x8 __attribute__((ext_vector_type(8)));
+// 16-B staging registers: a clang vector, not HIP's uint4 struct -- arrays of the struct were kept
+// in scratch memory (ScratchSize 48-128 B per lane) instead of registers
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 typedef float dg_f32x4 __attribute__((ext_vector_type(4)));
 
 template <class D>
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(512) void dgrad_lds_kernel(DgArgs q) {
 
   float pre[St::ITERS][D::DZCHW ? 1 : 4];
   uint4 prex[St::XITERS];
-  auto prefetch = [&](int img) {
+  auto prefetch = [&](int img) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < St::XITERS; ++i) {
       const int u = tid + i * 512;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(512) void dgrad_lds_kernel(DgArgs q) {
       }
     }
   };
-  auto stage = [&]() {
+  auto stage = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < St::XITERS; ++i) {
       const int u = tid + i * 512;
@@ -329,14 +332,14 @@ __global__ __launch_bounds__(512) void fwd_lds_kernel(FwArgs q) {
     for (int i = 0; i < 4; ++i) bias[j][i] = q.bias[z][co + 4 * g + i];
   }
 
-  uint4 pre[ITERS];
-  auto prefetch = [&](int img) {
+  u32x4_t pre[ITERS];
+  auto prefetch = [&](int img) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < ITERS; ++i) {
       const int u = tid + i * 512;
       const int uc = u < D::UNITS ? u : D::UNITS - 1;
       const int zz = uc / (D::UNITS / 2), w = uc - zz * (D::UNITS / 2);
-      pre[i] = *reinterpret_cast<const uint4 *>(q.xin[zz] + static_cast<int64_t>(img) * D::IMG + 8 * w);
+      pre[i] = *reinterpret_cast<const u32x4_t *>(q.xin[zz] + static_cast<int64_t>(img) * D::IMG + 8 * w);
     }
   };
   int img = blockIdx.x;
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(512) void fwd_lds_kernel(FwArgs q) {
       const int u = tid + i * 512;
       if (u < D::UNITS) {
         int zz;
-        *reinterpret_cast<uint4 *>(sx + fw_unit_slot<D>(u, zz)) = pre[i];
+        *reinterpret_cast<u32x4_t *>(sx + fw_unit_slot<D>(u, zz)) = pre[i];
       }
     }
     lds_barrier();
@@ -441,15 +444,15 @@ __global__ __launch_bounds__(512) void wgrad_lds_kernel(FwArgs q) {
   float crow = 0.f;                                                  // CHW: this thread's row
   const int cz = tid >> 8, cco = (tid >> 2) & 63, csub = tid & 3;
 
-  uint4 px[XITERS];
+  u32x4_t px[XITERS];
   float pd[DITERS][D::OUTCHW ? 1 : 4];
-  auto prefetch = [&](int img) {
+  auto prefetch = [&](int img) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < XITERS; ++i) {
       const int u = tid + i * 512;
       const int uc = u < D::UNITS ? u : D::UNITS - 1;
       const int zz = uc / (D::UNITS / 2), w = uc - zz * (D::UNITS / 2);
-      px[i] = *reinterpret_cast<const uint4 *>(q.xin[zz] + static_cast<int64_t>(img) * D::IMG + 8 * w);
+      px[i] = *reinterpret_cast<const u32x4_t *>(q.xin[zz] + static_cast<int64_t>(img) * D::IMG + 8 * w);
     }
 #pragma unroll
     for (int i = 0; i < DITERS; ++i) {
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(512) void wgrad_lds_kernel(FwArgs q) {
       const int u = tid + i * 512;
       if (u < D::UNITS) {
         int zz;
-        *reinterpret_cast<uint4 *>(sx + fw_unit_slot<D>(u, zz)) = px[i];
+        *reinterpret_cast<u32x4_t *>(sx + fw_unit_slot<D>(u, zz)) = px[i];
       }
     }
 #pragma unroll
@@ -494,7 +497,10 @@ __global__ __launch_bounds__(512) void wgrad_lds_kernel(FwArgs q) {
         if constexpr (!D::OUTCHW) {  // w = p * 16 + channel quad (= tid % 16)
           const int p = w >> 4, c4 = (w & 15) * 4;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) csum[zz][j] += pd[i][j];
+          for (int j = 0; j < 4; ++j) {  // zz is a run-time value: select, not index
+            csum[0][j] += zz == 0 ? pd[i][j] : 0.f;
+            csum[1][j] += zz == 0 ? 0.f : pd[i][j];
+          }
           *reinterpret_cast<uint2 *>(sd + zz * D::DZIMG + p * D::DZPITCH + c4) =
               make_uint2(pack_bf16x2(pd[i][0], pd[i][1]), pack_bf16x2(pd[i][2], pd[i][3]));
         }

@@ -78,7 +78,22 @@ __device__ __forceinline__ void pix_unit_load(const uint8_t *frame, int u, uint3
 // the bf16 staging multiplies instead of running the IEEE divide sequence per byte.
 constexpr float kInv255 = 1.f / 255.f;
 
+// the same units held in a clang vector (components x, y, z): arrays of these stay in registers
+// where arrays of uint32_t[3] were kept in scratch memory in pixel_wgrad_kernel
+typedef uint32_t pix_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pix_unit_load(const uint8_t *frame, int u, pix_u32x4 &w) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(frame) + 3 * u;
+  w.x = p[0];
+  w.y = p[1];
+  w.z = p[2];
+}
+
 // unit u = (y, bx) -> 12 bf16 at block (y / 4, bx), offset (y % 4) * 12
+__device__ __forceinline__ void pix_unit_store(__bf16 *s, int u, const uint32_t (&w)[3]);
+__device__ __forceinline__ void pix_unit_store(__bf16 *s, int u, const pix_u32x4 &v) {
+  const uint32_t w[3] = {v.x, v.y, v.z};
+  pix_unit_store(s, u, w);
+}
 __device__ __forceinline__ void pix_unit_store(__bf16 *s, int u, const uint32_t (&w)[3]) {
   const int y = u / kS2dSide, bx = u - y * kS2dSide;
   __bf16 *dst = s + ((y >> 2) * kS2dSide + bx) * kS2dPitch + (y & 3) * 12;
@@ -165,7 +180,7 @@ __global__ __launch_bounds__(kPixFwdThreads) void pixel_fwd_kernel(PixArgs q) {
   }
 
   uint32_t pre[kPixFwdUnits][3];
-  auto prefetch = [&](int img) {
+  auto prefetch = [&](int img) __attribute__((always_inline)) {
     const uint8_t *f = pix_frame(q, img);
 #pragma unroll
     for (int i = 0; i < kPixFwdUnits; ++i) {
@@ -275,8 +290,8 @@ __global__ __launch_bounds__(kPixWgThreads) void pixel_wgrad_kernel(PixArgs q) {
   float csum[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 
   float4 pd[kPixWgDzIters];
-  uint32_t pf[kPixWgFrIters][3];
-  auto prefetch = [&](int img) {
+  pix_u32x4 pf[kPixWgFrIters];
+  auto prefetch = [&](int img) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kPixWgDzIters; ++i) {
       const int e = tid + i * kPixWgThreads;
@@ -302,10 +317,17 @@ __global__ __launch_bounds__(kPixWgThreads) void pixel_wgrad_kernel(PixArgs q) {
         const int z = e / (kPixDzUnits / 2), w = e - z * (kPixDzUnits / 2);
         const int p = w >> 3, c4 = (w & 7) * 4;
         const float4 v = pd[i];
-        csum[z][0] += v.x;
-        csum[z][1] += v.y;
-        csum[z][2] += v.z;
-        csum[z][3] += v.w;
+        // z is a run-time value: select instead of indexing (an indexed csum lived in scratch);
+        // adding +0 to the other net's sums leaves them bitwise unchanged
+        const bool z0 = z == 0;
+        csum[0][0] += z0 ? v.x : 0.f;
+        csum[0][1] += z0 ? v.y : 0.f;
+        csum[0][2] += z0 ? v.z : 0.f;
+        csum[0][3] += z0 ? v.w : 0.f;
+        csum[1][0] += z0 ? 0.f : v.x;
+        csum[1][1] += z0 ? 0.f : v.y;
+        csum[1][2] += z0 ? 0.f : v.z;
+        csum[1][3] += z0 ? 0.f : v.w;
         *reinterpret_cast<uint2 *>(dzs + (z * kPixPosPad + p) * kPixDzPitch + c4) =
             make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
       }
@@ -330,14 +352,13 @@ __global__ __launch_bounds__(kPixWgThreads) void pixel_wgrad_kernel(PixArgs q) {
       // S rows of positions >= 400 (zero dz) read a valid block
       const int blo = pix_block(plo < L1::P ? plo : L1::P - 1) * kS2dPitch;
       const int bhi = pix_block(phi < L1::P ? phi : L1::P - 1) * kS2dPitch;
-      bf16x8_t b[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) b[j] = pix_tr_pair(fs + blo + scol[j], fs + bhi + scol[j]);
+      for (int j = 0; j < 3; ++j) {  // one B fragment at a time (an array of them sat in scratch)
+        const bf16x8_t b = pix_tr_pair(fs + blo + scol[j], fs + bhi + scol[j]);
 #pragma unroll
-      for (int z = 0; z < 2; ++z)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          acc[z][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[z], b[j], acc[z][j], 0, 0, 0);
+        for (int z = 0; z < 2; ++z)
+          acc[z][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[z], b, acc[z][j], 0, 0, 0);
+      }
     }
   }
   __syncthreads();  // LDS free for the folds

@@ -87,7 +87,7 @@ for S in $STEPS; do
     trafficlegs)
       # FETCH_SIZE / WRITE_SIZE passes per workload (LEGS="main ant hum cnn lstm"), one process each,
       # merged into gpurun_out/trafficlegs_${TAG}.json (copy it to bench_traffic.json)
-      BASE="--steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs"
+      BASE="--steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-legs --no-graphs"  # rocprofv3 --pmc crashed in hipGraph replay
       outs=""
       for L in ${LEGS:-main ant hum lstm cnn}; do
         case $L in
