@@ -268,6 +268,12 @@ struct CellBwdArgs {
   int b, w, h, s;
 };
 
+// float4 in and out as clang vectors (element access by constant index keeps them in registers;
+// local float[4] arrays of the first float4 form were kept in scratch)
+typedef float lstm_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ lstm_f4 ld4(const float *p) { return *reinterpret_cast<const lstm_f4 *>(p); }
+__device__ __forceinline__ void st4(float *p, lstm_f4 v) { *reinterpret_cast<lstm_f4 *>(p) = v; }
+
 __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int H = q.h, W = q.w, H4 = H / 4;
@@ -280,46 +286,38 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
   const int tp = d == 0 ? t - 1 : t + 1;
   const int64_t o = (b * W + t) * (2 * H) + d * H + j;
   const int64_t r = b * (2 * H) + d * H + j;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 dh4 = z4;
-  if (q.dy_mode == 1) dh4 = *reinterpret_cast<const float4 *>(q.dy + o);
-  else if (t == W - 1) dh4 = *reinterpret_cast<const float4 *>(q.dy_last + r);
-  const float4 dr4 = q.s > 0 ? *reinterpret_cast<const float4 *>(q.dh_rec + r) : z4;
-  const float4 dc4 = q.s > 0 ? *reinterpret_cast<const float4 *>(q.dcarry + r) : z4;
+  const lstm_f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  lstm_f4 dh4 = z4;
+  if (q.dy_mode == 1) dh4 = ld4(q.dy + o);
+  else if (t == W - 1) dh4 = ld4(q.dy_last + r);
+  const lstm_f4 dr4 = q.s > 0 ? ld4(q.dh_rec + r) : z4;
+  const lstm_f4 dc4 = q.s > 0 ? ld4(q.dcarry + r) : z4;
   float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
-  const float4 ig4 = *reinterpret_cast<const float4 *>(g + j);
-  const float4 fg4 = *reinterpret_cast<const float4 *>(g + H + j);
-  const float4 gg4 = *reinterpret_cast<const float4 *>(g + 2 * H + j);
-  const float4 og4 = *reinterpret_cast<const float4 *>(g + 3 * H + j);
-  const float4 c4 = *reinterpret_cast<const float4 *>(q.c + o);
-  const float4 cp4 = first_fwd ? z4 : *reinterpret_cast<const float4 *>(q.c + (b * W + tp) * (2 * H) + d * H + j);
-  const float dhv[4] = {dh4.x, dh4.y, dh4.z, dh4.w}, drv[4] = {dr4.x, dr4.y, dr4.z, dr4.w};
-  const float dcv[4] = {dc4.x, dc4.y, dc4.z, dc4.w};
-  const float igv[4] = {ig4.x, ig4.y, ig4.z, ig4.w}, fgv[4] = {fg4.x, fg4.y, fg4.z, fg4.w};
-  const float ggv[4] = {gg4.x, gg4.y, gg4.z, gg4.w}, ogv[4] = {og4.x, og4.y, og4.z, og4.w};
-  const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, cpv[4] = {cp4.x, cp4.y, cp4.z, cp4.w};
-  float carry[4], di[4], df[4], dg[4], dout[4];
+  const lstm_f4 ig = ld4(g + j), fg = ld4(g + H + j), gg = ld4(g + 2 * H + j), og = ld4(g + 3 * H + j);
+  const lstm_f4 c4 = ld4(q.c + o);
+  const lstm_f4 cp4 = first_fwd ? z4 : ld4(q.c + (b * W + tp) * (2 * H) + d * H + j);
+  lstm_f4 carry, di, df, dg, dout;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    float dh = dhv[e];
-    if (q.s > 0) dh += drv[e];
-    const float dc_in = q.s > 0 ? dcv[e] : 0.f;
-    const float tc = tanhf(cv[e]);
+    float dh = dh4[e];
+    if (q.s > 0) dh += dr4[e];
+    const float dc_in = q.s > 0 ? dc4[e] : 0.f;
+    const float tc = tanhf(c4[e]);
     const float d_o = dh * tc;                          // hy = outgate * cy.tanh()
-    const float d_tc = dh * ogv[e];
+    const float d_tc = dh * og[e];
     const float dc = d_tc * (1.f - tc * tc) + dc_in;    // tanh_backward, + the next step's dcx
-    const float d_f = dc * cpv[e], d_i = dc * ggv[e], d_g = dc * igv[e];
-    carry[e] = dc * fgv[e];
-    di[e] = (d_i * (1.f - igv[e])) * igv[e];            // sigmoid_backward: g * (1 - y) * y
-    df[e] = (d_f * (1.f - fgv[e])) * fgv[e];
-    dg[e] = d_g * (1.f - ggv[e] * ggv[e]);              // tanh_backward
-    dout[e] = (d_o * (1.f - ogv[e])) * ogv[e];
+    const float d_f = dc * cp4[e], d_i = dc * gg[e], d_g = dc * ig[e];
+    carry[e] = dc * fg[e];
+    di[e] = (d_i * (1.f - ig[e])) * ig[e];              // sigmoid_backward: g * (1 - y) * y
+    df[e] = (d_f * (1.f - fg[e])) * fg[e];
+    dg[e] = d_g * (1.f - gg[e] * gg[e]);                // tanh_backward
+    dout[e] = (d_o * (1.f - og[e])) * og[e];
   }
-  *reinterpret_cast<float4 *>(q.dcarry + r) = make_float4(carry[0], carry[1], carry[2], carry[3]);
-  *reinterpret_cast<float4 *>(g + j) = make_float4(di[0], di[1], di[2], di[3]);
-  *reinterpret_cast<float4 *>(g + H + j) = make_float4(df[0], df[1], df[2], df[3]);
-  *reinterpret_cast<float4 *>(g + 2 * H + j) = make_float4(dg[0], dg[1], dg[2], dg[3]);
-  *reinterpret_cast<float4 *>(g + 3 * H + j) = make_float4(dout[0], dout[1], dout[2], dout[3]);
+  st4(q.dcarry + r, carry);
+  st4(g + j, di);
+  st4(g + H + j, df);
+  st4(g + 2 * H + j, dg);
+  st4(g + 3 * H + j, dout);
 }
 
 __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) {
