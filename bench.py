@@ -115,13 +115,26 @@ def apply_model_defaults(args, default_of) -> None:
         args.window = 1
 
 
-def load_traffic(path):
-    """{kernel name: HBM bytes per launch} from a PMC pass over this same command
-    (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or {}."""
+def load_traffic(path, workload=None):
+    """{kernel name: HBM bytes per launch} from PMC passes over the same workload
+    (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or {}.  The table
+    holds one sub-table per workload (tools/merge_traffic.py): the headline's at the top level and
+    each leg's under by_workload[name] -- the layered GEMM instantiations are shared by the pixel
+    and BiLSTM heads with different shapes, so a leg only ever reads its own workload's bytes."""
     if not path or not os.path.exists(path):
         return {}
     with open(path) as f:
-        return json.load(f).get("bytes_per_launch", {})
+        t = json.load(f)
+    if workload is None:
+        return t.get("bytes_per_launch", {})
+    return t.get("by_workload", {}).get(workload, {})
+
+
+def traffic_workload(args):
+    """The traffic sub-table of a run: None for the headline, else the config leg it measures."""
+    if args.model in ("cnn", "lstm"):
+        return args.model
+    return {(27, 8): "ant", (376, 17): "humanoid"}.get((args.obs_dim, args.act_dim))
 
 
 # gymnasium observation / action sizes of the BASELINE configs (SURVEY.md s8 notation)
@@ -500,7 +513,8 @@ def config_leg(args, name, dev, steps=None, **over) -> dict:
                          "peak": PEAK_BF16_MFMA_TFLOPS, "frac": e2e / PEAK_BF16_MFMA_TFLOPS}
     if kernels:
         kname, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])
-        out["roofline"] = roofline(kname, c, load_traffic(args.traffic))
+        # a leg run with overridden shapes has no table of its own (traffic null)
+        out["roofline"] = roofline(kname, c, load_traffic(args.traffic, name if not over else f"{name}*"))
         out["kernels_ms_per_step"] = {k: round(v["ms"], 4) for k, v in
                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:8]}
     else:
@@ -600,7 +614,7 @@ def main():
                                        else "dp1 rehearsal (the data-parallel step sequence, "
                                             "no peer: PPO_DP_REHEARSE=1)")}}
     if kernels:
-        traffic = load_traffic(args.traffic)
+        traffic = load_traffic(args.traffic, traffic_workload(args))
         name, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])
         line["roofline"] = roofline(name, c, traffic)
         gae = {k: v for k, v in kernels.items() if v["class"] == "gae"}

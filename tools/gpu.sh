@@ -95,7 +95,7 @@ for S in $STEPS; do
           ant) A="--num-envs 4096 --obs-dim 27 --act-dim 8" ;;
           hum) A="--num-envs 1024 --obs-dim 376 --act-dim 17 --hidden 512,512,512 --batch 8192" ;;
           cnn) A="--model cnn" ;;
-          lstm) A="--model lstm" ;;
+          lstm) A="--model lstm ${LSTM_TRAFFIC_ARGS}" ;;  # e.g. --epochs 1: same per-launch shapes, fewer dispatches
         esac
         for C in ${COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
           # the profiled run writes only to its log: a heartbeat on stdout keeps the call alive
@@ -109,7 +109,7 @@ for S in $STEPS; do
           python tools/pmc_traffic.py $(find gpurun_out/rp_${TAG}_${L}_FETCH_SIZE -name "*counter_collection.csv") \
             $(find gpurun_out/rp_${TAG}_${L}_WRITE_SIZE -name "*counter_collection.csv") gpurun_out/traffic_${TAG}_$L.json \
             > /dev/null
-          outs="$outs gpurun_out/traffic_${TAG}_$L.json"
+          outs="$outs $( [ $L = hum ] && echo humanoid || echo $L )=gpurun_out/traffic_${TAG}_$L.json"
         fi
       done
       [ -n "$outs" ] && python tools/merge_traffic.py gpurun_out/trafficlegs_${TAG}.json $outs ;;
