@@ -225,35 +225,52 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
     cur ^= 1;
   }
 
-  // epilogue: C row (r&3) + 8 (r>>2) + 4 (lane>>5) of the wave's 32 rows, unit j = lane & 31
+  // epilogue: C row (r&3) + 8 (r>>2) + 4 (lane>>5) of the wave's 32 rows, unit j = lane & 31.
+  // Eight rows at a time, every load first and unconditional (rows past b read row b-1): a load
+  // behind the row test made each row wait a memory round trip of its own.
   const int j = j0 + 32 * ug + (lane & 31);
   float bh[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bh[g] = c.b_hh[d][g * H + j];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int64_t bb = r0 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-    if (bb >= c.b) continue;
-    float *g = c.g + (bb * W + t) * (8 * H) + d * (4 * H);
-    float pre[4];
+  for (int e0 = 0; e0 < 16; e0 += 8) {
+    float gx[8][4], cpv[8], hpv[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pre[k] = (acc[k][e] + bh[k]) + g[k * H + j];  // gh.add_(igates)
-    const int64_t o = (bb * W + t) * (2 * H) + d * H + j;
-    const int64_t op = (bb * W + tp) * (2 * H) + d * H + j;
-    const float cp = c.c[op], hprev = c.y[op];
-    const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
-                og = sigmoidf_(pre[3]);
-    const float cn = fg * cp + ig * gg;  // (forgetgate * cx).add_(ingate * cellgate)
-    const float h = og * tanhf(cn);
-    g[j] = ig;
-    g[H + j] = fg;
-    g[2 * H + j] = gg;
-    g[3 * H + j] = og;
-    c.c[o] = cn;
-    c.y[o] = h;
-    c.hp[o] = hprev;
-    if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
-    else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u;
+      const int64_t bb = r0 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int64_t bc = bb < c.b ? bb : c.b - 1;
+      const float *g = c.g + (bc * W + t) * (8 * H) + d * (4 * H);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gx[u][k] = g[k * H + j];
+      const int64_t op = (bc * W + tp) * (2 * H) + d * H + j;
+      cpv[u] = c.c[op];
+      hpv[u] = c.y[op];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u;
+      const int64_t bb = r0 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      if (bb >= c.b) continue;
+      float *g = c.g + (bb * W + t) * (8 * H) + d * (4 * H);
+      float pre[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pre[k] = (acc[k][e] + bh[k]) + gx[u][k];  // gh.add_(igates)
+      const int64_t o = (bb * W + t) * (2 * H) + d * H + j;
+      const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
+                  og = sigmoidf_(pre[3]);
+      const float cn = fg * cpv[u] + ig * gg;  // (forgetgate * cx).add_(ingate * cellgate)
+      const float h = og * tanhf(cn);
+      g[j] = ig;
+      g[H + j] = fg;
+      g[2 * H + j] = gg;
+      g[3 * H + j] = og;
+      c.c[o] = cn;
+      c.y[o] = h;
+      c.hp[o] = hpv[u];
+      if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
+      else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
+    }
   }
 }
 
