@@ -132,6 +132,12 @@ int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
  * (one wave per SIMD, 128-row chunks).  Default PPO_FUSED4 (1 -> 4, else 8);
  * variant < 0 queries.  The two agree to f32 rounding; each is bitwise deterministic. */
 int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant);
+/* How the 8-wave fused update reads the staged records (ppo_stage_records /
+ * ppo_gae_stage_records) of a minibatch: 1 (default, PPO_FUSED_DIRECT) = each row's 128-B record
+ * through the row indices, one chunk ahead, inside the fused launch (the step tail gathers
+ * nothing); 0 = the gathered copy written by the prep kernel or the previous step tail.  Bitwise
+ * the same results; enable < 0 queries. */
+int ppo_ctx_fused_direct(ppo_ctx *ctx, int enable);
 /* GEMM precision of every fc-layer GEMM the ctx launches (rollout forward, update forward,
  * dgrad, wgrad): PPO_PREC_F32 (default; parity with the f32 reference) or PPO_PREC_BF16 (bf16
  * operands on v_mfma_f32_32x32x16_bf16, f32 accumulation, f32 activations / params / Adam in

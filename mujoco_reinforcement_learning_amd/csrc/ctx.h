@@ -59,6 +59,7 @@ struct ppo_ctx {
   uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
   int fstamp_on, fstamp_g;
   int fused4;                   // ppo_ctx_fused_variant: 1 -> fused_update4_kernel (ReLU)
+  int fdirect;                  // ppo_ctx_fused_direct: the 8-wave kernel reads staged records via rows
   ppo::WideWork *wide;          // wide bf16-resident layered path (wide_path.h), or null
   ppo::Timing tim;
 };

@@ -102,6 +102,9 @@ struct FusedArgs {
   // per row instead of reading the five storage arrays
   const uint4 *rec;
   int64_t n_rec;
+  // direct (rec set, 8-wave kernel): the fused kernel reads each row's record through rows[]
+  // itself, one chunk ahead -- no gathered xb / srow copy is written or read
+  bool direct;
   bool pack_w;                 // prep also refreshes the bf16 weight images from the masters
   int b, din, act_dim, act, hidden;
   float omv, clip_lo, clip_hi, ent_coef, inv_b, inv_ba;

@@ -433,6 +433,35 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   const int nchunks = (q.b + R - 1) / R;
   const int count = q.rows_n ? *q.rows_n : q.b;
 
+  // Row staging: thread -> 8-B unit tid & 7 of row slot tid >> 3 of a chunk, in the row's state
+  // half (the X image: issued a chunk ahead, at phase 6a) or its scalar half (actions, old
+  // log-prob, advantage, value target: issued at phase 0 for the head phase).  Direct mode reads
+  // the row's 128-B record through rows[] -- the index loaded at the previous phase 0 -- otherwise
+  // the gathered xb / srow copies.  Loads come from clamped addresses and are masked
+  // where they are stored (slots >= b or >= count, out-of-range rows: zero, as the prep gather
+  // writes them).  One uniform address form: base + row * pitch + 8 (tid & 7) + (scalars ? hi : 0).
+  const char *const rbase = q.direct ? reinterpret_cast<const char *>(q.rec)
+                                     : reinterpret_cast<const char *>(q.xb);
+  const int rshift = q.direct ? 7 : 6;  // 128-B records, 64-B xb / srow rows
+  const int64_t rhi = q.direct ? 64
+                               : reinterpret_cast<const char *>(q.srow) - reinterpret_cast<const char *>(q.xb);
+  const int rlast = static_cast<int>(min(q.n_rec, static_cast<int64_t>(INT32_MAX)) - 1);
+  auto row_index = [&](int c) -> int {
+    const int j = min(c * R + (tid0 >> 3), q.b - 1);
+    return *gptr(q.rows + j);
+  };
+  auto row_ok = [&](int c, int sr, int t) -> bool {
+    const int j = c * R + (t >> 3);
+    return j < q.b && j < count && (!q.direct || (sr >= 0 && sr <= rlast));
+  };
+  auto load_half = [&](int c, int sr, int t, bool scalars) -> uint64_t {
+    const int j = c * R + (t >> 3);
+    const int row = q.direct ? min(max(sr, 0), rlast) : min(j, q.b - 1);
+    const int64_t off = (static_cast<int64_t>(row) << rshift) + 8 * (t & 7) + (scalars ? rhi : 0);
+    return *gptr(reinterpret_cast<const uint64_t *>(rbase + off));
+  };
+  const int i_first = row_index(blockIdx.x);
+
   uint64_t t_body0 = 0, t_real0 = 0;
   if constexpr (STAMP) {
     t_body0 = __builtin_amdgcn_s_memtime();
@@ -465,6 +494,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     }
   }
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
+  uint64_t xpre = load_half(blockIdx.x, i_first, tid0, false);
+  bool xok = row_ok(blockIdx.x, i_first, tid0);
   __syncthreads();
 
   // ---- persistent accumulators ----
@@ -484,15 +515,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   float gb1 = 0.f, gb0 = 0.f;                 // rs16-scattered bias grads (feature rs16_feature)
   float g_bh = 0.f, g_ls = 0.f, g_loss = 0.f;  // head (lane & 15) partials
 
-  // X staging: thread -> 8 B (row tid>>3, unit tid&7) of the chunk's bf16 states
-  auto load_x = [&](int c) -> uint2 {
-    const int j = c * R + (tid0 >> 3);
-    if (c < nchunks && j < q.b)
-      return *reinterpret_cast<const uint2 *>(q.xb + static_cast<int64_t>(j) * kFusedKX + 4 * (tid0 & 7));
-    return make_uint2(0u, 0u);
-  };
   int chunk = blockIdx.x;
-  uint2 xpre = load_x(chunk);
+  int icur = i_first;  // this chunk's row index (thread's slot)
   uint64_t t_prev = 0, t_acc[kStampSlots];
   if constexpr (STAMP) {
 #pragma unroll
@@ -510,14 +534,14 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 
   bf16x8 ring[PD + 1];
   for (; chunk < nchunks; chunk += G) {
-    // ---- phase 0: X image; W0 fragments; the chunk's row scalars (actions, old log-prob,
-    //      advantage, value target: 64 x 64 B) issued for the head phase, staged at phase 2's end
+    // ---- phase 0: the chunk's rows (loaded during the previous chunk) -> X image and the row
+    //      scalars (actions, old log-prob, advantage, value target: 64 x 64 B); W0 fragments;
+    //      the next chunk's row indices ----
     OPAQUE_LANE();
-    *reinterpret_cast<uint2 *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xpre;
-    const int srow_j = chunk * R + (tid >> 3);
-    const uint2 srow_v = srow_j < q.b
-        ? *reinterpret_cast<const uint2 *>(q.srow + static_cast<int64_t>(srow_j) * kFusedSP + 2 * (tid & 7))
-        : make_uint2(0u, 0u);
+    *reinterpret_cast<uint64_t *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xok ? xpre : 0;
+    const bool sok = xok;
+    const uint64_t srow_v = load_half(chunk, icur, tid, true);
+    const int inext = row_index(chunk + G);  // lands by phase 6a
     bf16x8 w0f[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -569,10 +593,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
-    *reinterpret_cast<uint2 *>(lds + L::SROW + tid0 * 8) = srow_v;  // landed during phases 1-2
+    *reinterpret_cast<uint64_t *>(lds + L::SROW + tid0 * 8) = sok ? srow_v : 0;  // landed during phases 1-2
     STAMP_AT(2);
 
-    // ---- phase 3: bias + act -> a2 region; the head phase's row scalars issued here ----
+    // ---- phase 3: bias + act -> a2 region ----
     OPAQUE_LANE();
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -759,7 +783,10 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     // this LDS-only phase.
     OPAQUE_LANE();
     wring_prime<H>(w_frag_base<H>(N.w1bt, w, lane), ring);
-    xpre = load_x(chunk + G);  // next chunk's states: in flight until the next phase 0
+    // the next chunk's states: in flight until the next phase 0
+    xpre = load_half(chunk + G, inext, tid, false);
+    xok = row_ok(chunk + G, inext, tid);
+    icur = inext;
 #pragma unroll 1
     for (int ks = 0; ks < R / 16; ++ks) {
       bf16x8 af[2];
@@ -1039,6 +1066,8 @@ int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   PPO_REQUIRE(q.G >= 1 && q.G <= kFusedMaxWG, "fused update: bad workgroup count %d", q.G);
   PPO_REQUIRE(q.act_dim >= 1 && q.act_dim <= kFusedMaxAct, "fused update: act_dim %d", q.act_dim);
   PPO_REQUIRE(!q.stamps || q.act == PPO_ACT_RELU, "fused update: phase stamps only for ReLU");
+  PPO_REQUIRE(q.rows && q.b > 0 && (!q.direct || (q.rec && q.n_rec > 0)),
+              "fused update: rows / records missing (b=%d, direct=%d)", q.b, int(q.direct));
   if (q.act == PPO_ACT_RELU) launch_act<PPO_ACT_RELU>(q, rec, st);
   else if (q.act == PPO_ACT_TANH) launch_act<PPO_ACT_TANH>(q, rec, st);
   else launch_act<PPO_ACT_ELU>(q, rec, st);

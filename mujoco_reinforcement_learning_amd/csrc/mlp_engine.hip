@@ -690,6 +690,10 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
 static const int g_fused_enabled = env_knob("PPO_FUSED", 1);
 // PPO_FUSED4=1: the 4-wave / 128-row fused update (fused_update4.hip) for ReLU nets
 static const int g_fused4 = env_knob("PPO_FUSED4", 0);
+// PPO_FUSED_DIRECT=0: the 8-wave fused update reads the gathered xb / srow copies (written by the
+// prep kernel or the previous step tail) instead of the staged records through the row indices
+// (the ctx default; ppo_ctx_fused_direct switches it)
+static const int g_fused_direct = env_knob("PPO_FUSED_DIRECT", 1);
 
 // Pointers of both nets for the fused kernels (bf16 images from ctx->fw, f32 masters in params).
 static void fused_nets(const ppo_ctx *ctx, FusedNet (&out)[2]) {
@@ -760,6 +764,7 @@ static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *ac
   // the 4-wave kernel when selected (its phase-stamp build covers act_dim 5-6 only)
   q.v4 = ctx->fused4 && fused_update4_ok(q) && (!q.stamps || (q.act_dim > 4 && q.act_dim <= 6));
   q.G = std::min(kFusedMaxWG, ceil_div(b, q.v4 ? kFused4Rows : kFusedRows));
+  q.direct = staged && !q.v4 && ctx->fdirect;
   return q;
 }
 
@@ -848,9 +853,9 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   const FusedArgs q = fused_args(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d,
                                  b, count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
                                  staged, pack_w);
-  if (!gathered || pack_w) {
+  if ((!gathered && !q.direct) || pack_w) {
     FusedArgs p = q;
-    p.b = gathered ? 0 : b;
+    p.b = (gathered || q.direct) ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
   }
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
@@ -1053,6 +1058,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       ctx->floss = reinterpret_cast<float *>(c);
       c += kFusedMaxWG * 2 * 4;
       ctx->fused4 = g_fused4 != 0;
+      ctx->fdirect = g_fused_direct != 0;
     }
   }
   *out = ctx;
@@ -1330,14 +1336,18 @@ extern "C" int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, 
   t.n_rec = ctx->frec_rows;
   t.xb = ctx->fxb;
   t.srow = ctx->fsrow;
-  t.b = next_b;
+  // direct: the next fused launch reads its rows through the indices, nothing to gather
+  const bool direct = next_b > 0 && fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                               next_rows_d, next_b, nullptr, 0.f, 0.f, 0.f, 0.f,
+                                               0.f, true, false).direct;
+  t.b = direct ? 0 : next_b;
   t.reduce = false;
   ReduceArgs r{};
   r.total = ctx->total_params;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_ADAM, "step_tail_kernel", 0.0,
                    28.0 * P + 2.0 * 2.0 * H * (t.a.din + 2.0 * H) +
-                       static_cast<double>(next_b) * (4.0 + 2.0 * kRecordBytes)};
+                       static_cast<double>(t.b) * (4.0 + 2.0 * kRecordBytes)};
   return step_tail_launch(r, t, rec, as_stream(stream));
 }
 
@@ -1394,9 +1404,9 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   const bool current = flags & PPO_STAGED_WEIGHTS_CURRENT;
   FusedArgs q = fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b, nullptr,
                            clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, true, !current);
-  if (!gathered || !current) {
+  if ((!gathered && !q.direct) || !current) {
     FusedArgs p = q;
-    p.b = gathered ? 0 : b;
+    p.b = (gathered || q.direct) ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
   }
   // tail: slab reduction + Adam + weight images, and the next minibatch's row gather
@@ -1409,13 +1419,13 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.n_rec = ctx->frec_rows;
   t.xb = ctx->fxb;
   t.srow = ctx->fsrow;
-  t.b = next_b;
+  t.b = q.direct ? 0 : next_b;  // direct: the next fused launch reads its rows itself
   t.reduce = true;
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
                    4.0 * (q.G + 1.0) * P + 24.0 * P + 2.0 * 2.0 * H * (q.din + 2.0 * H) +
-                       static_cast<double>(next_b) * (4.0 + 2.0 * kRecordBytes)};
+                       static_cast<double>(t.b) * (4.0 + 2.0 * kRecordBytes)};
   return step_tail_launch(r, t, rec, st);
 }
 
@@ -1798,6 +1808,13 @@ extern "C" int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant) {
   if (variant < 0) return ctx->fused4 ? 4 : 8;
   PPO_REQUIRE(variant == 4 || variant == 8, "ppo_ctx_fused_variant: variant %d (4 or 8)", variant);
   ctx->fused4 = variant == 4;
+  return 0;
+}
+
+extern "C" int ppo_ctx_fused_direct(ppo_ctx *ctx, int enable) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_direct: null ctx");
+  if (enable < 0) return ctx->fdirect ? 1 : 0;
+  ctx->fdirect = enable != 0;
   return 0;
 }
 

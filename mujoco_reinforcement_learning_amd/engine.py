@@ -215,6 +215,13 @@ class Engine:
             check(self.lib.ppo_ctx_fused_variant(self._ctx, int(variant)))
         return int(self.lib.ppo_ctx_fused_variant(self._ctx, -1))
 
+    def fused_direct(self, enable: Optional[bool] = None) -> bool:
+        """ppo_ctx_fused_direct: the 8-wave fused kernel reads the staged records through the row
+        indices itself (True, default) or the gathered copy (False); returns the current mode."""
+        if enable is not None:
+            check(self.lib.ppo_ctx_fused_direct(self._ctx, int(bool(enable))))
+        return bool(self.lib.ppo_ctx_fused_direct(self._ctx, -1))
+
     # ---- measurement ---------------------------------------------------------------------
     def timing(self, enable: bool, capacity: int = 65536) -> None:
         """Record a HIP event pair around every kernel this context launches (live roofline)."""

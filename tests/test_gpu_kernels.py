@@ -775,3 +775,57 @@ def test_update_step_staged_matches_grad_plus_adam_pack(gpu):
         for name, x, y in zip(("grad", "loss", "params", "m", "v"), outs["separate"], outs[mode]):
             assert torch.equal(x, y), (mode, name, int((x != y).sum()))
     assert not torch.equal(outs["separate"][2], p0)
+
+
+@pytest.mark.parametrize("with_count", [False, True])
+def test_fused_direct_records_match_gathered_copy(gpu, with_count):
+    """ppo_ctx_fused_direct: the 8-wave fused kernel reading each row's staged record through the
+    row indices (default) gives the gradient, losses and Adam state of the gathered-copy path bit
+    for bit -- two chained ppo_update_step_staged steps (the second with rows_gathered, i.e. the
+    rows the first step's tail gathered in copy mode) and ppo_minibatch_grad_staged with a device
+    row count; minibatch sizes that are not a multiple of the 64-row chunk, and out-of-range rows
+    (masked to zero as the prep gather does)."""
+    n, t, b = 512, 16, 2000
+    run, eng, ref, cfg = _agents(gpu, 14, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    assert e.fused and e.fused_direct()
+    g = torch.Generator().manual_seed(6)
+    rows_total = n * t
+    states = torch.randn(t + 1, n, 17, generator=g).to(gpu)
+    actions = torch.randn(t, n, 6, generator=g).to(gpu)
+    old_lp = torch.randn(t, n, generator=g).to(gpu) - 5
+    adv = torch.randn(t, n, generator=g).to(gpu)
+    vt = torch.randn(t, n, generator=g).to(gpu)
+    rows = [torch.randperm(rows_total, generator=g)[:b].to(torch.int32) for _ in range(2)]
+    rows[1][7] = rows_total + 5  # out of range: a zero row in both modes
+    rows = [r.to(gpu) for r in rows]
+    count = torch.tensor([b - 333], dtype=torch.int32, device=gpu) if with_count else None
+    args = (0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    hyper = dict(one_minus_beta1=0.1, beta2=0.999, one_minus_beta2=0.001, eps=1e-8)
+    p0 = eng.flat_params.clone()
+    m0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-3
+    v0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-6
+    e.stage_records(states, actions, old_lp, adv, vt)
+    outs = {}
+    for direct in (True, False):
+        e.fused_direct(direct)
+        assert e.fused_direct() == direct
+        eng.flat_params.copy_(p0)
+        m, v = m0.clone(), v0.clone()
+        e.pack_weights()
+        res = []
+        for k in range(2):
+            grad, loss = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+            e.update_step_staged(rows[k], b, grad, loss, m, v, *args, neg_step_actor=-1e-3,
+                                 neg_step_critic=-2e-3, bc2_sqrt=0.3,
+                                 next_rows=rows[1] if k == 0 else None,
+                                 weights_current=k > 0, rows_gathered=k > 0, **hyper)
+            res += [grad.clone(), loss.clone()]
+        gc, lc = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+        e.minibatch_grad_staged(rows[1], b, gc, lc, *args, count=count, weights_current=True)
+        torch.cuda.synchronize()
+        outs[direct] = res + [gc, lc, eng.flat_params.clone(), m, v]
+    e.fused_direct(True)
+    for i, (x, y) in enumerate(zip(outs[True], outs[False])):
+        assert torch.equal(x, y), (i, int((x != y).sum()))

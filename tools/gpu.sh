@@ -160,6 +160,17 @@ for S in $STEPS; do
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['ms_per_step'])" \
           gpurun_out/bench_${TAG}_hum_$V.json
       done ;;
+    abmain)
+      # A/B of environment settings on the headline line (no legs): ABSETS="X=0,Y=1 X=1,Y=1 ..."
+      i=0
+      for SET in $ABSETS; do
+        i=$((i+1))
+        env ${SET//,/ } timeout -k 10 300 python bench.py --no-legs --no-cpu-baseline $BENCH_ARGS \
+          > gpurun_out/bench_${TAG}_m$i.json 2> gpurun_out/bench_${TAG}_m$i.err \
+          || fail "abmain $SET" gpurun_out/bench_${TAG}_m$i.err
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d.get('kernels_ms_per_step',{}); print(sys.argv[2], d['value'], d['ms_per_step'], {n: round(v, 4) for n, v in k.items() if v > 0.1})" \
+          gpurun_out/bench_${TAG}_m$i.json "$SET"
+      done ;;
     abmodel)
       # A/B of environment settings on one model's line: MODEL=lstm|cnn ABSETS="X=0,Y=1 X=1,Y=1 ..."
       i=0
