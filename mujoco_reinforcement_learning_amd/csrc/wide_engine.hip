@@ -320,6 +320,10 @@ int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
     for (int l = 0; l <= nd.n_hidden; ++l) {
       const LayerDesc &L = nd.layer[l];
       for (int t = 0; t < 2; ++t) {
+        // only the images a minibatch step or rollout reads: W^T feeds DGRAD, which layer 0 has
+        // none of; W feeds the layered forward, which the fused kernels (fragment-major images)
+        // replace
+        if ((t == 1 && l == 0) || (t == 0 && W.fused_rollout)) continue;
         ImageDesc &d = q.img[q.n++];
         d.w = ctx->params + L.w_off;
         d.out = L.out;
@@ -1191,8 +1195,117 @@ __global__ __launch_bounds__(256) void wide_loss_kernel(WideLossArgs q) {
   }
 }
 
-__global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q) {
-  (void)reduce_slab_block(q, blockIdx.x);
+// The wide path's slab fold in one launch of two block kinds (deterministic, fixed orders):
+// - fast blocks, one thread per float4 group of the flat gradient: groups of segments with
+//   kRedChunks splits (the hidden-layer WGRAD slabs, nearly all the bytes) issue all their slab
+//   loads before the first add and sum them in split order (reduce_slab_block's order for these
+//   segments: its chunks hold one split each); pure padding groups are written as zeros;
+// - slow blocks over the groups of every other segment (heads: 64 splits, bias column sums,
+//   the loss kernel's 1024 per-block partials, a tensor's partial last group): 4 groups x 128
+//   chunks per block, so no thread reads more than a handful of splits, then the 128 chunk sums
+//   in chunk order.
+// The 16-chunk reduce_slab_block kept one 16-B load in flight per thread on the 16-split slabs
+// and 64 sequential loads per thread on the 1024-split partials.
+constexpr int kSlowGroups = 4;
+constexpr int kSlowChunks = kRedThreads / kSlowGroups;  // 128
+struct WideRedPlan {
+  int fast_blocks;
+  int nslow;                      // slow runs: groups [first, first + 4 * count) of segment seg
+  int seg[kMaxSegs];
+  int64_t first[kMaxSegs];
+  int64_t prefix[kMaxSegs + 1];   // cumulative group counts of the runs
+};
+
+__device__ __forceinline__ bool fast_seg(const ReduceSeg &g) {
+  return g.nsplit == kRedChunks && g.stride % 4 == 0 && reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
+}
+
+// splits [k0, k1) of parameters i..i+3 (i - g.dst = off >= 0): slab_item_sum's arithmetic
+__device__ __forceinline__ float4 split_range_sum(const ReduceSeg &g, int64_t off, int k0, int k1) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (off + 3 < g.len && g.stride % 4 == 0 && reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
+    const float *src = g.src + off;
+    float4 acc1 = acc;
+    int k = k0;
+    for (; k + 1 < k1; k += 2) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+      const float4 u = *reinterpret_cast<const float4 *>(src + (k + 1) * g.stride);
+      acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
+      acc1 = make_float4(acc1.x + u.x, acc1.y + u.y, acc1.z + u.z, acc1.w + u.w);
+    }
+    if (k < k1) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + k * g.stride);
+      acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
+    }
+    return make_float4(acc.x + acc1.x, acc.y + acc1.y, acc.z + acc1.z, acc.w + acc1.w);
+  }
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (off + e >= g.len) continue;
+    for (int k = k0; k < k1; ++k) a4[e] += g.src[off + e + static_cast<int64_t>(k) * g.stride];
+  }
+  return make_float4(a4[0], a4[1], a4[2], a4[3]);
+}
+
+__global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q, WideRedPlan pl) {
+  __shared__ __attribute__((aligned(16))) char scratch[kRedScratchBytes];
+  __shared__ float4 part[kSlowChunks][kSlowGroups];
+  const RedScratch sc = red_scratch(scratch);
+  const int tid = threadIdx.x;
+  if (tid < q.nseg) sc.sseg[tid] = q.seg[tid];
+  __syncthreads();
+  if (static_cast<int>(blockIdx.x) < pl.fast_blocks) {
+    const int64_t i = (static_cast<int64_t>(blockIdx.x) * kRedThreads + tid) * 4;
+    if (i < q.total) {
+      const ReduceSeg &g = sc.sseg[seg_find(sc.sseg, q.nseg, i)];
+      const int64_t off = i - g.dst;
+      if (off < 0 || off >= g.len) {  // between tensors: padding
+        *reinterpret_cast<float4 *>(q.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else if (fast_seg(g) && off + 3 < g.len) {
+        float4 v[kRedChunks];
+#pragma unroll
+        for (int c = 0; c < kRedChunks; ++c)
+          v[c] = *reinterpret_cast<const float4 *>(g.src + off + c * g.stride);
+        // a one-split chunk's sum is (0 + v) + 0 (the two partial sums), then chunk order
+        auto one = [](float4 a) {
+          return make_float4((0.f + a.x) + 0.f, (0.f + a.y) + 0.f, (0.f + a.z) + 0.f, (0.f + a.w) + 0.f);
+        };
+        float4 out = one(v[0]);
+#pragma unroll
+        for (int c = 1; c < kRedChunks; ++c) {
+          const float4 b = one(v[c]);
+          out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
+        }
+        *reinterpret_cast<float4 *>(q.grad + i) = out;
+      }
+    }
+    if (blockIdx.x == 0 && q.loss_out) reduce_loss_block(q, sc.lred);
+    return;
+  }
+  // slow block: groups 4 sb .. 4 sb + 3 of the slow runs, 128 chunks each
+  const int64_t gs = static_cast<int64_t>(blockIdx.x - pl.fast_blocks) * kSlowGroups + (tid % kSlowGroups);
+  const int chunk = tid / kSlowGroups;
+  int run = 0;
+  while (run + 1 < pl.nslow && pl.prefix[run + 1] <= gs) ++run;
+  const bool valid = gs < pl.prefix[pl.nslow];
+  const ReduceSeg &g = sc.sseg[pl.seg[run]];
+  const int64_t i = pl.first[run] + 4 * (gs - pl.prefix[run]);
+  float4 ps = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    const int k0 = (g.nsplit * chunk) / kSlowChunks, k1 = (g.nsplit * (chunk + 1)) / kSlowChunks;
+    ps = split_range_sum(g, i - g.dst, k0, k1);
+  }
+  part[chunk][tid % kSlowGroups] = ps;
+  __syncthreads();
+  if (chunk == 0 && valid) {
+    float4 out = part[0][tid];
+    for (int c = 1; c < kSlowChunks; ++c) {
+      const float4 b = part[c][tid];
+      out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
+    }
+    *reinterpret_cast<float4 *>(q.grad + i) = out;
+  }
 }
 
 int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *actions_d,
@@ -1369,8 +1482,30 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   r.loss_out = loss_d;
   double slab_floats = 0;
   for (int i = 0; i < ns; ++i) slab_floats += static_cast<double>(r.seg[i].nsplit) * r.seg[i].len;
+  // the fold plan: fast groups (16-split aligned segments) by the fast blocks, the rest in runs
+  WideRedPlan pl{};
+  pl.fast_blocks = static_cast<int>(ceil_div(P, 4 * kRedThreads));
+  auto add_run = [&](int seg, int64_t first, int64_t groups) {
+    PPO_REQUIRE(pl.nslow < kMaxSegs, "wide reduce: more than %d slow runs", kMaxSegs);
+    pl.seg[pl.nslow] = seg;
+    pl.first[pl.nslow] = first;
+    pl.prefix[pl.nslow + 1] = pl.prefix[pl.nslow] + groups;
+    ++pl.nslow;
+    return 0;
+  };
+  for (int i = 0; i < ns; ++i) {
+    const ReduceSeg &g = r.seg[i];
+    const bool fast = g.nsplit == kRedChunks && g.stride % 4 == 0 &&
+                      reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
+    if (!fast) {
+      if (int rc = add_run(i, g.dst, ceil_div(g.len, 4))) return rc;
+    } else if (g.len % 4) {  // the partial last group
+      if (int rc = add_run(i, g.dst + 4 * (g.len / 4), 1)) return rc;
+    }
+  }
+  const int slow_blocks = static_cast<int>(ceil_div(pl.prefix[pl.nslow], kSlowGroups));
   launch_k(TimRec{KC_REDUCE, "wide_reduce_kernel", slab_floats, 4.0 * (slab_floats + P)},
-           wide_reduce_kernel, dim3(ceil_div(P, kRedParams)), dim3(kRedThreads), 0, st, r);
+           wide_reduce_kernel, dim3(pl.fast_blocks + slow_blocks), dim3(kRedThreads), 0, st, r, pl);
   PPO_LAUNCHED();
   return 0;
 }
