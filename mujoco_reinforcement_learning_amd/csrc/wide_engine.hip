@@ -213,12 +213,12 @@ struct PackArgs {
   int n;
 };
 
-__global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q) {
+__device__ __forceinline__ void pack_tile(const PackArgs &q, int blk) {
   __shared__ float tile[kPackT][kPackT + 1];
   int i = 0;
-  while (i + 1 < q.n && q.img[i + 1].blocks <= static_cast<int>(blockIdx.x)) ++i;
+  while (i + 1 < q.n && q.img[i + 1].blocks <= blk) ++i;
   const ImageDesc d = q.img[i];
-  const int t = static_cast<int>(blockIdx.x) - d.blocks;
+  const int t = blk - d.blocks;
   const int tiles_c = d.cols / kPackT;
   const int r0 = (t / tiles_c) * kPackT, c0 = (t % tiles_c) * kPackT;  // image tile origin
   // master tile: rows o0.. (out), columns i0.. (in); image (r, c) = master (r, c) or (c, r)
@@ -259,11 +259,11 @@ struct FragArgs {
   int n;
 };
 
-__global__ __launch_bounds__(256) void wide_frag_pack_kernel(FragArgs q) {
+__device__ __forceinline__ void pack_frag(const FragArgs &q, int b) {
   int i = 0;
-  while (i + 1 < q.n && q.img[i + 1].blocks <= static_cast<int>(blockIdx.x)) ++i;
+  while (i + 1 < q.n && q.img[i + 1].blocks <= b) ++i;
   const FragDesc d = q.img[i];
-  const int64_t f = static_cast<int64_t>(blockIdx.x - d.blocks) * 256 + threadIdx.x;  // fragment
+  const int64_t f = static_cast<int64_t>(b - d.blocks) * 256 + threadIdx.x;  // fragment
   if (f >= static_cast<int64_t>(d.tiles) * d.ks * 64) return;
   const int lane = static_cast<int>(f & 63);
   const int blk = static_cast<int>(f >> 6), ks = blk / d.tiles, ot = blk - ks * d.tiles;
@@ -280,11 +280,19 @@ __global__ __launch_bounds__(256) void wide_frag_pack_kernel(FragArgs q) {
                  wide::pack2(v[6], v[7]));
 }
 
-static int wide_frag_pack(ppo_ctx *ctx, hipStream_t st) {
+// One launch for every image an optimizer step refreshes: blocks [0, frag_blocks) the
+// fragment-major images (fused forward / rollout), the rest the 64x64 tiles of the W^T (and, for
+// the layered forward, W) images.
+__global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q, FragArgs fq, int frag_blocks) {
+  const int b = static_cast<int>(blockIdx.x);
+  if (b < frag_blocks) pack_frag(fq, b);
+  else pack_tile(q, b - frag_blocks);
+}
+
+// the fragment-major images' descriptors (blocks counted from 0)
+static int frag_args(ppo_ctx *ctx, FragArgs &q, double &elems) {
   WideWork &W = *ctx->wide;
-  FragArgs q{};
   int blocks = 0;
-  double elems = 0;
   for (int z = 0; z < 2; ++z) {
     const NetDesc &nd = ctx->net[z];
     const WideNetWork &wn = W.net[z];
@@ -301,19 +309,16 @@ static int wide_frag_pack(ppo_ctx *ctx, hipStream_t st) {
       elems += static_cast<double>(d.out) * d.in;
     }
   }
-  launch_k(TimRec{KC_GATHER, "wide_frag_pack_kernel", 0.0, elems * (4.0 + 2.0)},
-           wide_frag_pack_kernel, dim3(blocks), dim3(256), 0, st, q);
-  PPO_LAUNCHED();
-  return 0;
+  return blocks;
 }
 
 int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
-  if (frag && ctx->wide->fused_rollout)
-    if (int rc = wide_frag_pack(ctx, st)) return rc;
   WideWork &W = *ctx->wide;
+  FragArgs fq{};
+  double elems = 0;
+  const int frag_blocks = (frag && W.fused_rollout) ? frag_args(ctx, fq, elems) : 0;
   PackArgs q{};
   int blocks = 0;
-  double elems = 0;
   for (int z = 0; z < 2; ++z) {
     const NetDesc &nd = ctx->net[z];
     const WideNetWork &wn = W.net[z];
@@ -339,7 +344,7 @@ int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
     }
   }
   launch_k(TimRec{KC_GATHER, "wide_pack_kernel", 0.0, elems * (4.0 + 2.0)}, wide_pack_kernel,
-           dim3(blocks), dim3(256), 0, st, q);
+           dim3(frag_blocks + blocks), dim3(256), 0, st, q, fq, frag_blocks);
   PPO_LAUNCHED();
   return 0;
 }
@@ -1200,27 +1205,30 @@ __global__ __launch_bounds__(256) void wide_loss_kernel(WideLossArgs q) {
 //   kRedChunks splits (the hidden-layer WGRAD slabs, nearly all the bytes) issue all their slab
 //   loads before the first add and sum them in split order (reduce_slab_block's order for these
 //   segments: its chunks hold one split each); pure padding groups are written as zeros;
-// - slow blocks over the groups of every other segment (heads: 64 splits, bias column sums,
-//   the loss kernel's 1024 per-block partials, a tensor's partial last group): 4 groups x 128
-//   chunks per block, so no thread reads more than a handful of splits, then the 128 chunk sums
-//   in chunk order.
+// - slow blocks over the groups of every other segment (heads: 64 splits, bias column sums, the
+//   loss kernel's 1024 per-block partials, a tensor's partial last group, other split counts):
+//   G groups x C chunks per block (C = 16, reduce_slab_block's layout and order, or C = 128 for
+//   segments of more than 256 splits, so no thread reads more than a handful), then the C chunk
+//   sums in chunk order.
 // The 16-chunk reduce_slab_block kept one 16-B load in flight per thread on the 16-split slabs
 // and 64 sequential loads per thread on the 1024-split partials.
-constexpr int kSlowGroups = 4;
-constexpr int kSlowChunks = kRedThreads / kSlowGroups;  // 128
+constexpr int kHeavyChunks = 128;
 struct WideRedPlan {
   int fast_blocks;
-  int nslow;                      // slow runs: groups [first, first + 4 * count) of segment seg
+  int nslow;                      // slow runs: `groups` float4 groups from parameter `first`
   int seg[kMaxSegs];
+  int chunks[kMaxSegs];           // kRedChunks or kHeavyChunks
   int64_t first[kMaxSegs];
-  int64_t prefix[kMaxSegs + 1];   // cumulative group counts of the runs
+  int64_t groups[kMaxSegs];
+  int bprefix[kMaxSegs + 1];      // cumulative block counts of the runs
 };
 
 __device__ __forceinline__ bool fast_seg(const ReduceSeg &g) {
   return g.nsplit == kRedChunks && g.stride % 4 == 0 && reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
 }
 
-// splits [k0, k1) of parameters i..i+3 (i - g.dst = off >= 0): slab_item_sum's arithmetic
+// splits [k0, k1) of parameters i..i+3 (i - g.dst = off >= 0): slab_item_sum's arithmetic (two
+// interleaved float4 sums, or eight strided partial sums per element off the aligned path)
 __device__ __forceinline__ float4 split_range_sum(const ReduceSeg &g, int64_t off, int k0, int k1) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (off + 3 < g.len && g.stride % 4 == 0 && reinterpret_cast<uintptr_t>(g.src) % 16 == 0) {
@@ -1243,14 +1251,21 @@ __device__ __forceinline__ float4 split_range_sum(const ReduceSeg &g, int64_t of
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (off + e >= g.len) continue;
-    for (int k = k0; k < k1; ++k) a4[e] += g.src[off + e + static_cast<int64_t>(k) * g.stride];
+    const float *src = g.src + off + e;
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int k = k0;
+    for (; k + 7 < k1; k += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s8[j] += src[static_cast<int64_t>(k + j) * g.stride];
+    }
+    for (; k < k1; ++k) s8[0] += src[static_cast<int64_t>(k) * g.stride];
+    a4[e] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   }
   return make_float4(a4[0], a4[1], a4[2], a4[3]);
 }
 
 __global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q, WideRedPlan pl) {
   __shared__ __attribute__((aligned(16))) char scratch[kRedScratchBytes];
-  __shared__ float4 part[kSlowChunks][kSlowGroups];
   const RedScratch sc = red_scratch(scratch);
   const int tid = threadIdx.x;
   if (tid < q.nseg) sc.sseg[tid] = q.seg[tid];
@@ -1283,25 +1298,27 @@ __global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q, 
     if (blockIdx.x == 0 && q.loss_out) reduce_loss_block(q, sc.lred);
     return;
   }
-  // slow block: groups 4 sb .. 4 sb + 3 of the slow runs, 128 chunks each
-  const int64_t gs = static_cast<int64_t>(blockIdx.x - pl.fast_blocks) * kSlowGroups + (tid % kSlowGroups);
-  const int chunk = tid / kSlowGroups;
+  // slow block: G = kRedThreads / C groups of one run, C chunks each
+  const int sb = static_cast<int>(blockIdx.x) - pl.fast_blocks;
   int run = 0;
-  while (run + 1 < pl.nslow && pl.prefix[run + 1] <= gs) ++run;
-  const bool valid = gs < pl.prefix[pl.nslow];
+  while (run + 1 < pl.nslow && pl.bprefix[run + 1] <= sb) ++run;
+  const int C = pl.chunks[run], G = kRedThreads / C;
+  const int grp = tid % G, chunk = tid / G;
+  const int64_t gi = static_cast<int64_t>(sb - pl.bprefix[run]) * G + grp;
+  const bool valid = gi < pl.groups[run];
   const ReduceSeg &g = sc.sseg[pl.seg[run]];
-  const int64_t i = pl.first[run] + 4 * (gs - pl.prefix[run]);
+  const int64_t i = pl.first[run] + 4 * gi;
   float4 ps = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
-    const int k0 = (g.nsplit * chunk) / kSlowChunks, k1 = (g.nsplit * (chunk + 1)) / kSlowChunks;
+    const int k0 = (g.nsplit * chunk) / C, k1 = (g.nsplit * (chunk + 1)) / C;
     ps = split_range_sum(g, i - g.dst, k0, k1);
   }
-  part[chunk][tid % kSlowGroups] = ps;
+  sc.part[chunk * G + grp] = ps;
   __syncthreads();
   if (chunk == 0 && valid) {
-    float4 out = part[0][tid];
-    for (int c = 1; c < kSlowChunks; ++c) {
-      const float4 b = part[c][tid];
+    float4 out = sc.part[grp];
+    for (int c = 1; c < C; ++c) {
+      const float4 b = sc.part[c * G + grp];
       out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
     }
     *reinterpret_cast<float4 *>(q.grad + i) = out;
@@ -1487,9 +1504,13 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   pl.fast_blocks = static_cast<int>(ceil_div(P, 4 * kRedThreads));
   auto add_run = [&](int seg, int64_t first, int64_t groups) {
     PPO_REQUIRE(pl.nslow < kMaxSegs, "wide reduce: more than %d slow runs", kMaxSegs);
+    const int c = r.seg[seg].nsplit > 256 ? kHeavyChunks : kRedChunks;
     pl.seg[pl.nslow] = seg;
+    pl.chunks[pl.nslow] = c;
     pl.first[pl.nslow] = first;
-    pl.prefix[pl.nslow + 1] = pl.prefix[pl.nslow] + groups;
+    pl.groups[pl.nslow] = groups;
+    pl.bprefix[pl.nslow + 1] =
+        pl.bprefix[pl.nslow] + static_cast<int>(ceil_div(groups, kRedThreads / c));
     ++pl.nslow;
     return 0;
   };
@@ -1503,7 +1524,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
       if (int rc = add_run(i, g.dst + 4 * (g.len / 4), 1)) return rc;
     }
   }
-  const int slow_blocks = static_cast<int>(ceil_div(pl.prefix[pl.nslow], kSlowGroups));
+  const int slow_blocks = pl.bprefix[pl.nslow];
   launch_k(TimRec{KC_REDUCE, "wide_reduce_kernel", slab_floats, 4.0 * (slab_floats + P)},
            wide_reduce_kernel, dim3(pl.fast_blocks + slow_blocks), dim3(kRedThreads), 0, st, r, pl);
   PPO_LAUNCHED();
