@@ -337,6 +337,35 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
   st4(g + 3 * H + j, dout);
 }
 
+// The slab fold when every tensor is float4-aligned (the usual case): one thread per float4
+// group, its 32 split loads issued 16 at a time, summed in reduce_slab_block's order (chunk c =
+// splits 2c, 2c + 1 as (0 + v_2c) + (0 + v_2c+1), chunks in order) -- bitwise that kernel's
+// result, with 16 loads in flight per thread instead of 2.
+static_assert(kSplits == 2 * kRedChunks, "lstm_reduce_fast_kernel: two splits per chunk");
+__global__ __launch_bounds__(256) void lstm_reduce_fast_kernel(float *__restrict__ grad,
+                                                               const float *__restrict__ slabs,
+                                                               int64_t total) {
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i >= total) return;
+  const float *src = slabs + i;
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    float4 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      v[j] = *reinterpret_cast<const float4 *>(src + (16 * half + j) * total);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float4 a = v[2 * c], b = v[2 * c + 1];
+      const float4 p = make_float4((0.f + a.x) + (0.f + b.x), (0.f + a.y) + (0.f + b.y),
+                                   (0.f + a.z) + (0.f + b.z), (0.f + a.w) + (0.f + b.w));
+      out = (half == 0 && c == 0) ? p : make_float4(out.x + p.x, out.y + p.y, out.z + p.z, out.w + p.w);
+    }
+  }
+  *reinterpret_cast<float4 *>(grad + i) = out;
+}
+
 __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) {
   (void)reduce_slab_block(q, blockIdx.x);
 }
@@ -1192,8 +1221,16 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   r.nseg = ns;
   r.total = x->total;
   r.grad = grad_d;
-  launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 0.0}, lstm_reduce_kernel,
-           dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);
+  bool aligned = x->total % 4 == 0 && reinterpret_cast<uintptr_t>(x->slabs) % 16 == 0 &&
+                 reinterpret_cast<uintptr_t>(grad_d) % 16 == 0;
+  for (size_t i = 0; i < x->offsets.size(); ++i) aligned = aligned && x->offsets[i] % 4 == 0;
+  if (aligned)
+    launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 4.0 * (kSplits + 1.0) * x->total},
+             lstm_reduce_fast_kernel, dim3(ceil_div(x->total, 4 * 256)), dim3(256), 0, st, grad_d,
+             x->slabs, x->total);
+  else
+    launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 0.0}, lstm_reduce_kernel,
+             dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);
   PPO_LAUNCHED();
   return 0;
 }
