@@ -23,6 +23,7 @@
 #   dp1       the data-parallel step sequence on one rank (PPO_DP_REHEARSE=1)
 #   lstm      bench.py --model lstm (BiLSTM agent, main.py network) -> bench_${TAG}_lstm.json
 #   lstmtrace rocprofv3 --kernel-trace --stats over one LSTM bench iteration
+#   abmain    the headline line (no legs) per environment setting (ABSETS="A=0,B=1 ...")
 #   abmodel   one model's line (MODEL) per environment setting (ABSETS="A=0,B=1 ...")
 #   abhum     Humanoid shard line per value of one env knob (ABVAR, ABVALS)
 #   cnnpmc    SQ counter passes over one pixel-CNN iteration (LDS-staged conv kernels)
