@@ -278,6 +278,7 @@ struct CellBwdArgs {
   float *g;            // gate activations in, dG out
   const float *c;
   const float *dy;     // [B*W][2H] gradient of the layer output (nullable rows handled by dy_mode)
+  const float *dy2;    // mode 1, nullable: a second [B*W][2H] term, dy + dy2 (the actor's two MLPs)
   const float *dy_last;  // mode 2: [B][2H] gradient of h at t = W-1 only
   int dy_mode;         // 1: dy full, 2: dy_last
   const float *dh_rec; // [B][2H] recurrent gradient (nullptr at s = 0)
@@ -305,8 +306,12 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
   const int64_t r = b * (2 * H) + d * H + j;
   const lstm_f4 z4 = {0.f, 0.f, 0.f, 0.f};
   lstm_f4 dh4 = z4;
-  if (q.dy_mode == 1) dh4 = ld4(q.dy + o);
-  else if (t == W - 1) dh4 = ld4(q.dy_last + r);
+  if (q.dy_mode == 1) {
+    dh4 = ld4(q.dy + o);
+    if (q.dy2) dh4 = dh4 + ld4(q.dy2 + o);  // add_inplace's dy + dy2, at its one read
+  } else if (t == W - 1) {
+    dh4 = ld4(q.dy_last + r);
+  }
   const lstm_f4 dr4 = q.s > 0 ? ld4(q.dh_rec + r) : z4;
   const lstm_f4 dc4 = q.s > 0 ? ld4(q.dcarry + r) : z4;
   float *g = q.g + (b * W + t) * (8 * H) + d * (4 * H);
@@ -752,7 +757,7 @@ int mlp_forward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm,
 // into the slabs, the input gradient (times act'(input) of the feature activation) into din.
 int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm, const float *in,
                  float *const *pp[2], float *din, int64_t ld_din, int feat_act, int b,
-                 hipStream_t st) {
+                 hipStream_t st, bool sum_din = true) {
   // pp[k]: the problem's two ping-pong buffers; pp[k][0] holds the output-layer gradient
   const float *P = x->params;
   float *cur[2] = {pp[0][0], nm == 2 ? pp[1][0] : nullptr};
@@ -796,7 +801,9 @@ int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm
     }
     const int act = l > 0 ? m[0]->l[l - 1].act : feat_act;
     if (int rc = gemm_dx(x, q, nm, L0.out, b, L0.in, act, st)) return rc;
-    if (l == 0 && nm == 2) {  // the two actor MLPs read the same features: sum their dX
+    // the two actor MLPs read the same features: sum their dX (sum_din = false: the consumer
+    // adds x->tmp where it reads din, lstm_backward's dy2)
+    if (l == 0 && nm == 2 && sum_din) {
       const int64_t n = static_cast<int64_t>(b) * ld_din;
       launch_k(TimRec{KC_LSTM, "add_inplace_kernel", 0.0, 0.0}, add_inplace_kernel,
                dim3(ceil_div(n, 256)), dim3(256), 0, st, din, x->tmp, n);
@@ -810,7 +817,8 @@ int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm
 
 // BPTT of LSTM net z given dY of the top layer (actor: full [b*W][2H] in x->dy[0]; critic: the
 // [b][2H] gradient of h at t = W-1 in x->dy[0]); weight grads into the slabs.
-int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st) {
+int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st,
+                  const float *dy2 = nullptr) {
   const LstmNet &N = x->net[z];
   const int H = N.hidden, W = x->cfg.window;
   const float *P = x->params;
@@ -839,6 +847,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
       a.c = x->c[z][l];
       a.dy_mode = (top && z == 1) ? 2 : 1;
       a.dy = x->dy[cur];
+      a.dy2 = top ? dy2 : nullptr;  // the top layer's second dY term (the actor's log-std MLP)
       a.dy_last = x->dy[cur];
       a.dh_rec = s > 0 ? x->dhrec : nullptr;
       a.dcarry = x->dcarry;
@@ -1202,9 +1211,9 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
     float *const *aa[2] = {x->act_mu, x->act_ls};
     float *const *pp[2] = {x->dz[0], x->dz[1]};
     if (int rc = mlp_backward(x, am, aa, 2, x->feat_a, pp, x->dy[0],
-                              static_cast<int64_t>(W) * 2 * H, c.activation, b, st))
+                              static_cast<int64_t>(W) * 2 * H, c.activation, b, st, false))
       return rc;
-    if (int rc = lstm_backward(x, 0, x->x, b, st)) return rc;
+    if (int rc = lstm_backward(x, 0, x->x, b, st, x->tmp)) return rc;
   }
   // slabs -> flat gradient, tensor by tensor in a fixed split order
   ReduceArgs r{};
