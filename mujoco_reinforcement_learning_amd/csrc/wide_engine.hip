@@ -223,16 +223,33 @@ __device__ __forceinline__ void pack_tile(const PackArgs &q, int blk) {
   const int r0 = (t / tiles_c) * kPackT, c0 = (t % tiles_c) * kPackT;  // image tile origin
   // master tile: rows o0.. (out), columns i0.. (in); image (r, c) = master (r, c) or (c, r)
   const int o0 = d.transposed ? c0 : r0, i0 = d.transposed ? r0 : c0;
-  const int tid = threadIdx.x, li = tid & 63;
-#pragma unroll 4
-  for (int k = 0; k < kPackT / 4; ++k) {
-    const int lo = 4 * k + (tid >> 6);
-    const int o = o0 + lo, in = i0 + li;
-    const bool ok = o < d.out && in < d.in;
-    // clamped address, masked value: no load behind a branch
-    const float v = d.w[static_cast<int64_t>(ok ? o : 0) * d.in + (ok ? in : 0)];
-    if (d.transposed) tile[li][lo] = ok ? v : 0.f;  // tile[image row][image col]
-    else tile[lo][li] = ok ? v : 0.f;
+  const int tid = threadIdx.x;
+  // 16 rows x 64 columns per pass, a float4 per thread (clamped address, masked values: no load
+  // behind a branch); the masters' rows are 16-B aligned when d.in % 4 == 0
+  const bool vec = d.in % 4 == 0 && reinterpret_cast<uintptr_t>(d.w) % 16 == 0;
+  const int cg = 4 * (tid & 15);
+#pragma unroll
+  for (int k = 0; k < kPackT / 16; ++k) {
+    const int lo = 16 * k + (tid >> 4);
+    const int o = o0 + lo, in = i0 + cg;
+    float v[4];
+    if (vec) {
+      const bool ok = o < d.out && in < d.in;  // d.in % 4 == 0: the whole float4 is in
+      const float4 u = *reinterpret_cast<const float4 *>(d.w + static_cast<int64_t>(ok ? o : 0) * d.in + (ok ? in : 0));
+      v[0] = ok ? u.x : 0.f, v[1] = ok ? u.y : 0.f, v[2] = ok ? u.z : 0.f, v[3] = ok ? u.w : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = o < d.out && in + e < d.in;
+        const float u = d.w[static_cast<int64_t>(ok ? o : 0) * d.in + (ok ? in + e : 0)];
+        v[e] = ok ? u : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (d.transposed) tile[cg + e][lo] = v[e];  // tile[image row][image col]
+      else tile[lo][cg + e] = v[e];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -269,11 +286,22 @@ __device__ __forceinline__ void pack_frag(const FragArgs &q, int b) {
   const int blk = static_cast<int>(f >> 6), ks = blk / d.tiles, ot = blk - ks * d.tiles;
   const int o = 32 * ot + (lane & 31), i0 = 16 * ks + 8 * (lane >> 5);
   float v[8];
+  if (d.in % 4 == 0 && reinterpret_cast<uintptr_t>(d.w) % 16 == 0) {
+    // two float4 loads (d.in % 4 == 0: a 4-group is wholly inside or outside the row)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool ok = o < d.out && i0 + j < d.in;
-    const float u = d.w[ok ? static_cast<int64_t>(o) * d.in + i0 + j : 0];
-    v[j] = ok ? u : 0.f;
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const bool ok = o < d.out && i0 + 4 * h2 < d.in;
+      const float4 u = *reinterpret_cast<const float4 *>(d.w + (ok ? static_cast<int64_t>(o) * d.in + i0 + 4 * h2 : 0));
+      v[4 * h2] = ok ? u.x : 0.f, v[4 * h2 + 1] = ok ? u.y : 0.f;
+      v[4 * h2 + 2] = ok ? u.z : 0.f, v[4 * h2 + 3] = ok ? u.w : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = o < d.out && i0 + j < d.in;
+      const float u = d.w[ok ? static_cast<int64_t>(o) * d.in + i0 + j : 0];
+      v[j] = ok ? u : 0.f;
+    }
   }
   reinterpret_cast<uint4 *>(d.dst)[f] =
       make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
