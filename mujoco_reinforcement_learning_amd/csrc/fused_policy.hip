@@ -45,6 +45,8 @@ struct PolicyLds {
   static_assert(TOTAL <= 163840, "LDS budget");
 };
 
+// Barriers are LDS-only (lds_sync): the waves hand each other data through LDS only, and the
+// window / state stores issued before a barrier are not waited for there
 template <int H, int ACT, int NH, bool ACTOR, bool STAMP = false>
 __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const FusedNet &N,
                                             char *lds) {
@@ -159,7 +161,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     if (ok && writer && q.obs_d)
       q.window_d[static_cast<int64_t>(row0 + row) * O + f] = xv[k];
   }
-  __syncthreads();
+  lds_sync();
   PSTAMP(2);
   // ---- per-(row, slice) mean and std on every wave: lane = feature (lanes 0-31 and 32-63 are
   //      two rows), each wave 4 rows as two interleaved chains.  row_stats.h's pairwise tree over
@@ -182,7 +184,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   PSTAMP(3);
   // ---- standardised states: thread -> (row, feature pair); bf16 X image and the f32 state
   //      (writer workgroups) ----
@@ -203,7 +205,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     }
     *reinterpret_cast<uint32_t *>(ximg + x_off(xr, c2 >> 3) + 2 * (c2 & 7)) = pack2(y[0], y[1]);
   }
-  __syncthreads();
+  lds_sync();
   PSTAMP(4);
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----
@@ -235,7 +237,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   PSTAMP(5);
 
   // ---- L1: a2 = act(W1 a1 + b1) -> A2 image (bf16: the head's operand) ----
@@ -258,7 +260,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
                        pack2(act_forward(a2[t][4 * g + 2] + bv.z, ACT), act_forward(a2[t][4 * g + 3] + bv.w, ACT)));
     }
   }
-  __syncthreads();
+  lds_sync();
   PSTAMP(7);
 
   // ---- heads: z = a2 . W_h^T on the 16x16x32 MFMA (the update kernel's bf16 products); waves w
@@ -281,7 +283,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
     float *const xch = reinterpret_cast<float *>(a1img);  // [8 waves][64 lanes][2]
     *reinterpret_cast<float2 *>(xch + 2 * (w * 64 + lane)) =
         half ? make_float2(zacc[0], zacc[1]) : make_float2(zacc[2], zacc[3]);
-    __syncthreads();
+    lds_sync();
     const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
     const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
     if (!head_wave) {

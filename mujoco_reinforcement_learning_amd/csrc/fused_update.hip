@@ -398,6 +398,9 @@ __device__ __forceinline__ void mfma16_drain(f32x4 &acc) { asm volatile("s_nop 1
 // the head-dW tiles of its features.  NH = head width padded to 2/4/6/8 (actor) or 1 (critic),
 // compile-time so the per-action loops are branch-free.  Every fc product -- the three hidden
 // GEMMs and the head -- is a bf16-operand MFMA with f32 accumulation (oracle.use_bf16_gemms).
+// Phase barriers are LDS-only (lds_sync): waves hand each other data through LDS only, so the
+// record prefetch and the weight-ring primes stay in flight across them (__syncthreads drained
+// them at every phase; measured 10.40-10.47 -> 10.29-10.33 ms per iteration, profiles/r04_lds_barrier/)
 template <int H, int ACT, int NH, bool ACTOR, bool STAMP>
 __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N, char *lds,
                                            uint64_t *stamps) {
@@ -496,7 +499,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
   uint64_t xpre = load_half(blockIdx.x, i_first, tid0, false);
   bool xok = row_ok(blockIdx.x, i_first, tid0);
-  __syncthreads();
+  lds_sync();
 
   // ---- persistent accumulators ----
   f32x16 gw1[2][4];   // dW1 tiles: o-tiles 2*(w&3)+{0,1}, i-tiles 4*(w>>2)+{0..3}
@@ -550,7 +553,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       else
         w0f[s] = lds_b128(lds + L::W0 + x_off(32 * w + r, 2 * s + h));
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(0);
 
     // ---- phase 1: a1 = act(W0 x + b0) -> A1 image ----
@@ -582,7 +585,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         }
       }
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(1);
 
     // ---- phase 2: a2 = W1 a1 (f32 accumulators) ----
@@ -615,7 +618,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
               make_uint2(pack2(y0, y1), pack2(y2, y3));
       }
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(3);
 
     // ---- phase 4: head z = a2 . W_h^T on the 16x16x32 MFMA, then the per-(row, action) loss
@@ -646,7 +649,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       float *const xch = reinterpret_cast<float *>(lds + L::D2);  // [8 waves][64 lanes][2]
       *reinterpret_cast<float2 *>(xch + 2 * (w * 64 + lane)) =
           half ? make_float2(zacc[0], zacc[1]) : make_float2(zacc[2], zacc[3]);
-      __syncthreads();
+      lds_sync();
       const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
       const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
       const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
@@ -714,7 +717,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         *reinterpret_cast<uint16_t *>(dzimg + (lr0 + i) * kDzRowBytes + 2 * n) = bf16_bits(dz[i]);
       *reinterpret_cast<uint32_t *>(dztimg + n * kDzTPitch + 2 * lr0) = pack2(dz[0], dz[1]);
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(4);
 
     // ---- phase 5: d2 = (dz . W_h) * act'(a2) on MFMA -> bias grad, D2 image; head dW ----
@@ -774,7 +777,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         ghw[u] = mfma16(af, bv, ghw[u]);
       }
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(5);
 
     // ---- phase 6a: dW1 += D2^T A1 (k = the chunk's 64 rows) ----
@@ -867,7 +870,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       gw0 = mfma(tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane), tr_frag_x(ximg, 16 * ks, lane), gw0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+    lds_sync();
     STAMP_AT(9);
   }
 #undef STAMP_AT
@@ -927,7 +930,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       dst[2] = g_loss;
     }
   }
-  __syncthreads();
+  lds_sync();
   if (tid < na) {
     float sb = 0.f, sl = 0.f;
 #pragma unroll
