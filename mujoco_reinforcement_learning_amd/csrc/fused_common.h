@@ -282,16 +282,6 @@ __device__ __forceinline__ void mlp_pass(const __bf16 *wfrag, const char *img, i
   mfma_drain(acc);
 }
 
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
-// outstanding global loads and stores (__syncthreads drains vmcnt, so a prefetch meant to stay in
-// flight across a phase, or a store nobody in the workgroup reads, stalls every barrier).
-__device__ __forceinline__ void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 }  // namespace fu
 
 }  // namespace ppo

@@ -22,6 +22,8 @@
 
 #include <cstdint>
 
+#include "common.h"
+
 namespace ppo {
 
 struct GaeNoEmit {
@@ -79,7 +81,7 @@ __device__ __forceinline__ void gae_pipe_body(const float *__restrict__ value,
       s_q[buf][tt][c] = ok ? q : static_cast<RT>(0);
       em.load(buf, static_cast<int64_t>(t >= 0 ? t : 0) * n + envc, ok);
     }
-    __syncthreads();
+    lds_sync();  // LDS hand-off only: the record loads and the previous chunk's stores stay in flight
     if (k < KMAX && tid < EB) {  // the chain: rows of this chunk in descending time
       RT d[TC], qq[TC];
 #pragma unroll

@@ -861,11 +861,11 @@ __global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q)
     const uint4 v = *reinterpret_cast<const uint4 *>(q.x + static_cast<int64_t>(r0 + row) * q.ldx + 8 * c);
     *reinterpret_cast<uint4 *>(lds + fimg_off(row, c)) = v;
   }
-  __syncthreads();
+  lds_sync();
   int cur = 0;
   for (int l = 0; l < N.n_hidden; ++l) {
     fused_hidden<1>(N, l, lds + cur * kFRows * kFPitch, lds + (cur ^ 1) * kFRows * kFPitch, w, lane);
-    __syncthreads();
+    lds_sync();
     cur ^= 1;
   }
   // ---- head pre-activations (<= 32 outputs) on wave 0 ----
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) zt[lane & 31][(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = acc[0][0][r];
   }
-  __syncthreads();
+  lds_sync();
   const int row = tid >> 4, j = r0 + row;
   const bool row_ok = j < q.n;
   if (z == 0) {
@@ -904,7 +904,7 @@ __global__ __launch_bounds__(512) void wide_policy_fused_kernel(WideFusedArgs q)
       }
       lpt[row][a] = lp;
     }
-    __syncthreads();
+    lds_sync();
     if ((tid & 15) == 0 && row_ok && q.logp) {
       float s = 0.f;
       for (int a = 0; a < A; ++a) s += lpt[row][a];  // action order (policy_head_kernel)
@@ -956,12 +956,12 @@ __global__ __launch_bounds__(512) void wide_forward_fused_kernel(WideFwdArgs q) 
     const uint4 v = *reinterpret_cast<const uint4 *>(q.x + static_cast<int64_t>(r0 + row) * q.ldx + 8 * c);
     *reinterpret_cast<uint4 *>(lds + fimg_off(row, c)) = v;
   }
-  __syncthreads();
+  lds_sync();
   int cur = 0;
   for (int l = 0; l < N.n_hidden; ++l) {
     char *dst = lds + (cur ^ 1) * kFwdRows * kFPitch;
     fused_hidden<2>(N, l, lds + cur * kFwdRows * kFPitch, dst, w, lane);
-    __syncthreads();
+    lds_sync();
     // the layer's output rows out (16-B coalesced), zero past the device count
     const int width = 32 * N.tiles[l], cw = width / 8, ld = q.ldh[z][l];
     __bf16 *hout = q.h[z][l];
