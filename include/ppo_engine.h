@@ -503,6 +503,41 @@ int ppo_synthetic_pixel_step(uint32_t seed, int t, const float *action_d, int n,
                              const uint8_t *base_term_d, double *reward_out_d,
                              uint8_t *term_out_d, void *stream);
 
+/* ---- (e) data-parallel gradient exchange (csrc/comm.hip) ----------------
+ * The reference has no distributed code; the engine shards envs over the GPUs of one node (one
+ * process per GPU) and sums the flat actor+critic gradient of every optimizer step (ppo.py:120-135)
+ * with ONE in-place RCCL all-reduce, issued on the caller's compute stream -- so a hipGraph
+ * capture of the optimizer loop records it like a kernel.  RCCL is resolved at run time (the
+ * instance torch.distributed loaded, else librccl.so.1, or $PPO_RCCL_LIB); without it only these
+ * calls fail (PPO_EHIP, message in ppo_last_error).
+ *   ppo_comm_unique_id   rank 0 draws the 128-byte id; the host broadcasts it (torch.distributed)
+ *   ppo_comm_create      every rank, with the same id, its rank and its device (collective call)
+ *   ppo_comm_allreduce   buf_d[0, n) f32 := SUM over ranks, in place, ordered on `stream`
+ *   ppo_comm_check       the communicator's asynchronous error state (0 = healthy)
+ *   ppo_ctx_set_comm / ppo_allreduce_grads   SURVEY.md s8(b)'s ctx-owned form: the ctx keeps the
+ *                        communicator (not owned: ppo_comm_destroy after the ctx) and
+ *                        ppo_allreduce_grads(ctx, flat, n, stream) sums n <= ppo_param_count(ctx, -1)
+ *                        floats of the flat gradient layout. */
+#define PPO_COMM_ID_BYTES 128
+typedef struct ppo_comm ppo_comm;
+int ppo_comm_version(void); /* NCCL_VERSION_CODE of the RCCL in use, 0 if none */
+int ppo_comm_unique_id(uint8_t *id_out);
+int ppo_comm_create(const uint8_t *id, int nranks, int rank, int device, ppo_comm **out);
+int ppo_comm_destroy(ppo_comm *comm);
+int ppo_comm_allreduce(ppo_comm *comm, float *buf_d, int64_t n, void *stream);
+int ppo_comm_check(ppo_comm *comm);
+int ppo_ctx_set_comm(ppo_ctx *ctx, ppo_comm *comm);
+int ppo_allreduce_grads(ppo_ctx *ctx, float *flat_d, int64_t n, void *stream);
+
+/* Logged-loss share of the entropy bonus (ppo.py:128-132 `- entropy * entropy_eps`): the loss_d
+ * actor value a minibatch entry point writes is -(sum of the rows' clipped surrogate) * inv_b -
+ * share * entropy_eps * H.  Data-parallel ranks each see the same H (replicated log-std), so with
+ * the per-rank losses SUMMED for logging, rank 0 passes 1 and the others 0 and the sum carries the
+ * bonus once.  Default 1.  Gradients are unaffected (the per-row log-std term uses inv_ba). */
+int ppo_ctx_loss_entropy_share(ppo_ctx *ctx, float share);
+int ppo_lstm_loss_entropy_share(ppo_lstm_ctx *ctx, float share);
+int ppo_cnn_loss_entropy_share(ppo_cnn_ctx *ctx, float share);
+
 /* ---- wide layered path (bf16-resident activations; csrc/wide_gemm.h) ----------------------------
  * One bf16 MFMA GEMM of the wide path on caller buffers (kernel-level parity tests and tuning).
  * The products of network_block_creator.py:74-86 (Linear layers) and their autograd backward

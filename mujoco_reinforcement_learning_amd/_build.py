@@ -14,7 +14,7 @@ ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip", "csrc/fused_update4.hip",
            "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip",
            "csrc/cnn_engine.hip", "csrc/gemm_ops.hip", "csrc/wide_gemm.hip",
-           "csrc/wide_engine.hip"]
+           "csrc/wide_engine.hip", "csrc/comm.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]
 

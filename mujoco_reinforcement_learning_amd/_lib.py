@@ -209,7 +209,21 @@ _SIGNATURES = {
     "ppo_synthetic_pixel_step": (c_int, [ctypes.c_uint32, c_int, c_void_p, c_int, c_int, c_int,
                                          c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p]),
+    # data-parallel gradient exchange (comm.hip) and the logged loss's entropy share
+    "ppo_comm_version": (c_int, []),
+    "ppo_comm_unique_id": (c_int, [c_void_p]),
+    "ppo_comm_create": (c_int, [c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "ppo_comm_destroy": (c_int, [c_void_p]),
+    "ppo_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ppo_comm_check": (c_int, [c_void_p]),
+    "ppo_ctx_set_comm": (c_int, [c_void_p, c_void_p]),
+    "ppo_allreduce_grads": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ppo_ctx_loss_entropy_share": (c_int, [c_void_p, c_float]),
+    "ppo_lstm_loss_entropy_share": (c_int, [c_void_p, c_float]),
+    "ppo_cnn_loss_entropy_share": (c_int, [c_void_p, c_float]),
 }
+
+COMM_ID_BYTES = 128  # PPO_COMM_ID_BYTES
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

@@ -15,8 +15,10 @@ from torch import nn
 
 from . import engine as E
 from .features import REFERENCE_CRITIC_HIDDEN, Run
+from .models import EngineActor, EngineCritic, move_to_flat
 
 ENGINE_RNG_FILE = "engine_rng_rank{rank}.pth"  # the per-rank torch generator of local data parallelism
+LEGACY_ENGINE_RNG_FILE = "engine_rng.pth"      # round-3 name (one file, holding its rank)
 
 
 def _dist_rank() -> int:
@@ -24,7 +26,6 @@ def _dist_rank() -> int:
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         return torch.distributed.get_rank()
     return 0
-from .models import EngineActor, EngineCritic, move_to_flat
 
 _ACT_NAMES = {nn.ReLU: "relu", nn.Tanh: "tanh", nn.ELU: "elu"}
 
@@ -335,6 +336,18 @@ class PPOEngineAgent:
         rank = algo.dp.rank if algo is not None else _dist_rank()
         rng_file = f"{path}/{ENGINE_RNG_FILE.format(rank=rank)}"
         state = torch.load(rng_file, weights_only=True) if os.path.exists(rng_file) else None
+        legacy = f"{path}/{LEGACY_ENGINE_RNG_FILE}"
+        if state is None and os.path.exists(legacy):
+            # a checkpoint written before the per-rank files: use it when it holds this rank's
+            # generator, otherwise say that this rank continues from a fresh seed
+            old = torch.load(legacy, weights_only=True)
+            if isinstance(old, dict) and old.get("rank") == rank:
+                state = old
+            else:
+                import warnings
+                warnings.warn(f"{legacy} holds rank {old.get('rank') if isinstance(old, dict) else '?'}'s "
+                              f"generator; rank {rank} continues from a freshly seeded one",
+                              stacklevel=2)
         if algo is not None:
             algo.set_rng_state(state)
         else:

@@ -43,6 +43,9 @@ class PPOEngine:
                                                            "local"))
         self.world = self.dp.world
         self.dp.broadcast_params(agent.flat_params)  # every replica starts from rank 0's params
+        eng = getattr(agent, "engine", None)
+        if eng is not None:  # native RCCL communicator on the ctx (RCCL groups), logged-loss share
+            self.dp.attach(eng, agent.device)
         agent._algorithm = self  # agent.save / load carry the per-rank generator (engine_rng_rank*.pth)
         self.set_rng_state(getattr(agent, "_loaded_rng_state", None))  # agent.load() before us
         agent._loaded_rng_state = None
@@ -378,7 +381,10 @@ class PPOEngine:
                         eng.minibatch_grad_staged(rows, b, agent.flat_grad, self._loss_buf[epoch, i],
                                                   clip_lo, clip_hi, ppo.entropy_eps, inv_b, inv_ba,
                                                   weights_current=k > 0, rows_gathered=k > 0)
-                        self.dp.allreduce_grad(agent.flat_grad)
+                        if self.dp.comm is not None:  # ppo_allreduce_grads: the ctx's comm
+                            eng.allreduce_grads(agent.flat_grad)
+                        else:
+                            self.dp.allreduce_grad(agent.flat_grad)
                         eng.adam_pack(agent.flat_grad, agent.flat_m, agent.flat_v, sched,
                                       one_minus_beta1=1 - beta1, beta2=beta2,
                                       one_minus_beta2=1 - beta2, eps=eps, next_rows=nxt)
@@ -399,8 +405,9 @@ class PPOEngine:
                     E.adam_sched(agent.flat_params, agent.flat_grad, agent.flat_m, agent.flat_v,
                                  eng.n_actor, sched, 1 - beta1, beta2, 1 - beta2, eps)
 
-        if self.dp.active or not getattr(self.run.engine_config, "train_graph", True):
-            body()  # collectives stay outside hipGraphs
+        if (self.dp.active and not self.dp.graph_safe or self.dp.rehearse and not self.dp.comm
+                or not getattr(self.run.engine_config, "train_graph", True)):
+            body()  # torch.distributed (gloo) collectives and the no-op rehearsal stay eager
             return self._loss_buf
         if self._tg_graph is None:
             if not self._tg_warm:  # first call eager: lazy workspace / timing setup outside capture
@@ -409,7 +416,10 @@ class PPOEngine:
                 return self._loss_buf
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # the native RCCL all-reduce (DataParallel.comm) is recorded like a kernel; its proxy
+            # threads keep running during capture, so only this thread's calls are checked
+            mode = "thread_local" if self.dp.comm is not None else "global"
+            with torch.cuda.graph(g, capture_error_mode=mode):
                 body()
             self._tg_graph = g
         self._tg_graph.replay()
@@ -501,8 +511,9 @@ class PPOEngine:
             # every rank's loss terms are already divided by the GLOBAL minibatch size
             # (DataParallel.loss_scale), so the SUM over ranks is the reference's per-minibatch
             # mean loss (ppo.py:139-153); one all-reduce per iteration, for logging only
+            # (rank 0's entries alone carry the entropy bonus: DataParallel.attach)
             loss_buf = loss_buf.clone()
-            self.dp.allreduce_grad(loss_buf)
+            self.dp.allreduce_log(loss_buf)
         losses = loss_buf.double().cpu()
         epoch_means = losses.mean(dim=1)
         actor_loss = float(epoch_means[:, 0].mean())

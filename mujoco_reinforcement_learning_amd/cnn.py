@@ -146,6 +146,10 @@ class CNNEngine:
         check(self.lib.ppo_cnn_bind_params(self._ctx, ptr(flat_params)))
         self._params = flat_params
 
+    def loss_entropy_share(self, share: float) -> None:
+        """Share of the entropy bonus in the LOGGED actor loss (ppo_cnn_loss_entropy_share)."""
+        check(self.lib.ppo_cnn_loss_entropy_share(self._ctx, float(share)))
+
     def set_precision(self, precision: str) -> None:
         if precision not in _lib.PREC_CODES:
             raise ValueError(f"unknown precision {precision!r}; use one of {sorted(_lib.PREC_CODES)}")

@@ -522,6 +522,7 @@ struct ppo_lstm_ctx {
   ppo_lstm_cfg cfg;
   int device;
   int prec;
+  float ent_log_share;  // ppo_*_loss_entropy_share (logged actor loss only)
   LstmNet net[2];  // 0 actor, 1 critic
   Mlp mu, ls, vc;  // actor mean / logstd MLPs, critic MLP
   int64_t total, n_actor;
@@ -948,6 +949,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   x->cfg = c;
   x->device = device;
   x->prec = PPO_PREC_F32;
+  x->ent_log_share = 1.f;
   x->fused_step = g_lstm_fused_step;
   const int H = c.latent, W = c.window, O = c.obs_dim, A = c.act_dim;
   int64_t off = 0;
@@ -1076,6 +1078,12 @@ extern "C" int ppo_lstm_bind_params(ppo_lstm_ctx *x, float *params_d) {
   return 0;
 }
 
+extern "C" int ppo_lstm_loss_entropy_share(ppo_lstm_ctx *x, float share) {
+  PPO_REQUIRE(x != nullptr, "ppo_lstm_loss_entropy_share: null ctx");
+  x->ent_log_share = share;
+  return 0;
+}
+
 extern "C" int ppo_lstm_set_precision(ppo_lstm_ctx *x, int prec) {
   PPO_REQUIRE(x != nullptr, "ppo_lstm_set_precision: null ctx");
   PPO_REQUIRE(prec == PPO_PREC_F32 || prec == PPO_PREC_BF16, "ppo_lstm_set_precision: %d", prec);
@@ -1195,7 +1203,8 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   PPO_LAUNCHED();
   if (loss_d) {
     launch_k(TimRec{KC_REDUCE, "lstm_loss_kernel", 0.0, 0.0}, lstm_loss_kernel, dim3(1),
-             dim3(256), 0, st, x->row_part, b, inv_b, inv_ba, entropy_coef, loss_d);
+             dim3(256), 0, st, x->row_part, b, inv_b, inv_ba, entropy_coef * x->ent_log_share,
+             loss_d);
     PPO_LAUNCHED();
   }
   {  // critic: MLP, then BiLSTM (the gradient of h at t = W-1 lands in dy[0])

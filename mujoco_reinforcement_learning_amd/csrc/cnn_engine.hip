@@ -259,6 +259,7 @@ struct ppo_cnn_ctx {
   ppo_cnn_cfg cfg;
   int device;
   int prec;
+  float ent_log_share;  // ppo_*_loss_entropy_share (logged actor loss only)
   ConvParams conv[2][3];   // per net, per encoder layer
   int64_t logstd_off;
   Mlp mlp[2];              // actor mean MLP, critic MLP (input: 3136 features)
@@ -845,6 +846,7 @@ extern "C" int ppo_cnn_ctx_create(const ppo_cnn_cfg *cfg, int device, ppo_cnn_ct
   x->cfg = c;
   x->device = device;
   x->prec = PPO_PREC_F32;
+  x->ent_log_share = 1.f;
   const int A = c.act_dim;
   int64_t off = 0;
   // actor: actor_logstd (the module's own parameter comes first in parameters()), encoder, MLP
@@ -966,6 +968,12 @@ extern "C" int ppo_cnn_bind_params(ppo_cnn_ctx *x, float *params_d) {
   PPO_REQUIRE(reinterpret_cast<uintptr_t>(params_d) % 64 == 0,
               "ppo_cnn_bind_params: parameter buffer must be 64-B aligned");
   x->params = params_d;
+  return 0;
+}
+
+extern "C" int ppo_cnn_loss_entropy_share(ppo_cnn_ctx *x, float share) {
+  PPO_REQUIRE(x != nullptr, "ppo_cnn_loss_entropy_share: null ctx");
+  x->ent_log_share = share;
   return 0;
 }
 
@@ -1126,7 +1134,7 @@ extern "C" int ppo_cnn_minibatch_grad(ppo_cnn_ctx *x, const uint8_t *frames_d,
   r.inv_b = inv_b;
   r.logstd = x->params + x->logstd_off;
   r.act_dim = A;
-  r.ent_coef = entropy_coef;
+  r.ent_coef = entropy_coef * x->ent_log_share;
   r.loss_out = loss_d;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 0.0}, cnn_reduce_kernel,
            dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);

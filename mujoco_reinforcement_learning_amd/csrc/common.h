@@ -132,11 +132,13 @@ __device__ __forceinline__ float philox_normal_at(uint64_t seed, uint64_t idx) {
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // outstanding global loads and stores (__syncthreads drains vmcnt, so a prefetch meant to stay in
-// flight across a phase, or a store nobody in the workgroup reads, stalls every barrier).
+// flight across a phase, or a store nobody in the workgroup reads, stalls every barrier).  The
+// wait and the barrier are ONE asm statement with a memory clobber (CK's block_sync_lds form): the
+// compiler can neither put a memory operation between them nor move one across the pair in either
+// direction; the scheduling barriers keep the machine scheduler from doing the same.
 __device__ __forceinline__ void lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 

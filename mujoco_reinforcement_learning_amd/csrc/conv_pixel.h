@@ -128,13 +128,8 @@ __device__ __forceinline__ int pix_block(int p) {
 // Workgroup barrier for the per-image LDS hand-offs: waits for this wave's LDS operations only.
 // __syncthreads() is a workgroup-scope release / acquire, which also waits for every global load
 // and store the wave has in flight -- the next image's prefetch and this image's output stores --
-// and serialised one memory round trip per image.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
+// and serialised one memory round trip per image.  The same barrier as common.h's lds_sync.
+__device__ __forceinline__ void lds_barrier() { lds_sync(); }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

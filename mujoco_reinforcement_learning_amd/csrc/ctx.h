@@ -60,6 +60,13 @@ struct ppo_ctx {
   int fstamp_on, fstamp_g;
   int fused4;                   // ppo_ctx_fused_variant: 1 -> fused_update4_kernel (ReLU)
   int fdirect;                  // ppo_ctx_fused_direct: the 8-wave kernel reads staged records via rows
+  // which minibatch the gathered copy (fxb / fsrow) holds: the rows_d pointer and count of the
+  // last staged gather (prep or step tail), nullptr when unknown -- PPO_STAGED_ROWS_GATHERED is
+  // honoured only when it names exactly these rows, otherwise the entry point gathers again
+  const int32_t *fg_rows;
+  int fg_b;
   ppo::WideWork *wide;          // wide bf16-resident layered path (wide_path.h), or null
+  ppo_comm *comm;               // data-parallel communicator (ppo_ctx_set_comm; not owned)
+  float ent_log_share;          // ppo_ctx_loss_entropy_share (logged actor loss only)
   ppo::Timing tim;
 };

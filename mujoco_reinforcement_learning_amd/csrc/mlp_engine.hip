@@ -782,6 +782,17 @@ static int fused_prep(const ppo_ctx *ctx, const FusedArgs &q, hipStream_t st) {
   return fused_prep_launch(q, rec, st);
 }
 
+// The gathered-copy record (ctx.h fg_rows): a caller's PPO_STAGED_ROWS_GATHERED is a promise
+// about stream order that nothing on the device checks, so the host keeps which rows the last
+// staged gather wrote and gathers again when the promise names other rows.
+static bool gathered_holds(const ppo_ctx *ctx, const int32_t *rows_d, int b) {
+  return rows_d != nullptr && ctx->fg_rows == rows_d && ctx->fg_b == b;
+}
+static void note_gathered(ppo_ctx *ctx, const int32_t *rows_d, int b) {
+  ctx->fg_rows = rows_d;
+  ctx->fg_b = rows_d ? b : 0;
+}
+
 static int fused_forward_backward(ppo_ctx *ctx, const FusedArgs &q, hipStream_t st) {
   const int H = ctx->fused_hidden, din = q.din, A = q.act_dim, b = q.b;
   const int64_t P = ctx->total_params;
@@ -838,7 +849,7 @@ static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, floa
   r.inv_b = q.inv_b;
   r.logstd = ctx->params + ctx->net[0].logstd_off;
   r.act_dim = A;
-  r.ent_coef = q.ent_coef;
+  r.ent_coef = q.ent_coef * ctx->ent_log_share;
   r.loss_out = loss_d;
   return r;
 }
@@ -853,10 +864,12 @@ static int fused_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float
   const FusedArgs q = fused_args(ctx, states_d, actions_d, old_logp_d, adv_d, vtarget_d, rows_d,
                                  b, count_d, clip_lo, clip_hi, entropy_coef, inv_b, inv_ba,
                                  staged, pack_w);
+  gathered = gathered && staged && gathered_holds(ctx, rows_d, b);
   if ((!gathered && !q.direct) || pack_w) {
     FusedArgs p = q;
     p.b = (gathered || q.direct) ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
+    if (p.b > 0) note_gathered(ctx, staged && count_d == nullptr ? rows_d : nullptr, b);
   }
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
@@ -927,6 +940,7 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
   PPO_REQUIRE(ctx != nullptr, "ppo_ctx_create: out of host memory");
   ctx->cfg = *cfg;
   ctx->device = device;
+  ctx->ent_log_share = 1.f;
   const int din = cfg->obs_dim * cfg->window;
   int64_t off = 0;
   int64_t ws_floats = 0;
@@ -1228,6 +1242,7 @@ extern "C" int ppo_stage_records(ppo_ctx *ctx, const float *states_d, const floa
   if (int rc = check_ctx(ctx)) return rc;
   PPO_REQUIRE(fused_active(ctx), "ppo_stage_records: needs the fused bf16 path "
                                  "(ppo_ctx_fused_active)");
+  note_gathered(ctx, nullptr, 0);  // new records: any gathered copy is stale
   PPO_REQUIRE(states_d && actions_d && old_logp_d && adv_d && vtarget_d && n_rows > 0,
               "ppo_stage_records: null buffer or n_rows <= 0");
   hipStream_t st = as_stream(stream);
@@ -1251,6 +1266,7 @@ extern "C" int ppo_gae_stage_records(ppo_ctx *ctx, const float *value_d,
   if (int rc = check_ctx(ctx)) return rc;
   PPO_REQUIRE(fused_active(ctx), "ppo_gae_stage_records: needs the fused bf16 path "
                                  "(ppo_ctx_fused_active)");
+  note_gathered(ctx, nullptr, 0);  // new records: any gathered copy is stale
   PPO_REQUIRE(value_d && next_value_d && reward_d && terminated_d && adv_d && vtarget_d &&
                   states_d && actions_d && old_logp_d,
               "ppo_gae_stage_records: null buffer");
@@ -1342,6 +1358,7 @@ extern "C" int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, 
                                                0.f, true, false).direct;
   t.b = direct ? 0 : next_b;
   t.reduce = false;
+  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
   ReduceArgs r{};
   r.total = ctx->total_params;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
@@ -1360,7 +1377,9 @@ extern "C" int ppo_gather_staged_rows(ppo_ctx *ctx, const int32_t *rows_d, int b
   TimingScope timing_scope(ctx);
   const FusedArgs q = fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b,
                                  nullptr, 0.f, 0.f, 0.f, 0.f, 0.f, true, false);
-  return fused_prep(ctx, q, as_stream(stream));
+  if (int rc = fused_prep(ctx, q, as_stream(stream))) return rc;
+  note_gathered(ctx, rows_d, b);
+  return 0;
 }
 
 extern "C" int ppo_adam_pack(ppo_ctx *ctx, const float *g_d, float *m_d, float *v_d,
@@ -1400,7 +1419,7 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
               "ppo_update_step_staged: flags %d", flags);
   hipStream_t st = as_stream(stream);
   TimingScope timing_scope(ctx);
-  const bool gathered = flags & PPO_STAGED_ROWS_GATHERED;
+  const bool gathered = (flags & PPO_STAGED_ROWS_GATHERED) && gathered_holds(ctx, rows_d, b);
   const bool current = flags & PPO_STAGED_WEIGHTS_CURRENT;
   FusedArgs q = fused_args(ctx, nullptr, nullptr, nullptr, nullptr, nullptr, rows_d, b, nullptr,
                            clip_lo, clip_hi, entropy_coef, inv_b, inv_ba, true, !current);
@@ -1408,6 +1427,7 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
     FusedArgs p = q;
     p.b = (gathered || q.direct) ? 0 : b;
     if (int rc = fused_prep(ctx, p, st)) return rc;
+    if (p.b > 0) note_gathered(ctx, rows_d, b);
   }
   // tail: slab reduction + Adam + weight images, and the next minibatch's row gather
   const ReduceArgs r = fused_reduce_args(ctx, q, grad_d, loss_d);
@@ -1421,6 +1441,7 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.srow = ctx->fsrow;
   t.b = q.direct ? 0 : next_b;  // direct: the next fused launch reads its rows itself
   t.reduce = true;
+  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
   if (int rc = fused_forward_backward(ctx, q, st)) return rc;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
@@ -1763,7 +1784,7 @@ extern "C" int ppo_minibatch_grad(ppo_ctx *ctx, const float *states_d, const flo
   r.inv_b = inv_b;
   r.logstd = ctx->params + NA.logstd_off;
   r.act_dim = A;
-  r.ent_coef = entropy_coef;
+  r.ent_coef = entropy_coef * ctx->ent_log_share;
   r.loss_out = loss_d;
   launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", static_cast<double>(splits) * P,
                   4.0 * (static_cast<double>(splits) + 1) * P},
@@ -1808,6 +1829,13 @@ extern "C" int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant) {
   if (variant < 0) return ctx->fused4 ? 4 : 8;
   PPO_REQUIRE(variant == 4 || variant == 8, "ppo_ctx_fused_variant: variant %d (4 or 8)", variant);
   ctx->fused4 = variant == 4;
+  note_gathered(ctx, nullptr, 0);
+  return 0;
+}
+
+extern "C" int ppo_ctx_loss_entropy_share(ppo_ctx *ctx, float share) {
+  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_loss_entropy_share: null ctx");
+  ctx->ent_log_share = share;
   return 0;
 }
 
@@ -1815,6 +1843,7 @@ extern "C" int ppo_ctx_fused_direct(ppo_ctx *ctx, int enable) {
   PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_direct: null ctx");
   if (enable < 0) return ctx->fdirect ? 1 : 0;
   ctx->fdirect = enable != 0;
+  note_gathered(ctx, nullptr, 0);
   return 0;
 }
 

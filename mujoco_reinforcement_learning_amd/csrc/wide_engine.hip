@@ -1523,7 +1523,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   r.inv_b = inv_b;
   r.logstd = ctx->params + NA.logstd_off;
   r.act_dim = A;
-  r.ent_coef = entropy_coef;
+  r.ent_coef = entropy_coef * ctx->ent_log_share;
   r.loss_out = loss_d;
   double slab_floats = 0;
   for (int i = 0; i < ns; ++i) slab_floats += static_cast<double>(r.seg[i].nsplit) * r.seg[i].len;

@@ -125,6 +125,22 @@ class Engine:
                                        ptr(action), ptr(logp), ptr(value), ptr(mean),
                                        _stream(self.device)))
 
+    def set_comm(self, comm) -> None:
+        """Attach a ``distributed.NativeComm`` to the ctx (``ppo_ctx_set_comm``); None detaches."""
+        check(self.lib.ppo_ctx_set_comm(self._ctx, None if comm is None else comm.handle))
+        self._comm = comm  # the ctx does not own it: keep it alive as long as the ctx uses it
+
+    def allreduce_grads(self, flat_grad: torch.Tensor) -> None:
+        """``ppo_allreduce_grads``: SUM of the flat gradient over the attached
+        communicator's ranks, in place, on the current stream."""
+        _need(flat_grad, "flat_grad", torch.float32, (self.n_params,), self.device)
+        check(self.lib.ppo_allreduce_grads(self._ctx, ptr(flat_grad), flat_grad.numel(),
+                                           _stream(self.device)))
+
+    def loss_entropy_share(self, share: float) -> None:
+        """Share of the entropy bonus in the LOGGED actor loss (ppo_ctx_loss_entropy_share)."""
+        check(self.lib.ppo_ctx_loss_entropy_share(self._ctx, float(share)))
+
     def pack_weights(self) -> None:
         """Refresh the bf16 weight images of the fused kernels from the bound parameters (after
         an optimizer step, before a rollout).  No-op outside the fused bf16 path."""

@@ -94,6 +94,10 @@ class LSTMEngine:
         check(self.lib.ppo_lstm_bind_params(self._ctx, ptr(flat_params)))
         self._params = flat_params
 
+    def loss_entropy_share(self, share: float) -> None:
+        """Share of the entropy bonus in the LOGGED actor loss (ppo_lstm_loss_entropy_share)."""
+        check(self.lib.ppo_lstm_loss_entropy_share(self._ctx, float(share)))
+
     def set_precision(self, precision: str) -> None:
         if precision not in _lib.PREC_CODES:
             raise ValueError(f"unknown precision {precision!r}; use one of {sorted(_lib.PREC_CODES)}")

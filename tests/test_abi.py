@@ -51,3 +51,20 @@ def test_bad_arguments_return_einval_with_message():
     assert b"act_dim" in lib.ppo_last_error()
     with pytest.raises(_lib.EngineError, match="act_dim"):
         _lib.check(-22)
+
+
+def test_comm_entry_points_resolve_rccl_and_check_arguments():
+    """The data-parallel exchange (comm.hip, SURVEY.md s8(b) ppo_allreduce_grads): RCCL resolves
+    at run time (the instance torch loaded, else ROCm's), a unique id can be drawn without a GPU,
+    and bad arguments fail with EINVAL before any collective."""
+    lib = _lib.load()
+    assert lib.ppo_comm_version() >= 22000  # NCCL_VERSION_CODE 2.20+
+    uid = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    assert lib.ppo_comm_unique_id(uid) == 0
+    assert any(bytes(uid))
+    handle = ctypes.c_void_p()
+    assert lib.ppo_comm_create(uid, 2, 2, 0, ctypes.byref(handle)) == -22
+    assert b"rank 2 of 2" in lib.ppo_last_error()
+    assert lib.ppo_allreduce_grads(None, None, 4, None) == -22
+    assert lib.ppo_comm_allreduce(None, None, 4, None) == -22
+    assert lib.ppo_ctx_loss_entropy_share(None, 0.0) == -22

@@ -42,26 +42,26 @@ def _run(n_envs, shard, dp_mode, dev, capture=False):
     mem = algo.rollout()
     algo.calculate_advantages(mem)
     grads = capture_engine_grads(algo) if capture else None
-    algo.train(mem)
+    algo._finish_logging(algo.train(mem))  # the logged losses: all-reduced over the ranks
     if capture:
-        return agent.packed_params().cpu(), mem["advantage"].cpu(), grads, agent
-    return agent.packed_params().cpu(), mem["advantage"].cpu()
+        return agent.packed_params().cpu(), mem["advantage"].cpu(), grads, agent, algo.last_losses
+    return agent.packed_params().cpu(), mem["advantage"].cpu(), algo.last_losses
 
 
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     n_local = N_GLOBAL // world
-    params, adv = _run(n_local, (rank * n_local, (rank + 1) * n_local), "exact",
-                       torch.device("cuda", 0))
-    q.put((rank, params, adv))
+    params, adv, losses = _run(n_local, (rank * n_local, (rank + 1) * n_local), "exact",
+                               torch.device("cuda", 0))
+    q.put((rank, params, adv, losses))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
 
 def test_exact_dp_two_ranks_match_single_process(gpu):
-    p_single, adv_single, g_single, agent = _run(N_GLOBAL, (0, N_GLOBAL), "local", gpu,
-                                                 capture=True)
+    p_single, adv_single, g_single, agent, loss_single = _run(N_GLOBAL, (0, N_GLOBAL), "local",
+                                                              gpu, capture=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     s = socket.socket()
@@ -73,8 +73,8 @@ def test_exact_dp_two_ranks_match_single_process(gpu):
         p.start()
     got = {}
     for _ in range(2):
-        r, params, adv = q.get(timeout=300)
-        got[r] = (params, adv)
+        r, params, adv, losses = q.get(timeout=300)
+        got[r] = (params, adv, losses)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -86,6 +86,12 @@ def test_exact_dp_two_ranks_match_single_process(gpu):
     # the single process is the reference here: rtol 1e-5 except the counted Adam sign-flip-prone
     # set (gradient below 1e-3 of its tensor's max at some step; tests/parity_util.py)
     assert_params_match(got[0][0], p_single, g_single, agent, 1e-4, label="exact DP x2")
+    # the logged losses (ppo.py:139-153): every rank reports the SUM over ranks of its shard's
+    # terms, with the entropy bonus counted once (rank 0's share), i.e. the single process's loss
+    print(f"exact DP x2 losses {got[0][2]} {got[1][2]} vs single {loss_single}")
+    assert got[0][2] == got[1][2]
+    for a, b in zip(got[0][2], loss_single):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (got[0][2], loss_single)
 
 
 _LOCAL_SHAPES = {  # name -> (hidden, obs, act)
@@ -282,3 +288,88 @@ def test_bench_self_launches_two_ranks_on_one_gpu(gpu):
     print(f"bench --gpus 2 (one GPU, gloo): {rec['value']:.4g} env-steps/s, "
           f"{rec['ms_per_step']:.2f} ms/step")
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["steps"] == 2
+
+
+def _graph_dp_worker(q):
+    """World-1 nccl process group: the data-parallel step sequence (fused gradient -> native RCCL
+    all-reduce -> Adam tail) captured in one hipGraph (PPO_DP_REHEARSE=rccl) against the same
+    sequence run eagerly with a no-op exchange (PPO_DP_REHEARSE=1), then the all-reduce's per-call
+    cost on this GPU at the 2x256 and Humanoid 3x512 flat-gradient sizes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                      WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.distributed.init_process_group("nccl", device_id=dev)
+    from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
+    from mujoco_reinforcement_learning_amd.algorithm import PPOEngine
+    from mujoco_reinforcement_learning_amd.environments import (SyntheticVecEnvHelper,
+                                                                make_synthetic_streams)
+    from mujoco_reinforcement_learning_amd.runconfig import make_run
+    out = {}
+    for mode in ("1", "rccl"):
+        os.environ["PPO_DP_REHEARSE"] = mode
+        s = make_synthetic_streams(64, 16, 17, seed=41, p_terminate=0.05, device=dev)
+        run = make_run(num_envs=64, horizon=16, hidden=(256, 256), batch_size=256, epochs=2,
+                       rng="philox", seed=3, dp_mode="local", precision="bf16")
+        torch.manual_seed(0)
+        agent = PPOEngineAgent(run, device=dev)
+        algo = PPOEngine(SyntheticVecEnvHelper(s, run, device=dev), agent, log=lambda m: None)
+        for _ in range(3):  # eager warm-up, capture + replay, replay
+            algo.iterate(verbose=False)
+        torch.cuda.synchronize()
+        out[mode] = (agent.packed_params().cpu(), algo.dp.comm is not None,
+                     getattr(algo, "_tg_graph", None) is not None, algo.last_losses)
+        if algo.dp.comm is not None:
+            algo.dp.comm.check()
+            comm = algo.dp.comm
+    del os.environ["PPO_DP_REHEARSE"]
+    # per-call cost of the native all-reduce (world 1: RCCL's launch / proxy floor)
+    times = {}
+    for n in (142605, 1445923):  # 2x256 HalfCheetah, 3x512 Humanoid flat gradients
+        x = torch.ones(n, dtype=torch.float32, device=dev)
+        for _ in range(20):
+            comm.allreduce(x)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            comm.allreduce(x)
+        e1.record()
+        torch.cuda.synchronize()
+        eager_us = e0.elapsed_time(e1) * 1e3 / 200
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for _ in range(100):
+                comm.allreduce(x)
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        times[n] = (eager_us, e0.elapsed_time(e1) * 1e3 / 100, bool(torch.all(x == 1.0)))
+    q.put((out, times))
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_step_graph_captured_with_rccl_allreduce(gpu):
+    """VERDICT r04 item 4 / SURVEY s8(e): the data-parallel optimizer loop with the native RCCL
+    all-reduce (csrc/comm.hip, ppo_allreduce_grads on the ctx's communicator) captured inside the
+    hipGraph is bitwise equal to the eager DP sequence; per-call all-reduce times printed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_dp_worker, args=(q,))
+    p.start()
+    out, times = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    p_eager, comm_eager, graph_eager, loss_eager = out["1"]
+    p_graph, comm_graph, graph_graph, loss_graph = out["rccl"]
+    assert not comm_eager and not graph_eager
+    assert comm_graph and graph_graph, "the rccl rehearsal did not capture the DP loop"
+    assert torch.equal(p_eager, p_graph)
+    assert loss_eager == loss_graph
+    for n, (eager_us, graph_us, ok) in times.items():
+        print(f"native RCCL all-reduce, world 1, {n * 4 / 1e6:.2f} MB: eager {eager_us:.2f} us, "
+              f"in a hipGraph {graph_us:.2f} us per call")
+        assert ok
