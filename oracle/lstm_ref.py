@@ -33,20 +33,33 @@ from typing import List, Sequence
 import torch
 from torch import nn
 
-from .ppo_ref import ACTIVATIONS, MLPBlock, RefConfig
+from .ppo_ref import ACTIVATIONS, MLPBlock, RefConfig, _BF16Linear, use_bf16_gemms as _mlp_bf16
 
 
-def lstm_direction(x: torch.Tensor, w_ih, w_hh, b_ih, b_hh, reverse: bool) -> torch.Tensor:
-    """One direction of one layer over x (B, W, I) -> h (B, W, L) (torch CPU LSTM cell order)."""
+def _linear(x, w, b, bf16: bool):
+    """torch's F.linear, or the bf16-operand product of the engine's PPO_PREC_BF16 mode
+    (ppo_ref._BF16Linear: both operands rounded to bf16, accumulation in x's dtype, f32 bias and
+    bias gradient) -- not a reference behaviour."""
+    if not bf16:
+        return torch.nn.functional.linear(x, w, b)
+    lead = x.shape[:-1]
+    return _BF16Linear.apply(x.reshape(-1, x.shape[-1]), w, b).reshape(*lead, w.shape[0])
+
+
+def lstm_direction(x: torch.Tensor, w_ih, w_hh, b_ih, b_hh, reverse: bool,
+                   bf16: bool = False) -> torch.Tensor:
+    """One direction of one layer over x (B, W, I) -> h (B, W, L) (torch CPU LSTM cell order).
+    bf16=True: every GEMM of the layer (input projection, per-step recurrent projection, and so
+    their backward dgrad / wgrad) on bf16-rounded operands; the cells stay in x's dtype."""
     b, w, _ = x.shape
     hidden = w_hh.shape[1]
-    gx = torch.nn.functional.linear(x, w_ih, b_ih)  # every step's input projection at once
+    gx = _linear(x, w_ih, b_ih, bf16)  # every step's input projection at once
     h = x.new_zeros(b, hidden)
     c = x.new_zeros(b, hidden)
     out: List[torch.Tensor] = [None] * w
     steps = range(w - 1, -1, -1) if reverse else range(w)
     for t in steps:
-        gates = torch.nn.functional.linear(h, w_hh, b_hh) + gx[:, t]
+        gates = _linear(h, w_hh, b_hh, bf16) + gx[:, t]
         i, f, g, o = gates.chunk(4, 1)
         i, f, g, o = i.sigmoid(), f.sigmoid(), g.tanh(), o.sigmoid()
         c = f * c + i * g
@@ -58,12 +71,13 @@ def lstm_direction(x: torch.Tensor, w_ih, w_hh, b_ih, b_hh, reverse: bool) -> to
 def bilstm(x: torch.Tensor, lstm: nn.LSTM) -> torch.Tensor:
     """Multi-layer bidirectional LSTM over x (B, W, I) with ``lstm``'s parameters -> (B, W, 2L)."""
     y = x
+    bf16 = bool(getattr(lstm, "_ppo_bf16", False))  # set by use_bf16_gemms
     for layer in range(lstm.num_layers):
         outs = []
         for rev, sfx in ((False, ""), (True, "_reverse")):
             p = [getattr(lstm, f"{n}_l{layer}{sfx}") for n in ("weight_ih", "weight_hh", "bias_ih",
                                                                 "bias_hh")]
-            outs.append(lstm_direction(y, *p, reverse=rev))
+            outs.append(lstm_direction(y, *p, reverse=rev, bf16=bf16))
         y = torch.cat(outs, dim=2)
     return y
 
@@ -177,3 +191,26 @@ def minibatch_grads(agent, states, actions, old_logp, adv, vt, clip_epsilon: flo
 
 def param_names(agent) -> Sequence[str]:
     return [f"{k}.{n}" for k in ("actor", "critic") for n, _ in agent.networks[k].named_parameters()]
+
+
+# ---- bf16 GEMM emulation of the BiLSTM agent (engine precision "bf16"; not a reference behaviour)
+def use_bf16_gemms(agent: RefLSTMAgent) -> None:
+    """Switch every product of both nets to the engine's PPO_PREC_BF16 arithmetic
+    (csrc/bilstm.hip: every GEMM rounds both operands to bf16, RNE, and accumulates in f32; bias
+    adds, the LSTM cells, activations, the distribution and the losses stay f32):
+      * the BiLSTMs (lstm_actor.py:12-16, lstm_critic.py:19-23): the input projection X W_ih^T, the
+        per-step recurrent projection h W_hh^T, and through autograd their backward products
+        (dG W_hh, dG W_ih, dG^T X, dG^T h_prev) on bf16(dG); bias gradients from the f32 dG;
+      * the MLP heads (NetworkBlock, lstm_actor.py:17-38, lstm_critic.py:24-31): ppo_ref's
+        _BF16Linear on every Linear.
+    Run it on an agent cast to float64 (``agent.networks.double()`` with f64 inputs) for the
+    f64-accumulated emulation the bf16 kernels are held to: the same bf16-rounded operands, sums
+    without f32 rounding."""
+    nets = agent.networks
+    for lstm in (nets["actor"].feature_extractor, nets["critic"].feature_extractor[0]):
+        lstm._ppo_bf16 = True
+    blocks = (nets["actor"].actor, nets["actor"].actor_logstd, nets["critic"].network)
+    for blk in blocks:
+        for mod in list(blk.first_layers) + [blk.last_layer]:
+            if isinstance(mod, nn.Linear):
+                mod.forward = (lambda m: (lambda x: _BF16Linear.apply(x, m.weight, m.bias)))(mod)

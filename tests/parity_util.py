@@ -501,3 +501,154 @@ def stepwise_parity(algo, agent, ref, cfg, ref_mem, steps: List[dict], rows: Lis
             (label, k, totals)
     print(f"stepwise parity {label}: {totals}")
     return totals
+
+
+# ------------------------------------------------------------------------------------------------
+# bf16 step-wise parity: the engine's bf16 kernels (precision "bf16") restarted at every optimizer
+# step from the bf16-EMULATION oracle's own state and held to that step's gradient evaluated by the
+# f64-accumulated emulation (the same bf16-rounded operands, sums without f32 rounding).  What is
+# left is the engine's f32 summation order flipping a bf16 rounding of an intermediate (1 bf16 ulp
+# = 2^-8 relative), which cascades through the layers; the fixed bars below sit at ~3x the
+# emulation's own f32-vs-f64 spread at these shapes.
+# ------------------------------------------------------------------------------------------------
+WELL_DETERMINED = 1e-2  # bf16 step-wise: |g| >= 1e-2 of the tensor's max has a determined sign
+
+
+def load_packed(nets, p_packed: torch.Tensor) -> None:
+    """Copy a parameters()-order vector into a ModuleDict's parameters (any float dtype)."""
+    off = 0
+    with torch.no_grad():
+        for p in nets.parameters():
+            p.copy_(p_packed[off:off + p.numel()].view(p.shape).to(p.dtype))
+            off += p.numel()
+
+
+def bf16_f64_grad(ref0, mem, rows: torch.Tensor, cfg, p_packed=None, bf16_fn=None,
+                  state_dtype=torch.float64) -> torch.Tensor:
+    """The minibatch gradient of ppo.py:109-135 under the bf16 emulation accumulated in float64,
+    at parameters ``p_packed`` (default: ``ref0``'s) on storage rows ``rows`` (t*N + n) of a
+    reference-layout (N, T, ...) buffer ``mem``.  ``bf16_fn`` switches an agent to the emulation
+    (oracle.ppo_ref.use_bf16_gemms, oracle.lstm_ref.use_bf16_gemms, oracle.cnn_ref.use_bf16);
+    ``state_dtype`` None passes the stored states as they are (u8 pixel frames, whose scaling
+    the caller routes to f64)."""
+    import copy
+    n, t = cfg.num_envs, cfg.horizon
+    ref = copy.deepcopy(ref0)
+    if p_packed is not None:
+        load_packed(ref.networks, p_packed)
+    (bf16_fn or R.use_bf16_gemms)(ref)
+    ref.networks.to(torch.float64)
+    r = rows.long()
+    em = (r % n) * t + r // n  # storage row t*N + n -> the reference's env-major n*T + t
+    flat = {k: mem[k].cpu().reshape(n * t, *mem[k].shape[2:]) for k in
+            ("current_state", "action", "action_log_prob", "advantage",
+             "current_state_value_target")}
+    x = flat["current_state"][em]
+    x = x.to(state_dtype) if state_dtype is not None else x
+    _, dist = ref.act(x, return_dist=True)
+    new_lp = dist.log_prob(flat["action"][em].double()).sum(dim=1)
+    v = ref.get_state_value(x)
+    vt = flat["current_state_value_target"][em].double().reshape(v.shape)
+    lc = torch.nn.functional.huber_loss(v, vt, reduction="mean")
+    ratio = (new_lp - flat["action_log_prob"][em].double().reshape(new_lp.shape)).exp()[:, None]
+    a_ = flat["advantage"][em].double().reshape(ratio.shape)
+    la = -torch.min(ratio * a_, torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon)
+                    * a_).mean() - dist.entropy().mean() * cfg.entropy_eps
+    ref.networks.zero_grad()
+    (la + lc).backward()
+    return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).flatten()
+                      for p in ref.networks.parameters()])
+
+
+def grad_errors(g_eng: torch.Tensor, g64: torch.Tensor, ref) -> List[tuple]:
+    """(name, max |err| / max |g64|, rel L2) per parameter tensor (all-zero tensors skipped)."""
+    out = []
+    for name, lo, hi in tensor_slices(ref):
+        gr = g64[lo:hi]
+        if float(gr.abs().max()) == 0.0:
+            assert float(g_eng[lo:hi].abs().max()) == 0.0, name
+            continue
+        ge = g_eng[lo:hi].double()
+        out.append((name, float((ge - gr).abs().max()) / float(gr.abs().max()),
+                    float((ge - gr).norm() / gr.norm())))
+    return out
+
+
+def bf16_stepwise(agent, ref0, cfg, ref_mem, steps: List[dict], rows: List[torch.Tensor],
+                  max_bar: float, l2_bar: float, update_bar: float, bf16_fn=None,
+                  label: str = "", grad_fn=None) -> dict:
+    """For every recorded step k of the bf16-emulation oracle (``steps``: record_oracle_steps,
+    ``rows``: replay_rows): load the oracle's (p, m, v, step count, lr) into the engine, run the
+    engine's bf16 minibatch gradient on the ORACLE's rollout buffer with step k's rows, then its
+    Adam step.  Bars per tensor: the gradient against bf16_f64_grad at the same parameters within
+    ``max_bar`` of the tensor's max and ``l2_bar`` relative L2; the parameter update (post - pre)
+    against the oracle's own within ``update_bar`` relative L2 over the elements whose gradient
+    sign is determined (|g| >= WELL_DETERMINED of the tensor's max), every element within 2*lr
+    (Adam's step is scale-free: an element whose gradient is small against its tensor's max takes
+    a full-size step whose sign follows the bf16 rounding noise).  Returns the observed maxima,
+    beside the emulation's own f32-vs-f64 spread at the same states (rec["g"] is the
+    f32-accumulated emulation's gradient)."""
+    dev = agent.device
+    n, t = cfg.num_envs, cfg.horizon
+    tm = lambda x: x.transpose(0, 1).reshape(t * n, *x.shape[2:]).contiguous().to(dev)
+    states = tm(ref_mem["current_state"].reshape(n, t, -1))
+    actions = tm(ref_mem["action"])
+    old_lp = tm(ref_mem["action_log_prob"])
+    adv = tm(ref_mem["advantage"][..., 0])
+    vt = tm(ref_mem["current_state_value_target"][..., 0])
+    b = cfg.batch_size
+    eng = agent.engine
+    grad = torch.empty(eng.n_params, device=dev)
+    loss = torch.empty(2, device=dev)
+    obs = {"steps": len(steps), "grad_max": 0.0, "grad_l2": 0.0, "update_l2": 0.0,
+           "param_max_abs_over_lr": 0.0}
+    bad = []
+    for k, (rec, r) in enumerate(zip(steps, rows)):
+        _to_flat(agent, rec["p"], agent.flat_params)
+        agent.flat_m.zero_()
+        agent.flat_v.zero_()
+        _to_flat(agent, rec["m"], agent.flat_m)
+        _to_flat(agent, rec["v"], agent.flat_v)
+        for name in ("actor", "critic"):
+            agent.optimizers[name].step_count = rec["k"]
+            agent.optimizers[name].param_groups[0]["lr"] = rec["lr"]
+        if hasattr(eng, "pack_weights"):
+            eng.pack_weights()
+        eng.minibatch_grad(states, actions, old_lp, adv, vt, r.to(dev), b, grad, loss,
+                           1.0 - cfg.clip_epsilon, 1.0 + cfg.clip_epsilon, cfg.entropy_eps,
+                           1.0 / b, 1.0 / (b * cfg.act_dim))
+        agent.flat_grad.copy_(grad)
+        g_eng = agent.packed(grad).cpu()
+        g64 = (grad_fn or bf16_f64_grad)(ref0, ref_mem, r, cfg, p_packed=rec["p"], bf16_fn=bf16_fn)
+        own = {nm: (e, l) for nm, e, l in grad_errors(rec["g"], g64, ref0)}
+        err_of = {}
+        for name, err, l2 in grad_errors(g_eng, g64, ref0):
+            err_of[name] = err
+            obs["grad_max"] = max(obs["grad_max"], err)
+            obs["grad_l2"] = max(obs["grad_l2"], l2)
+            obs["emulation_spread_max"] = max(obs.get("emulation_spread_max", 0.0), own[name][0])
+            obs["emulation_spread_l2"] = max(obs.get("emulation_spread_l2", 0.0), own[name][1])
+            if err > max_bar or l2 > l2_bar:
+                bad.append(("grad", k, name, err, l2, own[name]))
+        agent.step_both()
+        p_eng = agent.packed_params().cpu()
+        obs["param_max_abs_over_lr"] = max(obs["param_max_abs_over_lr"],
+                                           float((p_eng - rec["p_after"]).abs().max()) / rec["lr"])
+        for name, lo, hi in tensor_slices(ref0):
+            du_e = p_eng[lo:hi] - rec["p"][lo:hi]
+            du_r = rec["p_after"][lo:hi] - rec["p"][lo:hi]
+            # the update bar holds where the gradient's sign is determined (|g| >= WELL of the
+            # tensor's max in the f64 emulation); the rest are counted, bounded by 2*lr above
+            g = g64[lo:hi].abs()
+            well = g >= max(WELL_DETERMINED, 3 * err_of.get(name, 0.0)) * float(g.max())
+            obs["sign_free_elements"] = obs.get("sign_free_elements", 0) + int((~well).sum())
+            if float(du_r[well].norm()) == 0.0:
+                continue
+            u = float((du_e[well] - du_r[well]).norm() / du_r[well].norm())
+            obs["update_l2"] = max(obs["update_l2"], u)
+            if u > update_bar:
+                bad.append(("update", k, name, u))
+    print(f"bf16 stepwise {label}: {obs}")
+    assert not bad, (label, bad[:8])
+    assert obs["param_max_abs_over_lr"] <= 2.0 + 1e-3, obs
+    return obs

@@ -10,8 +10,9 @@ import pytest
 import torch
 
 from oracle import ppo_ref as R
-from parity_util import (assert_params_match, compare_step_grads, make_pair, own_gae,
-                         replay_rows, run_iteration_pair, tensor_slices)
+from parity_util import (assert_params_match, bf16_stepwise, compare_step_grads, make_pair,
+                         own_gae, record_oracle_steps, replay_rows, run_iteration_pair,
+                         tensor_slices)
 
 pytestmark = pytest.mark.gpu
 
@@ -134,12 +135,18 @@ def test_bf16_wide_iteration_matches_bf16_emulation(gpu):
       * rollout values / actions / log-probs within 2e-3 of their scale;
       * the first step's gradient against the f64-accumulated emulation on the engine's own
         buffer within the fixed bf16 gradient bar (1e-2 of each tensor's max, 5e-3 relative L2);
-      * the parameter update (post - init) within 5 % relative L2 of the oracle's per tensor
-        (observed <= 2.6e-2, actor hidden layers; critic <= 1.7e-2): over 8 Adam steps each
-        element moves by ~lr * m / sqrt(v), so an element whose gradient is small against its
-        tensor's max takes a full-size step whose sign follows the bf16 rounding noise of its
+      * free-running, the parameter update (post - init) within 3.5 % relative L2 of the
+        oracle's per tensor (round 4 observed <= 2.8e-2, actor hidden layers): over 8 Adam steps
+        each element moves by ~lr * m / sqrt(v), so an element whose gradient is small against
+        its tensor's max takes a full-size step whose sign follows the bf16 rounding noise of its
         gradient -- the 2x256 case's 0.5 % bar does not transfer to 3x512 nets;
-      * every element within 2*lr*steps."""
+      * every element within 2*lr*steps;
+      * step-wise (parity_util.bf16_stepwise): EVERY optimizer step restarted from the emulation
+        oracle's own state, its gradient within 2e-2 of each tensor's max / 5e-3 relative L2 of
+        the f64-accumulated emulation at the same parameters, its update within 1e-2 relative L2
+        of the oracle's over the elements with a determined gradient sign.  1e-2 of max is below
+        the bf16 emulation's own f32-vs-f64 noise at these states (3.0e-2 of max, 3.3e-3 L2,
+        printed); round 5 observed the engine at 1.5e-2 / 3.9e-3, update 2.4e-3."""
     n, t, b = 256, 32, 2048
     algo, agent, ref, env, cfg = _setup(gpu, n=n, t=t, b=b, epochs=2, hidden=(512, 512, 512),
                                         obs=376, act=17, precision="bf16", p_term=0.02)
@@ -147,6 +154,7 @@ def test_bf16_wide_iteration_matches_bf16_emulation(gpu):
     ref0 = copy.deepcopy(ref)
     R.use_bf16_gemms(ref)
     p0 = R.flat_params(ref).clone()
+    orec = record_oracle_steps(ref)
     agent.engine.timing(True, capacity=100000)
     mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg, seed_train=99)
     kernels = agent.engine.timing_kernels()
@@ -190,12 +198,16 @@ def test_bf16_wide_iteration_matches_bf16_emulation(gpu):
         rel = float((du_e - du_r).norm() / (du_r.norm() + 1e-20))
         worst_u = max(worst_u, rel)
         print(f"wide bf16 update {name}: rel L2 {rel:.3e}")
-        if rel > 5e-2:
+        if rel > 3.5e-2:
             bad.append((name, rel))
     print(f"wide bf16 update: worst rel L2 {worst_u:.3e}")
     assert not bad, bad
     assert not roll_bad, roll_bad
     assert not grad_bad, grad_bad
+    # every optimizer step restarted from the emulation oracle's own state
+    rows = replay_rows(99, n, t, b, 2, 17)
+    bf16_stepwise(agent, ref0, cfg, ref_mem, orec, rows, max_bar=2e-2, l2_bar=5e-3,
+                  update_bar=1e-2, label="wide 3x512 bf16")
 
 
 def test_philox_mode_runs_and_is_reproducible(gpu):

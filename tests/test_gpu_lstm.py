@@ -6,6 +6,11 @@ are too large to store.
 Bars (f32 parity mode, exact-f32 MFMA GEMMs vs torch CPU): LSTM outputs, mean, std, value within
 rtol 1e-5 / atol 1e-5; minibatch losses within 1e-5 relative; gradients within 1e-4 of each
 tensor's largest entry; one full PPO iteration at the north_star parameter bar (parity_util).
+
+bf16 mode (the lstm_leg's precision) is held to the bf16 emulation oracle
+(oracle/lstm_ref.use_bf16_gemms: every GEMM on bf16-rounded operands, f32 cells), accumulated in
+f64 where a gradient is the reference: forward, the main.py network's minibatch gradient, and a
+full iteration free-running plus step-wise.
 """
 import os
 
@@ -16,7 +21,9 @@ import torch
 from oracle import lstm_ref as L
 from oracle import ppo_ref as R
 from oracle.ppo_ref import RefConfig
-from parity_util import assert_params_match, compare_step_grads, make_pair, run_iteration_pair
+from parity_util import (assert_params_match, bf16_f64_grad, bf16_stepwise, compare_step_grads,
+                         grad_errors, make_pair, record_oracle_steps, replay_rows,
+                         run_iteration_pair, tensor_slices)
 
 pytestmark = pytest.mark.gpu
 
@@ -170,6 +177,133 @@ def test_minibatch_grad_deterministic_and_bf16_close(gpu):
         rel = float((a - b).norm() / (b.norm() + 1e-20))
         print(f"bf16 vs f32 grad tensor {i}: rel L2 {rel:.3e}")
         assert rel <= 6e-2, (i, rel)
+
+
+MAIN_NET = dict(obs=348, window=5, act=17, latent=256, layers=1, hidden=(256, 256, 128, 128))
+
+
+def _main_net_case(gpu, b):
+    """The main.py network (O=348, W=5, latent 256, [256, 256, 128, 128], A=17) in bf16 mode and
+    its oracle twin on the same init, plus one minibatch of inputs."""
+    import copy
+    m = MAIN_NET
+    agent = _agent(gpu, m["obs"], m["window"], m["act"], m["latent"], m["layers"], m["hidden"],
+                   "relu", b, seed=24)
+    agent.engine.set_precision("bf16")
+    cfg = RefConfig(obs_dim=m["obs"], act_dim=m["act"], window=m["window"],
+                    actor_hidden=m["hidden"], critic_hidden=m["hidden"], activation="relu")
+    torch.manual_seed(24)
+    ref = L.RefLSTMAgent(cfg, m["latent"], m["layers"])
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref))
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(b, m["window"], m["obs"], generator=gen)
+    actions = torch.randn(b, m["act"], generator=gen) * 0.3
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    with torch.no_grad():
+        mean, std = ref.networks["actor"](x)
+        lp = torch.distributions.Normal(mean, std).log_prob(actions).sum(1)
+    old_logp = lp + 0.15 * torch.randn(b, generator=gen)
+    e32 = copy.deepcopy(ref)
+    L.use_bf16_gemms(e32)
+    e64 = copy.deepcopy(ref)
+    e64.networks.double()
+    L.use_bf16_gemms(e64)
+    return agent, ref, e32, e64, (x, actions, old_logp, adv, vt)
+
+
+def test_bf16_forward_matches_f64_emulation(gpu):
+    """bf16 LSTMActor / LSTMCritic forward (lstm_actor.py:41-48, lstm_critic.py:33-41) on the
+    main.py network against the f64-accumulated bf16 emulation: mean, std and value within 2e-3
+    of their scale (the emulation's own f32-vs-f64 spread here: <= 3e-4)."""
+    agent, ref, e32, e64, (x, *_rest) = _main_net_case(gpu, 512)
+    got = _forward(agent, x)
+    with torch.no_grad():
+        m64, s64 = e64.networks["actor"](x.double())
+        v64 = e64.networks["critic"](x.double())
+        m32, s32 = e32.networks["actor"](x)
+        v32 = e32.networks["critic"](x)
+    for k, want, emu in (("mean", m64, m32), ("std", s64, s32), ("value", v64, v32)):
+        scale = float(want.abs().max())
+        err = float((got[k].double() - want).abs().max()) / scale
+        spread = float((emu.double() - want).abs().max()) / scale
+        print(f"bf16 main.py net {k}: engine {err:.3e} of scale (emulation f32 vs f64 {spread:.3e})")
+        assert err <= 2e-3, (k, err)
+
+
+def test_bf16_minibatch_grad_matches_f64_emulation(gpu):
+    """the bf16 BiLSTM minibatch gradient (ppo.py:108-135 with the LSTM agent)
+    on the main.py network, B = 1024, against the f64-accumulated bf16 emulation at a FIXED bar per
+    tensor: max error <= 1.5e-1 of the tensor's max and relative L2 <= 5e-2.  Why that loose: a
+    bf16 rounding of an intermediate flipped by the f32 summation order changes it by 2^-8, which
+    moves the next layer's sums by about their own bf16 half-ulp, so flips cascade through the
+    LSTM and the 4 MLP layers -- the emulation's OWN f32-vs-f64 spread at this shape is 5e-2 of
+    max / 1.5e-2 L2 (critic hidden layers).  Over all tensors, the engine's worst error must also
+    stay within 2x the emulation's own worst (the spread of one tensor alone is a noisy sample:
+    round 5 saw 4.2e-2 against 1.2e-2 on critic.network.first_layers.6.weight while the worst
+    over all tensors was 5.0e-2 against 3.8e-2).  Losses within 1e-3 relative."""
+    agent, ref, e32, e64, (x, actions, old_logp, adv, vt) = _main_net_case(gpu, 1024)
+    g, loss = _grad(agent, x, actions, old_logp, adv, vt)
+    g64, la, lc = L.minibatch_grads(e64, x.double(), actions.double(), old_logp.double(),
+                                    adv.double(), vt.double(), 0.1, 1e-4)
+    g32, _, _ = L.minibatch_grads(e32, x, actions, old_logp, adv, vt, 0.1, 1e-4)
+    assert abs(float(loss[0]) - la) <= 1e-3 * max(1.0, abs(la)), (float(loss[0]), la)
+    assert abs(float(loss[1]) - lc) <= 1e-3 * max(1.0, abs(lc)), (float(loss[1]), lc)
+    spread = {name: (e, l2) for name, e, l2 in grad_errors(g32, g64, ref)}
+    worst, worst_l2, bad = 0.0, 0.0, []
+    for name, err, l2 in grad_errors(g, g64, ref):
+        s_max, s_l2 = spread[name]
+        print(f"bf16 main.py grad {name}: err {err:.3e} of max, rel L2 {l2:.3e} "
+              f"(emulation f32 vs f64: {s_max:.3e}, {s_l2:.3e})")
+        worst, worst_l2 = max(worst, err), max(worst_l2, l2)
+        if err > 1.5e-1 or l2 > 5e-2:
+            bad.append((name, err, l2, s_max))
+    s_worst = max(e for e, _ in spread.values())
+    s_worst_l2 = max(l for _, l in spread.values())
+    print(f"bf16 main.py grad vs f64 emulation: worst {worst:.3e} of max, rel L2 {worst_l2:.3e} "
+          f"(emulation f32 vs f64: {s_worst:.3e}, {s_worst_l2:.3e})")
+    assert not bad, bad
+    assert worst <= 2 * s_worst and worst_l2 <= 2 * s_worst_l2, (worst, s_worst, worst_l2, s_worst_l2)
+
+
+def test_lstm_bf16_iteration_matches_bf16_emulation(gpu):
+    """One PPO iteration with the BiLSTM agent in bf16 mode (latent 64 so the forward steps run
+    as lstm_step_fwd_kernel) against the bf16 emulation oracle on the same torch RNG streams:
+    rollout values / actions / log-probs within 2e-3 of scale; free-running update within 2e-2
+    relative L2 per tensor; and step-wise (parity_util.bf16_stepwise) every optimizer step from
+    the oracle's own state: gradient within 1e-2 of each tensor's max / 5e-3 relative L2 of the
+    f64-accumulated emulation (its own f32 spread at these shapes: <= 1.9e-3 / 6.5e-4), update
+    within 1e-2 relative L2 where the gradient sign is determined."""
+    import copy
+    n, t, b = 32, 16, 128
+    algo, agent, ref, env, cfg = make_pair(gpu, n=n, t=t, b=b, epochs=2, p_term=0.05,
+                                           feature_extractor="LSTM", latent=64, window=3,
+                                           hidden=(64, 64), precision="bf16")
+    assert agent.engine.precision == "bf16"
+    ref0 = copy.deepcopy(ref)
+    L.use_bf16_gemms(ref)
+    p0 = R.flat_params(ref).clone()
+    steps = record_oracle_steps(ref)
+    mem, ref_mem, g_eng, g_ref = run_iteration_pair(algo, agent, ref, env, cfg, seed_train=99)
+    for key in ("current_state_value", "action", "action_log_prob"):
+        a, r = mem[key].cpu(), ref_mem[key]
+        err = float((a - r).abs().max()) / (float(r.abs().max()) + 1e-6)
+        print(f"lstm bf16 rollout {key}: max err {err:.3e} of scale")
+        assert err <= 2e-3, (key, err)
+    p_eng, p_ref = agent.packed_params().cpu(), R.flat_params(ref)
+    assert float((p_eng - p_ref).abs().max()) <= 2 * cfg.learning_rate * len(g_ref)
+    worst = 0.0
+    for name, lo, hi in tensor_slices(ref):
+        du_e, du_r = p_eng[lo:hi] - p0[lo:hi], p_ref[lo:hi] - p0[lo:hi]
+        if float(du_r.norm()) == 0.0:
+            continue
+        rel = float((du_e - du_r).norm() / du_r.norm())
+        worst = max(worst, rel)
+        assert rel <= 2e-2, (name, rel)
+    print(f"lstm bf16 free-running update: worst rel L2 {worst:.3e}")
+    rows = replay_rows(99, n, t, b, 2, cfg.act_dim)
+    bf16_stepwise(agent, ref0, cfg, ref_mem, steps, rows, max_bar=1e-2, l2_bar=5e-3,
+                  update_bar=1e-2, bf16_fn=L.use_bf16_gemms, label="lstm bf16")
 
 
 def test_fused_forward_step_bitwise_equals_layered(gpu):

@@ -104,3 +104,41 @@ def test_oracle_minibatch_grads_match_reference(name):
     norms = z[f"{name}/grad_norm"]
     for i, a in enumerate(parts):
         assert abs(float(a.double().norm()) - norms[i]) <= 1e-4 * max(norms[i], 1e-12), i
+
+
+def test_bf16_emulation_rounds_every_gemm_operand():
+    """oracle.lstm_ref.use_bf16_gemms (the engine's PPO_PREC_BF16 arithmetic): the input and
+    recurrent projections multiply bf16-rounded operands (known answer on a tiny direction), the
+    emulation differs from f32, and its f32- and f64-accumulated forms agree to bf16 noise."""
+    import copy
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 3, 5, generator=g)
+    w_ih, w_hh = torch.randn(8, 5, generator=g), torch.randn(8, 2, generator=g)
+    b_ih, b_hh = torch.randn(8, generator=g), torch.randn(8, generator=g)
+    bf = lambda t: t.to(torch.bfloat16).float()
+    h = L.lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse=False, bf16=True)
+    # hand-rolled first two steps
+    hp, cp = torch.zeros(4, 2), torch.zeros(4, 2)
+    for t in range(2):
+        gates = (bf(hp) @ bf(w_hh).t() + b_hh) + (bf(x[:, t]) @ bf(w_ih).t() + b_ih)
+        i, f, gg, o = gates.chunk(4, 1)
+        cp = f.sigmoid() * cp + i.sigmoid() * gg.tanh()
+        hp = o.sigmoid() * cp.tanh()
+        torch.testing.assert_close(h[:, t], hp, rtol=1e-6, atol=1e-6)
+    assert not torch.equal(h, L.lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse=False))
+    cfg = RefConfig(obs_dim=17, act_dim=6, window=3, actor_hidden=(32, 32), critic_hidden=(32, 32))
+    torch.manual_seed(1)
+    ref = L.RefLSTMAgent(cfg, 16, 2)
+    e32, e64 = copy.deepcopy(ref), copy.deepcopy(ref)
+    e64.networks.double()
+    L.use_bf16_gemms(e32)
+    L.use_bf16_gemms(e64)
+    s = torch.randn(64, 3, 17, generator=g)
+    with torch.no_grad():
+        m0, _ = ref.networks["actor"](s)
+        m1, s1 = e32.networks["actor"](s)
+        m2, s2 = e64.networks["actor"](s.double())
+        v1, v2 = e32.networks["critic"](s), e64.networks["critic"](s.double())
+    assert not torch.equal(m0, m1)
+    for a, b in ((m1, m2), (s1, s2), (v1, v2)):
+        assert float((a.double() - b).abs().max()) <= 1e-3 * float(b.abs().max())
