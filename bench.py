@@ -86,6 +86,9 @@ def parse():
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "bench_traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+    p.add_argument("--gae-sweep", default="16384,65536",
+                   help="env counts at which the headline line also times the standalone GAE scan "
+                        "(its bandwidth ceiling beyond 4096 envs; empty for none)")
     p.add_argument("--legs", default="ant,humanoid,cnn,lstm",
                    help="BASELINE-config legs the default N=1 line carries (comma list of ant, "
                         "humanoid, cnn, lstm; empty for none)")
@@ -546,6 +549,48 @@ parse_defaults = {"num_envs": 4096, "obs_dim": 17, "act_dim": 6, "hidden": "256,
                   "batch": 65536, "window": None, "horizon": 128, "epochs": 10}
 
 
+def parallelism_label(world: int) -> str:
+    rehearse = os.environ.get("PPO_DP_REHEARSE", "") if world == 1 else ""
+    if rehearse == "1":
+        return "dp1 rehearsal (the data-parallel step sequence, no peer: PPO_DP_REHEARSE=1)"
+    if rehearse == "rccl":
+        return ("dp1 rehearsal (the data-parallel step sequence with the native RCCL all-reduce "
+                "of a world-1 communicator, graph-captured: PPO_DP_REHEARSE=rccl)")
+    return f"dp{world} (env-sharded, RCCL grad all-reduce)"
+
+
+def gae_sweep_points(agent, dev, t: int, ns) -> list:
+    """ppo_gae (gae_pipe_kernel) alone at larger env counts, T steps, f64 rewards: 25 algorithmic
+    bytes per (env, step) (V, V', reward, terminated in; adv, target out), kernel time from the
+    engine's per-dispatch events (tools/gae_sweep.py's method)."""
+    from mujoco_reinforcement_learning_amd import engine as E
+    out = []
+    for n in ns:
+        g = torch.Generator(device=dev).manual_seed(n)
+        v = torch.randn(t, n, device=dev, generator=g)
+        vn = torch.randn(t, n, device=dev, generator=g)
+        r = torch.randn(t, n, device=dev, generator=g, dtype=torch.float64)
+        term = torch.rand(t, n, device=dev, generator=g) < 0.01
+        adv, vt = torch.empty(t, n, device=dev), torch.empty(t, n, device=dev)
+        for _ in range(3):
+            E.gae(v, vn, r, term, 0.99, 0.98, adv, vt, force_last_done=True)
+        torch.cuda.synchronize()
+        agent.engine.timing(True, capacity=64)
+        for _ in range(20):
+            E.gae(v, vn, r, term, 0.99, 0.98, adv, vt, force_last_done=True)
+        torch.cuda.synchronize()
+        ks = agent.engine.timing_kernels()
+        agent.engine.timing(False)
+        name, rec = max(ks.items(), key=lambda kv: kv[1]["ms"])
+        us = 1e3 * rec["ms"] / rec["launches"]
+        gbs = 25.0 * n * t / (us * 1e-6) / 1e9
+        out.append({"kernel": name, "num_envs": n, "horizon": t, "avg_launch_us": us,
+                    "achieved": gbs, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                    "algorithmic_per_launch": 25.0 * n * t})
+        del v, vn, r, term, adv, vt
+    return out
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -563,6 +608,12 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world == 1 and os.environ.get("PPO_DP_REHEARSE") == "rccl":
+        # the data-parallel step sequence with the native RCCL all-reduce, graph-captured, on one
+        # rank (DataParallel): a world-1 RCCL process group
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        torch.distributed.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
     if world > 1:
         backend = os.environ.get("PPO_BENCH_BACKEND", "nccl")
         if backend == "nccl":
@@ -609,10 +660,7 @@ def main():
                        "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
                                else f"host pool ({args.env_workers} worker processes, page-locked "
                                     "device-mapped shared memory, ppo_host_rollout)"),
-                       "parallelism": (f"dp{world} (env-sharded, RCCL grad all-reduce)"
-                                       if os.environ.get("PPO_DP_REHEARSE") != "1" or world > 1
-                                       else "dp1 rehearsal (the data-parallel step sequence, "
-                                            "no peer: PPO_DP_REHEARSE=1)")}}
+                       "parallelism": parallelism_label(world)}}
     if kernels:
         traffic = load_traffic(args.traffic, traffic_workload(args))
         name, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])
@@ -627,12 +675,24 @@ def main():
                 rows = n * t
                 payload = 2 * args.window * args.obs_dim + 4 * args.act_dim + 12
                 pb = gr["algorithmic_per_launch"] - (128 - payload) * rows
+                # the headline figure counts the record's payload only; the
+                # padded figure (every byte of the 128-B record written) stays as a secondary
+                gr["with_record_padding"] = {
+                    "achieved": gr["achieved"], "frac": gr["frac"],
+                    "algorithmic_per_launch": gr["algorithmic_per_launch"],
+                    "bytes_counted": "as below, but the full 128-B record written per (env, step)"}
+                gr["achieved"] = pb / (gr["avg_launch_us"] * 1e-6) / 1e9
+                gr["frac"] = gr["achieved"] / PEAK_HBM_GBS
+                gr["algorithmic_per_launch"] = pb
                 gr["bytes_counted"] = (f"reads: reward f64, V, V', terminated (scan, 25 B) + "
                                        f"state f32 {4 * args.window * args.obs_dim} B + actions "
-                                       f"{4 * args.act_dim} B + old log-prob 4 B; writes: "
-                                       f"adv / target and the full 128-B record per (env, step)")
-                gr["payload_only"] = {"bytes_per_launch": pb, "record_payload_bytes": payload,
-                                      "frac": pb / (gr["avg_launch_us"] * 1e-6) / 1e9 / PEAK_HBM_GBS}
+                                       f"{4 * args.act_dim} B + old log-prob 4 B; writes: adv / "
+                                       f"target 8 B + the record's {payload}-B payload (bf16 "
+                                       f"state, actions, old log-prob, adv, target) per (env, step)")
+            if args.gae_sweep and args.model == "mlp":
+                # the standalone scan's bandwidth ceiling beyond the headline's 4096 envs
+                gr["scan_sweep"] = gae_sweep_points(agent, dev, args.horizon,
+                                                    [int(x) for x in args.gae_sweep.split(",")])
             line["gae_roofline"] = gr
         ti = max(args.timing_iters, 1)
         line["kernel_classes_ms_per_step"] = {k: v["ms"] / ti for k, v in classes.items()
@@ -665,7 +725,7 @@ def main():
         print(json.dumps(line), flush=True)
     if hasattr(helper, "close"):
         helper.close()
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -319,6 +319,12 @@ int ppo_synthetic_env_step(const float *base_obs_d, const float *base_reward_d,
                            double *obs_out_d, double *reward_out_d, uint8_t *term_out_d,
                            void *stream);
 int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, int64_t n, void *stream);
+/* The same normals at offset + *counter_d (device uint64, read when the kernel runs; NULL: 0):
+ * element i = the Philox normal ppo_policy_step / ppo_observe_act draw at index offset +
+ * *counter_d + i, so a whole rollout's noise (T x N x A) comes from one launch ahead of the steps,
+ * bitwise the in-kernel draws, and a graph-captured rollout replays with fresh noise. */
+int ppo_philox_normal_ctr(uint64_t seed, uint64_t offset, const uint64_t *counter_d, float *out_d,
+                          int64_t n, void *stream);
 /* One step of the single evaluation env of Algorithm.test (base_algorithm.py:21-48) on the same
  * synthetic streams (env 0, base arrays (T+1, N, O) / (T, N) / (T, N)), with the reference's
  * host branch (:33-37) taken on the device: *step_d = k (device int32, zeroed by the test reset);

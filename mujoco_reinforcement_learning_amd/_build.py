@@ -20,13 +20,14 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=o
 
 
 def build_host_env(verbose: bool = True) -> str:
-    """libppo_hostenv.so: the host physics pool workers' per-slice dynamics (plain C, gcc)."""
+    """libppo_hostenv.so: the host physics pool workers' per-slice dynamics (plain C, gcc) and the
+    PPO_SEGV_MAPS crash diagnostics (csrc/host/crash_maps.c)."""
     out = os.path.join(HERE, "libppo_hostenv.so")
-    src = os.path.join(HERE, "csrc", "host", "synthetic_physics.c")
-    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+    srcs = [os.path.join(HERE, "csrc", "host", f) for f in ("synthetic_physics.c", "crash_maps.c")]
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in srcs):
         return out
     cmd = [os.environ.get("CC", "gcc"), "-O3", "-ffp-contract=off", "-fPIC", "-shared",
-           "-o", out + ".tmp", src]
+           "-o", out + ".tmp", *srcs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=HERE)

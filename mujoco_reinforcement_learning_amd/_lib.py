@@ -120,6 +120,7 @@ _SIGNATURES = {
     "ppo_synthetic_env_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "ppo_philox_normal": (c_int, [c_uint64, c_uint64, c_void_p, c_int64, c_void_p]),
+    "ppo_philox_normal_ctr": (c_int, [c_uint64, c_uint64, c_void_p, c_void_p, c_int64, c_void_p]),
     "ppo_synthetic_test_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
@@ -243,6 +244,9 @@ def load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import "
             "__graft_entry__ as g; g.build()' or make -C mujoco_reinforcement_learning_amd)")
+    if os.environ.get("PPO_SEGV_MAPS") == "1":
+        # diagnostics: a fatal SIGSEGV first dumps /proc/self/maps (csrc/host/crash_maps.c)
+        ctypes.CDLL(os.path.join(os.path.dirname(LIB_PATH), "libppo_hostenv.so"))
     lib = ctypes.CDLL(LIB_PATH)
     for name, (restype, argtypes) in _SIGNATURES.items():
         fn = getattr(lib, name)

@@ -169,14 +169,24 @@ class PPOEngine:
         window = helper.timestep.observation
         norm = bool(self.run.normalize_observations)
         seed = self._seed() * 1_000_003 + 17 + 7919 * self.dp.rank
-        eps, _ = self._eps(n, a)
+        noise = None
+        if self._rng() == "philox" and getattr(eng, "fused", False):
+            # the whole rollout's Philox noise in one launch ahead of the steps (bitwise the
+            # in-kernel draws: index base_off [+ the device counter] + t*N*A + env*A + a), so the
+            # policy kernel loads it with the observations instead of computing it on its
+            # critical path
+            if getattr(self, "_noise", None) is None or self._noise.shape != (t_len, n, a):
+                self._noise = torch.empty(t_len, n, a, device=self.agent.device)
+            noise = self._noise
+            E.philox_normal(seed, base_off, noise, counter=getattr(eng, "_rng_counter", None))
+        eps = noise[0] if noise is not None else self._eps(n, a)[0]
         eng.observe_act(window, buf.states[0], normalize=norm, eps=eps, seed=seed,
                         offset=base_off, action=buf.actions[0], logp=buf.logp[0],
                         value=buf.values[0])
         for t in range(t_len):
             obs = helper.step_raw(buf.actions[t], buf.reward[t], buf.terminated[t])
             if t + 1 < t_len:
-                eps, _ = self._eps(n, a)
+                eps = noise[t + 1] if noise is not None else self._eps(n, a)[0]
                 eng.observe_act(window, buf.states[t + 1], obs=obs, reset=buf.terminated[t],
                                 normalize=norm, eps=eps, seed=seed,
                                 offset=base_off + (t + 1) * n * a, action=buf.actions[t + 1],

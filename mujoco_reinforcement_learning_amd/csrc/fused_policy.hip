@@ -38,10 +38,8 @@ struct PolicyLds {
   static constexpr int BIAS = WH + HeadImg<H>::BYTES;           // f32 b0[H], b1[H]
   static constexpr int HS = BIAS + 2 * H * 4;                   // f32 head bias[8], logstd[8]
   static constexpr int XD = HS + 16 * 4;                        // f64 [RP][33] raw observations
-  static constexpr int ST = XD + RP * kPolicyXsPitch * 8;       // f64 [RP][16][2] slice mean, std
-  static constexpr int EPS = ST + RP * 16 * 2 * 8;              // f32 [RP][8] sampling noise
-  static constexpr int SMAP = EPS + RP * 8 * 4;                 // int [32] slice of feature f (-1: none)
-  static constexpr int TOTAL = SMAP + kFusedKX * 4;
+  static constexpr int EPS = XD + RP * kPolicyXsPitch * 8;      // f32 [RP][8] sampling noise
+  static constexpr int TOTAL = EPS + RP * 8 * 4;
   static_assert(TOTAL <= 163840, "LDS budget");
 };
 
@@ -65,9 +63,7 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   float *const bias = reinterpret_cast<float *>(lds + L::BIAS);
   float *const hs = reinterpret_cast<float *>(lds + L::HS);
   double *const xd = reinterpret_cast<double *>(lds + L::XD);
-  double *const st = reinterpret_cast<double *>(lds + L::ST);
   float *const eps_s = reinterpret_cast<float *>(lds + L::EPS);
-  int *const smap = reinterpret_cast<int *>(lds + L::SMAP);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -147,12 +143,6 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   if (tid < 16)
     hs[tid] = (tid < 8 ? (tid < nh_real && N.bh != nullptr) : (ACTOR && tid - 8 < A)) ? hraw : 0.f;
   if (ACTOR && tid < RP * 8) eps_s[tid] = q.eps ? ((ea < A && erow < nrow) ? eraw : 0.f) : epsv;
-  if (tid < kFusedKX) {  // feature -> slice map (the edges are uniform: scalar loads)
-    int sl_of = -1;
-    for (int sl = 0; sl < q.tab.count; ++sl)
-      if (tid >= q.tab.edge[sl] && tid < q.tab.edge[sl + 1]) sl_of = sl;
-    smap[tid] = q.normalize ? sl_of : -1;
-  }
 #pragma unroll
   for (int k = 0; k < XE; ++k) {
     const int e = tid + NT * k, row = e >> 5, f = e & 31;
@@ -163,49 +153,47 @@ __device__ __forceinline__ void policy_body(const PolicyFusedArgs &q, const Fuse
   }
   lds_sync();
   PSTAMP(2);
-  // ---- per-(row, slice) mean and std on every wave: lane = feature (lanes 0-31 and 32-63 are
-  //      two rows), each wave 4 rows as two interleaved chains.  row_stats.h's pairwise tree over
-  //      the 32 slots is a DPP / permlane butterfly across the 32 lanes (slice_stats_lanes), so
-  //      mean / std are bitwise the layered A1 kernel's ----
+  // ---- per-(row, slice) mean and std on every wave, and the standardised states in the same
+  //      phase: lane = feature (lanes 0-31 and 32-63 are two rows), each wave 4 rows as two
+  //      interleaved chains.  row_stats.h's pairwise tree over the 32 slots is a DPP / permlane
+  //      butterfly across the 32 lanes (slice_stats_lanes), so mean / std are bitwise the layered
+  //      A1 kernel's; every lane ends with its rows' statistics and standardises its own feature
+  //      right there ((x - mean) / std in f64, then f32): no statistics round trip through LDS and
+  //      no separate phase / barrier.  The bf16 X image (16-bit stores, RNE like pack2) and the
+  //      f32 state (writer workgroups) ----
   static_assert(4 * NW == RP, "four rows per wave");
-  if (q.normalize) {
+  {
     const int f = lane & 31;
     const int ra = 4 * w + 2 * (lane >> 5), rb = ra + 1;  // the two rows of this lane
     const double xa = xd[ra * kPolicyXsPitch + f], xb = xd[rb * kPolicyXsPitch + f];
-    for (int sl = 0; sl < q.tab.count; ++sl) {
-      const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
-      if (hi - lo <= 0) continue;  // uniform
-      const SliceStats2 s2 = slice_stats_lanes(xa, xb, f >= lo && f < hi, hi - lo);
-      if (f == 0) {
-        st[(ra * 16 + sl) * 2] = s2.mean[0];
-        st[(ra * 16 + sl) * 2 + 1] = s2.sd[0];
-        st[(rb * 16 + sl) * 2] = s2.mean[1];
-        st[(rb * 16 + sl) * 2 + 1] = s2.sd[1];
+    float ya = f < O ? static_cast<float>(xa) : 0.f, yb = f < O ? static_cast<float>(xb) : 0.f;
+    if (q.normalize) {
+      ya = 0.f;
+      yb = 0.f;
+      for (int sl = 0; sl < q.tab.count; ++sl) {
+        const int lo = q.tab.edge[sl], hi = q.tab.edge[sl + 1];
+        if (hi - lo <= 0) continue;  // uniform
+        const bool in = f >= lo && f < hi;
+        const SliceStats2 s2 = slice_stats_lanes(xa, xb, in, hi - lo);
+        if (in) {
+          ya = static_cast<float>((xa - s2.mean[0]) / s2.sd[0]);
+          yb = static_cast<float>((xb - s2.mean[1]) / s2.sd[1]);
+        }
       }
+    }
+    if (ra >= nrow) ya = 0.f;
+    if (rb >= nrow) yb = 0.f;
+    *reinterpret_cast<uint16_t *>(ximg + x_off(ra, f >> 3) + 2 * (f & 7)) =
+        static_cast<uint16_t>(pack2(ya, 0.f) & 0xffffu);
+    *reinterpret_cast<uint16_t *>(ximg + x_off(rb, f >> 3) + 2 * (f & 7)) =
+        static_cast<uint16_t>(pack2(yb, 0.f) & 0xffffu);
+    if (writer && f < O) {
+      if (ra < nrow) q.state_d[static_cast<int64_t>(row0 + ra) * O + f] = ya;
+      if (rb < nrow) q.state_d[static_cast<int64_t>(row0 + rb) * O + f] = yb;
     }
   }
   lds_sync();
   PSTAMP(3);
-  // ---- standardised states: thread -> (row, feature pair); bf16 X image and the f32 state
-  //      (writer workgroups) ----
-#pragma unroll
-  for (int k = 0; k < (RP * 16 + NT - 1) / NT; ++k) {
-    const int idx = tid + NT * k, xr = idx >> 4, c2 = (idx & 15) * 2;
-    if (RP * 16 % NT != 0 && idx >= RP * 16) break;
-    float y[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int f = c2 + u;
-      const double x = xd[xr * kPolicyXsPitch + f];
-      const int sl = smap[f];
-      float v = (!q.normalize && f < O) ? static_cast<float>(x) : 0.f;
-      if (sl >= 0) v = static_cast<float>((x - st[(xr * 16 + sl) * 2]) / st[(xr * 16 + sl) * 2 + 1]);
-      y[u] = xr < nrow ? v : 0.f;
-      if (writer && xr < nrow && f < O) q.state_d[static_cast<int64_t>(row0 + xr) * O + f] = y[u];
-    }
-    *reinterpret_cast<uint32_t *>(ximg + x_off(xr, c2 >> 3) + 2 * (c2 & 7)) = pack2(y[0], y[1]);
-  }
-  lds_sync();
   PSTAMP(4);
 
   // ---- L0: a1 = act(W0 x + b0) -> A1 image ----

@@ -2,10 +2,13 @@
 // vectorized.py:61-92: mean, unbiased std, std == 0 -> 1), shared by the layered A1 kernel
 // (obs_normalize_kernel, O <= 32) and the fused rollout step (policy_fused_kernel), so the two
 // produce bit-identical states.  The row sits in 32 registers (slots >= O are zero); each of the
-// three sums (x, x - mean, ((x - mean) - cmean)^2) is a fixed pairwise tree over the 32 slots with
-// the slots outside the slice zeroed: depth 5 instead of a 32-long dependent f64 chain.  Against
-// torch's own (vectorised) summation order the f64 results differ only in rounding, i.e. the f32
-// states agree up to rare 1-ulp ties (the bar of test_obs_window_and_normalize).
+// two sums (x, (x - mean)^2) is a fixed pairwise tree over the 32 slots with the slots outside the
+// slice zeroed: depth 5 instead of a 32-long dependent f64 chain.  mean = sum * (1/n) and var =
+// sum * (1/(n-1)) with the reciprocals taken off the data chain (they depend on the slice width
+// only), and no second-pass mean correction: every f64 step stays within ~1 ulp (1e-16) of torch's
+// own two-pass f64 std, so the f32 states agree with it up to rare 1-ulp ties (the bar of
+// test_obs_window_and_normalize) -- and the rollout step's dependent f64 chain is one butterfly
+// and three divides shorter (round 5: 8.8 -> <= 8 us per launch at N = 4096).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -24,22 +27,21 @@ struct SliceStats {
   double mean, sd;
 };
 
-// Statistics of slice [lo, hi) (cnt = hi - lo >= 1; cnt == 1 gives sd = NaN, as torch.std).
+// Statistics of slice [lo, hi) (cnt = hi - lo >= 1; cnt == 1 gives sd = NaN, as torch.std:
+// 0 * (1/0)).
 __device__ __forceinline__ SliceStats slice_stats32(const double (&x)[32], int lo, int hi) {
   const int cnt = hi - lo;
+  const double inv_n = 1.0 / cnt, inv_n1 = 1.0 / (cnt - 1);
   double t[32];
 #pragma unroll
   for (int f = 0; f < 32; ++f) t[f] = (f >= lo && f < hi) ? x[f] : 0.0;
-  const double mean = tree32(t) / cnt;
-#pragma unroll
-  for (int f = 0; f < 32; ++f) t[f] = (f >= lo && f < hi) ? x[f] - mean : 0.0;
-  const double cmean = tree32(t) / cnt;
+  const double mean = tree32(t) * inv_n;
 #pragma unroll
   for (int f = 0; f < 32; ++f) {
-    const double d = (x[f] - mean) - cmean;
+    const double d = x[f] - mean;
     t[f] = (f >= lo && f < hi) ? d * d : 0.0;
   }
-  double sd = sqrt(tree32(t) / (cnt - 1));
+  double sd = sqrt(tree32(t) * inv_n1);
   if (sd == 0.0) sd = 1.0;
   return SliceStats{mean, sd};
 }
@@ -87,18 +89,15 @@ struct SliceStats2 {
 
 __device__ __forceinline__ SliceStats2 slice_stats_lanes(double xa, double xb, bool in, int cnt) {
   SliceStats2 r;
+  const double inv_n = 1.0 / cnt, inv_n1 = 1.0 / (cnt - 1);  // off the data chain
   double ta = in ? xa : 0.0, tb = in ? xb : 0.0;
   butterfly2(ta, tb);
-  const double ma = ta / cnt, mb = tb / cnt;
-  ta = in ? xa - ma : 0.0;
-  tb = in ? xb - mb : 0.0;
-  butterfly2(ta, tb);
-  const double ca = ta / cnt, cb = tb / cnt;
-  const double da = (xa - ma) - ca, db = (xb - mb) - cb;
+  const double ma = ta * inv_n, mb = tb * inv_n;
+  const double da = xa - ma, db = xb - mb;
   ta = in ? da * da : 0.0;
   tb = in ? db * db : 0.0;
   butterfly2(ta, tb);
-  double sa = sqrt(ta / (cnt - 1)), sb = sqrt(tb / (cnt - 1));
+  double sa = sqrt(ta * inv_n1), sb = sqrt(tb * inv_n1);
   if (sa == 0.0) sa = 1.0;
   if (sb == 0.0) sb = 1.0;
   r.mean[0] = ma;

@@ -407,10 +407,11 @@ __global__ __launch_bounds__(256) void synthetic_test_step_kernel(
 // ============================================================================================
 // Philox4x32-10 normals (perf-mode eps; the parity mode takes host torch.randn instead)
 // ============================================================================================
-__global__ void philox_normal_kernel(uint64_t seed, uint64_t offset, float *__restrict__ out,
-                                     int64_t n) {
+__global__ void philox_normal_kernel(uint64_t seed, uint64_t offset, const uint64_t *counter,
+                                     float *__restrict__ out, int64_t n) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = philox_normal_at(seed, offset + static_cast<uint64_t>(i));
+  const uint64_t base = offset + (counter ? *counter : 0);
+  if (i < n) out[i] = philox_normal_at(seed, base + static_cast<uint64_t>(i));
 }
 
 // ============================================================================================
@@ -817,8 +818,21 @@ extern "C" int ppo_philox_normal(uint64_t seed, uint64_t offset, float *out_d, i
   PPO_REQUIRE(out_d && n >= 0, "ppo_philox_normal: bad args");
   if (n == 0) return 0;
   FreeTimingScope timing_scope;
+  const uint64_t *nul = nullptr;
   launch_k(TimRec{KC_ENV, "philox_normal_kernel", 0.0, 4.0 * n}, philox_normal_kernel,
-           dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), seed, offset, out_d, n);
+           dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), seed, offset, nul, out_d, n);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+extern "C" int ppo_philox_normal_ctr(uint64_t seed, uint64_t offset, const uint64_t *counter_d,
+                                     float *out_d, int64_t n, void *stream) {
+  PPO_REQUIRE(out_d && n >= 0, "ppo_philox_normal_ctr: bad args");
+  if (n == 0) return 0;
+  FreeTimingScope timing_scope;  // the rollout's sampling noise: policy-head work
+  launch_k(TimRec{KC_POLICY_HEAD, "philox_normal_kernel", 0.0, 4.0 * n}, philox_normal_kernel,
+           dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream), seed, offset, counter_d, out_d,
+           n);
   PPO_LAUNCHED();
   return 0;
 }

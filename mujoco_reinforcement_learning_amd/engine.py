@@ -564,10 +564,18 @@ def synthetic_test_step(base_obs, base_reward, base_term, action, window, step, 
                                       _stream(dev)))
 
 
-def philox_normal(seed: int, offset: int, out: torch.Tensor) -> None:
+def philox_normal(seed: int, offset: int, out: torch.Tensor,
+                  counter: Optional[torch.Tensor] = None) -> None:
+    """out[i] = the Philox normal at index offset (+ *counter, read on the device) + i: the draws
+    of ppo_policy_step / ppo_observe_act in perf mode, bitwise."""
     lib = _lib.load()
     _need(out, "out", torch.float32)
-    check(lib.ppo_philox_normal(seed, offset, ptr(out), out.numel(), _stream(out.device)))
+    if counter is None:
+        check(lib.ppo_philox_normal(seed, offset, ptr(out), out.numel(), _stream(out.device)))
+        return
+    _need(counter, "counter", torch.int64, (1,), out.device)
+    check(lib.ppo_philox_normal_ctr(seed, offset, ptr(counter), ptr(out), out.numel(),
+                                    _stream(out.device)))
 
 
 def adam_sched(p, g, m, v, n_actor: int, sched: torch.Tensor, one_minus_beta1: float, beta2: float,
