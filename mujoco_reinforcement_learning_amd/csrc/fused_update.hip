@@ -374,7 +374,10 @@ struct Lds {
   // ReLU: the W0 image (H x 32 bf16, x_off-swizzled 64-B rows) LDS-resident for the whole kernel
   // (the tanh / ELU instantiations, with their f32 a2 region, read it from L2)
   static constexpr int W0 = SROW + R * kFusedSP * 4;
-  static constexpr int TOTAL = W0 + (F32A2 ? 0 : H * 64);
+  // ReLU: W_h^T as a bf16 [H][16] image (32-B rows): the d2 product's A fragment is one 16-B read
+  // (head_t_frag gathers it from the head image with 8 two-byte reads otherwise)
+  static constexpr int WHT = W0 + (F32A2 ? 0 : H * 64);
+  static constexpr int TOTAL = WHT + (F32A2 ? 0 : H * 32);
   static_assert(TOTAL <= 163840, "LDS budget");
   static_assert(R * PITCH <= A2BYTES, "D1 image must fit in the a2 region");
 };
@@ -494,6 +497,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     for (int i = tid; i < H * 4; i += NT) {  // 16-B chunk (row i / 4, chunk i % 4) of W0
       const uint4 v = reinterpret_cast<const uint4 *>(N.w0b)[i];
       *reinterpret_cast<uint4 *>(lds + L::W0 + x_off(i >> 2, i & 3)) = v;
+    }
+    const int nh_real = ACTOR ? A : 1;
+    for (int i = tid; i < H * 16; i += NT) {  // W_h^T[f][a] = bf16(W_h[a][f]), heads >= A zero
+      const int a = i / H, f = i % H;           // coalesced reads of W_h's rows
+      const float v = a < nh_real ? N.wh[a * H + f] : 0.f;
+      *reinterpret_cast<uint16_t *>(lds + L::WHT + 2 * (f * 16 + a)) = bf16_bits(v);
     }
   }
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
@@ -629,6 +638,25 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     {
       const int n = lane & 15, qg = lane >> 4, tile = w & 3, half = w >> 2;
       const float *const srl = reinterpret_cast<const float *>(lds + L::SROW);
+      const int lr0 = 16 * tile + 4 * qg + 2 * half;  // this lane's two rows: lr0, lr0 + 1
+      // Every LDS operand of the loss is read here, unconditionally (in-range addresses; masked
+      // where used), before the z products and the exchange barrier: behind per-lane branches
+      // they were one LDS round trip each, after the barrier, row after row.  The two rows'
+      // chains below are straight-line code (selects, not branches), so they interleave.
+      float xs[2] = {0.f, 0.f}, olp[2] = {0.f, 0.f}, advs[2] = {0.f, 0.f}, vts[2] = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float *sp = srl + (lr0 + i) * kFusedSP;
+        if constexpr (ACTOR) {
+          xs[i] = sp[n];
+          olp[i] = sp[A];
+          advs[i] = sp[A + 1];
+        } else {
+          vts[i] = sp[A + 2];
+        }
+      }
+      const float h_b = hbias[ACTOR ? n : 0];
+      const float h_lsd = ACTOR ? hbias[32 + n] : 0.f, h_ivar = ACTOR ? hbias[48 + n] : 0.f;
       // K split between the wave pair: wave half 0 sums k-steps 0..H/64-1, half 1 the rest
       // (half the LDS reads and MFMAs per wave); each hands the partner the two rows it keeps
       // through the (still free) D2 region.  z = P_lo + P_hi on both sides (commutative), the
@@ -652,31 +680,31 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       lds_sync();
       const float2 px = *reinterpret_cast<const float2 *>(xch + 2 * ((w ^ (NW / 2)) * 64 + lane));
       const float zr[2] = {(half ? zacc[2] : zacc[0]) + px.x, (half ? zacc[3] : zacc[1]) + px.y};
-      const float h_lsd = hbias[32 + n], h_ivar = hbias[48 + n];
-      float dz[2];
+      bool valid[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int lr = 16 * tile + 4 * qg + 2 * half + i;
-        const bool valid = chunk * R + lr < count;
-        const float *sp = srl + lr * kFusedSP;
-        dz[i] = 0.f;
-        if constexpr (ACTOR) {
-          const bool act_lane = n < A;
+      for (int i = 0; i < 2; ++i) valid[i] = chunk * R + lr0 + i < count;
+      float dz[2];
+      if constexpr (ACTOR) {
+        // row after row: the interleaved branch-free form of the critic raised this body's
+        // register pressure past the cap (spills landing in the dW1 phase: measured slower)
+        const bool act_lane = n < A;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          dz[i] = 0.f;
           float y = 0.f, d = 0.f, lp = 0.f;
           if (act_lane) {
-            float zz = zr[i];
-            if (N.bh) zz += hbias[n];
+            const float zz = N.bh ? zr[i] + h_b : zr[i];
             y = tanhf(zz);
             const float mu = q.omv * y;
-            const float x = valid ? sp[n] : mu;
+            const float x = valid[i] ? xs[i] : mu;
             d = x - mu;
             lp = ((-(d * d)) * (0.5f * h_ivar) - h_lsd) - kLogSqrt2Pi;  // 0.5/var: exact scaling
           }
           // Normal.log_prob(...).sum(1): fixed xor tree over the 16 head lanes (pads are 0), the
           // same tree as the rollout's policy kernel
           const float logp = row16_sum(lp);
-          const float old_lp = valid ? sp[A] : logp;
-          const float adv = valid ? sp[A + 1] : 0.f;
+          const float old_lp = valid[i] ? olp[i] : logp;
+          const float adv = valid[i] ? advs[i] : 0.f;
           const float ratio = expf(logp - old_lp);
           const float s1 = ratio * adv;
           const float cl = ratio < q.clip_lo ? q.clip_lo : (ratio > q.clip_hi ? q.clip_hi : ratio);
@@ -687,31 +715,31 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
           const float g2 = (s2 < s1) ? gg : (s1 == s2 ? gg * 0.5f : 0.f);
           const bool inside = (ratio >= q.clip_lo) && (ratio <= q.clip_hi);
           const float dratio = g1 * adv + (inside ? g2 * adv : 0.f);
-          const float dlogp = valid ? dratio * ratio : 0.f;
+          const float dlogp = valid[i] ? dratio * ratio : 0.f;
           if (act_lane) {
             const float dmu = dlogp * (d * h_ivar);
             dz[i] = (dmu * q.omv) * (1.f - y * y);
-            if (valid) {
+            if (valid[i]) {
               g_ls += dlogp * ((d * d) * h_ivar - 1.f) - q.ent_coef * q.inv_ba;
               g_bh += dz[i];
             }
           }
-          if (valid && n == 0) g_loss += mn;
-        } else {
-          if (n == 0) {
-            float v = zr[i];
-            if (N.bh) v += hbias[0];
-            const float vt = valid ? sp[A + 2] : v;
-            const float diff = v - vt;
-            const float ad = fabsf(diff);
-            if (valid) g_loss += (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
-            dz[i] = q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff));
-            g_bh += dz[i];
-          }
+          if (valid[i] && n == 0) g_loss += mn;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float v = N.bh ? zr[i] + h_b : zr[i];
+          const float vt = valid[i] ? vts[i] : v;
+          const float diff = v - vt;
+          const float ad = fabsf(diff);
+          const float hl = (ad < 1.f) ? 0.5f * ad * ad : (ad - 0.5f);
+          g_loss = (valid[i] && n == 0) ? g_loss + hl : g_loss;
+          dz[i] = n == 0 ? q.inv_b * (diff < -1.f ? -1.f : (diff > 1.f ? 1.f : diff)) : 0.f;
+          g_bh = n == 0 ? g_bh + dz[i] : g_bh;
         }
       }
       // bf16 dz images (the head-backward operands; zero for padded heads and invalid rows)
-      const int lr0 = 16 * tile + 4 * qg + 2 * half;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
         *reinterpret_cast<uint16_t *>(dzimg + (lr0 + i) * kDzRowBytes + 2 * n) = bf16_bits(dz[i]);
@@ -723,7 +751,22 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     // ---- phase 5: d2 = (dz . W_h) * act'(a2) on MFMA -> bias grad, D2 image; head dW ----
     OPAQUE_LANE();
     {
-      const bf16x8 wht = head_t_frag<H>(whb, w, lane);  // A operand: W_h^T of the wave's features
+      // the A operand W_h^T of the wave's features, both row tiles' dz fragments and (ReLU) the
+      // bf16 a2 values act' needs, all read up front: one LDS round trip for the phase's inputs
+      bf16x8 wht;
+      if constexpr (F32A2) wht = head_t_frag<H>(whb, w, lane);
+      else wht = lds_b128(lds + L::WHT + (32 * w + r) * 32 + 16 * h);
+      bf16x8 dzf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) dzf[t] = lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h);
+      uint2 yb[2][4];
+      if constexpr (!F32A2) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            yb[t][g] = *reinterpret_cast<const uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h);
+      }
       float bsum[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) bsum[e] = 0.f;
@@ -732,20 +775,20 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
         f32x16 acc[1];
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[0][e] = 0.f;
-        acc[0] = mfma(wht, lds_b128(dzimg + (32 * t + r) * kDzRowBytes + 16 * h), acc[0]);
+        acc[0] = mfma(wht, dzf[t], acc[0]);
         mfma_drain(acc);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          float ya, yb, yc, yd;
+          float ya, ybv, yc, yd;
           if constexpr (F32A2) {
             const float4 yv = *reinterpret_cast<const float4 *>(a2img + (32 * t + r) * L::A2P + 4 * (32 * w + 8 * g + 4 * h));
-            ya = yv.x, yb = yv.y, yc = yv.z, yd = yv.w;
+            ya = yv.x, ybv = yv.y, yc = yv.z, yd = yv.w;
           } else {
-            const uint2 yv = *reinterpret_cast<const uint2 *>(a2img + img_off(32 * t + r, 4 * w + g, L::PITCH) + 8 * h);
-            ya = bf_lo(yv.x), yb = bf_hi(yv.x), yc = bf_lo(yv.y), yd = bf_hi(yv.y);
+            const uint2 yv = yb[t][g];
+            ya = bf_lo(yv.x), ybv = bf_hi(yv.x), yc = bf_lo(yv.y), yd = bf_hi(yv.y);
           }
           const float d0 = act_backward(acc[0][4 * g], ya, ACT);
-          const float d1 = act_backward(acc[0][4 * g + 1], yb, ACT);
+          const float d1 = act_backward(acc[0][4 * g + 1], ybv, ACT);
           const float d2 = act_backward(acc[0][4 * g + 2], yc, ACT);
           const float d3 = act_backward(acc[0][4 * g + 3], yd, ACT);
           bsum[4 * g] += d0;
@@ -865,10 +908,18 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     // ---- phase 7: dW0 += D1^T X (the wave's own D1 columns, written by this wave above: no
     //      barrier before it; the chunk's closing barrier follows) ----
     OPAQUE_LANE();
+    {
+      // every transposed fragment read issued first (16 ds_read_b64_tr_b16, 32 registers: the
+      // dgrad accumulators are dead here), then the four chained MFMAs -- one LDS round trip for
+      // the phase instead of one per k-step
+      bf16x8 fd[R / 16], fx[R / 16];
 #pragma unroll
-    for (int ks = 0; ks < R / 16; ++ks) {
-      gw0 = mfma(tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane), tr_frag_x(ximg, 16 * ks, lane), gw0);
-      __builtin_amdgcn_sched_barrier(0);
+      for (int ks = 0; ks < R / 16; ++ks) {
+        fd[ks] = tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane);
+        fx[ks] = tr_frag_x(ximg, 16 * ks, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < R / 16; ++ks) gw0 = mfma(fd[ks], fx[ks], gw0);
     }
     lds_sync();
     STAMP_AT(9);
