@@ -127,12 +127,7 @@ int ppo_pack_weights(ppo_ctx *ctx, void *stream);
  * `offset`.  (No reference counterpart: the reference draws from the host generator.) */
 int ppo_ctx_set_rng_counter(ppo_ctx *ctx, const uint64_t *counter_d);
 
-/* Which fused bf16 update kernel the ctx launches for ReLU 2x256 nets (A11-A13, ppo.py:109-135):
- * 8 = fused_update_kernel (8 waves, 64-row chunks; also tanh / ELU), 4 = fused_update4_kernel
- * (one wave per SIMD, 128-row chunks).  Default PPO_FUSED4 (1 -> 4, else 8);
- * variant < 0 queries.  The two agree to f32 rounding; each is bitwise deterministic. */
-int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant);
-/* How the 8-wave fused update reads the staged records (ppo_stage_records /
+/* How the fused update reads the staged records (ppo_stage_records /
  * ppo_gae_stage_records) of a minibatch: 1 (default, PPO_FUSED_DIRECT) = each row's 128-B record
  * through the row indices, one chunk ahead, inside the fused launch (the step tail gathers
  * nothing); 0 = the gathered copy written by the prep kernel or the previous step tail.  Bitwise

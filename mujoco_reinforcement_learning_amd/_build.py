@@ -11,7 +11,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip", "csrc/fused_update4.hip",
+SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip",
            "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip",
            "csrc/cnn_engine.hip", "csrc/gemm_ops.hip", "csrc/wide_gemm.hip",
            "csrc/wide_engine.hip", "csrc/comm.hip"]

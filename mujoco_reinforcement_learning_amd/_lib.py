@@ -125,7 +125,6 @@ _SIGNATURES = {
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p]),
     "ppo_ctx_set_rng_counter": (c_int, [c_void_p, c_void_p]),
-    "ppo_ctx_fused_variant": (c_int, [c_void_p, c_int]),
     "ppo_ctx_fused_direct": (c_int, [c_void_p, c_int]),
     "ppo_ctx_set_precision": (c_int, [c_void_p, c_int]),
     "ppo_ctx_timing": (c_int, [c_void_p, c_int, c_int]),

@@ -58,7 +58,6 @@ struct ppo_ctx {
   int64_t frec_cap, frec_rows;
   uint64_t *fstamps;            // diagnostics: per-phase cycle sums (ppo_ctx_phase_stamps)
   int fstamp_on, fstamp_g;
-  int fused4;                   // ppo_ctx_fused_variant: 1 -> fused_update4_kernel (ReLU)
   int fdirect;                  // ppo_ctx_fused_direct: the 8-wave kernel reads staged records via rows
   // which minibatch the gathered copy (fxb / fsrow) holds: the rows_d pointer and count of the
   // last staged gather (prep or step tail), nullptr when unknown -- PPO_STAGED_ROWS_GATHERED is

@@ -112,7 +112,6 @@ struct FusedArgs {
   int64_t slab_stride;
   float *loss_part;            // (G, 2): actor / critic loss-term sums per workgroup
   int G;                       // workgroups per net
-  bool v4;                     // run fused_update4_kernel (4 waves, 128-row chunks)
   uint64_t *stamps;            // diagnostics: (2, G, 11) per-phase cycle sums, or null
 };
 // Gather the minibatch (bf16 states + row scalars) and, with q.pack_w, refresh the bf16 weight
@@ -120,11 +119,6 @@ struct FusedArgs {
 int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // The persistent fused forward + loss + backward kernel.  grid (G, 2), 512 threads.
 int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
-// The 4-wave / 128-row re-decomposition of the same kernel (fused_update4.hip; ReLU, H = 256):
-// grid (G, 2), 256 threads, G = ceil(b / kFused4Rows) capped at kFusedMaxWG.
-constexpr int kFused4Rows = 128;
-bool fused_update4_ok(const FusedArgs &q);
-int fused_update4_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).
 bool fused_width_ok(int hidden);
 

@@ -688,8 +688,6 @@ static int forward_hidden(ppo_ctx *ctx, const bool use[2], const float *x, const
 }
 
 static const int g_fused_enabled = env_knob("PPO_FUSED", 1);
-// PPO_FUSED4=1: the 4-wave / 128-row fused update (fused_update4.hip) for ReLU nets
-static const int g_fused4 = env_knob("PPO_FUSED4", 0);
 // PPO_FUSED_DIRECT=0: the 8-wave fused update reads the gathered xb / srow copies (written by the
 // prep kernel or the previous step tail) instead of the staged records through the row indices
 // (the ctx default; ppo_ctx_fused_direct switches it)
@@ -761,10 +759,8 @@ static FusedArgs fused_args(ppo_ctx *ctx, const float *states_d, const float *ac
   q.slab_stride = ctx->total_params;
   q.loss_part = ctx->floss;
   q.stamps = ctx->fstamp_on ? ctx->fstamps : nullptr;
-  // the 4-wave kernel when selected (its phase-stamp build covers act_dim 5-6 only)
-  q.v4 = ctx->fused4 && fused_update4_ok(q) && (!q.stamps || (q.act_dim > 4 && q.act_dim <= 6));
-  q.G = std::min(kFusedMaxWG, ceil_div(b, q.v4 ? kFused4Rows : kFusedRows));
-  q.direct = staged && !q.v4 && ctx->fdirect;
+  q.G = std::min(kFusedMaxWG, ceil_div(b, kFusedRows));
+  q.direct = staged && ctx->fdirect;
   return q;
 }
 
@@ -810,12 +806,10 @@ static int fused_forward_backward(ppo_ctx *ctx, const FusedArgs &q, hipStream_t 
                     4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
   const int na = A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8;
   const TimRec rec{KC_FUSED,
-                   tim_active() ? (q.v4 ? intern_name("ppo::f4::fused_update4_kernel<%d>", na)
-                                        : intern_name("fused_update_kernel<%d, %d, %d, false>", H,
-                                                      q.act, na))
+                   tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act, na)
                                 : nullptr,
                    fl, by};
-  return q.v4 ? fused_update4_launch(q, rec, st) : fused_update_launch(q, rec, st);
+  return fused_update_launch(q, rec, st);
 }
 
 static ReduceArgs fused_reduce_args(const ppo_ctx *ctx, const FusedArgs &q, float *grad_d,
@@ -1071,7 +1065,6 @@ extern "C" int ppo_ctx_create(const ppo_net_cfg *cfg, int device, ppo_ctx **out)
       c += static_cast<int64_t>(kFusedMaxWG) * off * 4;
       ctx->floss = reinterpret_cast<float *>(c);
       c += kFusedMaxWG * 2 * 4;
-      ctx->fused4 = g_fused4 != 0;
       ctx->fdirect = g_fused_direct != 0;
     }
   }
@@ -1821,15 +1814,6 @@ extern "C" int ppo_ctx_set_precision(ppo_ctx *ctx, int prec) {
   ctx->prec = prec;
   if (prec == PPO_PREC_BF16)  // the wide path's workspace, for the shapes it covers
     if (int rc = wide_alloc(ctx)) return rc;
-  return 0;
-}
-
-extern "C" int ppo_ctx_fused_variant(ppo_ctx *ctx, int variant) {
-  PPO_REQUIRE(ctx != nullptr, "ppo_ctx_fused_variant: null ctx");
-  if (variant < 0) return ctx->fused4 ? 4 : 8;
-  PPO_REQUIRE(variant == 4 || variant == 8, "ppo_ctx_fused_variant: variant %d (4 or 8)", variant);
-  ctx->fused4 = variant == 4;
-  note_gathered(ctx, nullptr, 0);
   return 0;
 }
 

@@ -224,13 +224,6 @@ class Engine:
         check(self.lib.ppo_ctx_set_rng_counter(self._ctx, ptr(counter)))
         self._rng_counter = counter  # keep the buffer alive while the ctx may read it
 
-    def fused_variant(self, variant: Optional[int] = None) -> int:
-        """The fused bf16 update kernel (ppo_ctx_fused_variant): 8 = 8 waves / 64-row chunks,
-        4 = one wave per SIMD / 128-row chunks (ReLU); set it with variant, return the current."""
-        if variant is not None:
-            check(self.lib.ppo_ctx_fused_variant(self._ctx, int(variant)))
-        return int(self.lib.ppo_ctx_fused_variant(self._ctx, -1))
-
     def fused_direct(self, enable: Optional[bool] = None) -> bool:
         """ppo_ctx_fused_direct: the 8-wave fused kernel reads the staged records through the row
         indices itself (True, default) or the gathered copy (False); returns the current mode."""

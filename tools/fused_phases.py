@@ -14,11 +14,6 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-SEGMENTS4 = ["0 prologue (LDS images, constants, first X)", "1 L0 fwd + A1 image (+ W1 ring prime)",
-             "2 barrier", "3 L1 fwd MFMA passes + A2 image", "4 barrier",
-             "5 head z on MFMA + loss", "6 barrier", "7 head dW + d2 + D2 image (in place)",
-             "8 barrier", "9 dW1 wgrad (MFMA, tr reads; next X parked)",
-             "10 dgrad passes + D1 image + dW0 + chunk barrier", "11 epilogue: slab stores drained"]
 SEGMENTS = ["0 X stage + W0 frags", "1 L0 fwd (+ W1 ring prime)", "2 L1 fwd MFMA pass",
             "3 bias/act -> A2 image (+ row scalars to LDS)", "4 head z on MFMA + loss (waves 0-3)",
             "5 d2 = dz.Wh + head dW (MFMA) + D2 image", "6 dW1 wgrad (MFMA, tr reads)",
@@ -26,7 +21,7 @@ SEGMENTS = ["0 X stage + W0 frags", "1 L0 fwd (+ W1 ring prime)", "2 L1 fwd MFMA
             "10 prologue (LDS images, constants)", "11 epilogue: slab stores drained"]
 
 
-def main(variant: int = 8):
+def main():
     from mujoco_reinforcement_learning_amd.agent import PPOEngineAgent
     from mujoco_reinforcement_learning_amd.runconfig import make_run
     from mujoco_reinforcement_learning_amd import engine as E
@@ -44,8 +39,7 @@ def main(variant: int = 8):
     rows = torch.empty(b, dtype=torch.int32, device=dev)
     loss = torch.empty(2, device=dev)
     eng = agent.engine
-    eng.fused_variant(variant)
-    segments = SEGMENTS4 if variant == 4 else SEGMENTS
+    segments = SEGMENTS
     res = {}
     for rep in range(3):
         E.feistel_rows(1, rep, 0, b, n, t, rows)
@@ -68,8 +62,8 @@ def main(variant: int = 8):
             print(f"   {v:10.0f}  {100 * v / max(tot, 1):5.1f}%  {name}")
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "fused_phases.json"), "w") as f:
-        json.dump({"segments": segments, "variant": variant, **res}, f, indent=1)
+        json.dump({"segments": segments, **res}, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 8)
+    main()

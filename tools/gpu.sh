@@ -226,19 +226,6 @@ for S in $STEPS; do
       timeout -k 10 500 python bench.py --model lstm --steps 2 --warmup 1 \
         > gpurun_out/bench_${TAG}_lstm.json 2> gpurun_out/bench_${TAG}_lstm.err || fail lstm gpurun_out/bench_${TAG}_lstm.err
       for c in ant hum8k cnn lstm; do cut -c1-200 gpurun_out/bench_${TAG}_$c.json; done ;;
-    ab4)
-      # the fused update kernel variants on the headline line: 8 waves / 64 rows vs 4 waves / 128
-      for V in ${AB4:-0:0 1:0 1:1 1:2}; do
-        F4=${V%%:*}; CF=${V##*:}; OUT=gpurun_out/bench_${TAG}_f4_${F4}_${CF}
-        PPO_FUSED4=$F4 PPO_F4_CFG=$CF timeout -k 10 300 python bench.py --no-cpu-baseline --no-legs $BENCH_ARGS \
-          > $OUT.json 2> $OUT.err || fail ab4 $OUT.err
-        python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value']/1e6,2), 'M', round(d['ms_per_step'],3), 'ms', r['kernel'], round(r['avg_launch_us'],2), 'us', round(r['frac'],4))" $OUT.json $V
-      done ;;
-    phases4)
-      for C in ${F4CFGS:-0 1 2}; do
-        PPO_F4_CFG=$C timeout -k 10 200 python tools/fused_phases.py 4 > gpurun_out/phases4_${TAG}_$C.txt 2>&1 || fail phases4 gpurun_out/phases4_${TAG}_$C.txt
-        echo "cfg $C"; cat gpurun_out/phases4_${TAG}_$C.txt
-      done ;;
     wbench)
       timeout -k 10 200 python tools/wide_bench.py 20 > gpurun_out/wbench_${TAG}.txt 2>&1 || fail wbench gpurun_out/wbench_${TAG}.txt
       cat gpurun_out/wbench_${TAG}.txt ;;
