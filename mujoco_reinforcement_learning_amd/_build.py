@@ -13,7 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/scan_kernels.hip", "csrc/mlp_engine.hip", "csrc/fused_update.hip",
            "csrc/fused_policy.hip", "csrc/bilstm.hip", "csrc/host_rollout.hip",
-           "csrc/cnn_engine.hip", "csrc/gemm_ops.hip", "csrc/wide_gemm.hip",
+           "csrc/cnn_engine.hip", "csrc/gemm_ops_fwd_nk.hip", "csrc/gemm_ops_fwd_kn.hip",
+           "csrc/gemm_ops_dx.hip", "csrc/gemm_ops_wgrad.hip", "csrc/wide_gemm.hip",
            "csrc/wide_engine.hip", "csrc/comm.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-Wall", "-Wno-unused-result"]

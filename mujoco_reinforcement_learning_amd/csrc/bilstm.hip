@@ -26,6 +26,10 @@
 //   stacked layers dX = sum_d dG_d W_ih_d.
 // GEMMs are the engine's MFMA templates (exact-f32 v_mfma_f32_32x32x2_f32 by default, bf16
 // operands in PPO_PREC_BF16); the slabs reduce with reduce_slab_block in a fixed order.
+// In bf16 mode the producers of the operands only GEMMs read -- the gathered states, h_prev and
+// dG -- write them as bf16 (the RNE rounding the GEMM would apply while staging), so the
+// weight-gradient, recurrent-gradient and input-gradient GEMMs move half the bytes; the bias
+// gradients (column sums of dG) are then sums of those bf16 values.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -75,6 +79,7 @@ struct CellArgs {
   float *c;            // [B*W][2H] cell states
   float *y;            // [B*W][2H] layer output h
   float *hp;           // [B*W][2H] h_prev (zeros at each direction's first step)
+  __bf16 *hp16;        // bf16 mode: h_prev as bf16 instead (the dW_hh GEMM's only operand use)
   float *feat;         // optional act(h): mode 1 -> [B*W][2H] (actor), mode 2 -> [B][2H] at t=W-1
   int feat_mode, act;
   int b, w, h, s;
@@ -123,7 +128,11 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
   *reinterpret_cast<float4 *>(g + 3 * H + j) = make_float4(og[0], og[1], og[2], og[3]);
   *reinterpret_cast<float4 *>(q.c + o) = make_float4(c[0], c[1], c[2], c[3]);
   *reinterpret_cast<float4 *>(q.y + o) = make_float4(h[0], h[1], h[2], h[3]);
-  *reinterpret_cast<float4 *>(q.hp + o) = hp4;
+  if (q.hp16)
+    *reinterpret_cast<uint2 *>(q.hp16 + o) =
+        make_uint2(pack_bf16x2(hp4.x, hp4.y), pack_bf16x2(hp4.z, hp4.w));
+  else
+    *reinterpret_cast<float4 *>(q.hp + o) = hp4;
   if (q.feat_mode == 1 || (q.feat_mode == 2 && t == W - 1)) {
     float *f = q.feat_mode == 1 ? q.feat + o : q.feat + b * (2 * H) + d * H + j;
     *reinterpret_cast<float4 *>(f) = make_float4(act_forward(h[0], q.act), act_forward(h[1], q.act),
@@ -267,7 +276,8 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
       g[3 * H + j] = og;
       c.c[o] = cn;
       c.y[o] = h;
-      c.hp[o] = hpv[u];
+      if (c.hp16) c.hp16[o] = static_cast<__bf16>(hpv[u]);
+      else c.hp[o] = hpv[u];
       if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
       else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
     }
@@ -283,6 +293,7 @@ struct CellBwdArgs {
   int dy_mode;         // 1: dy full, 2: dy_last
   const float *dh_rec; // [B][2H] recurrent gradient (nullptr at s = 0)
   float *dcarry;       // [B][2H] dc flowing to the previous forward step
+  __bf16 *dg16;        // bf16 mode: dG written here as bf16 ([B*W][8H], g's layout) instead of g
   int b, w, h, s;
 };
 
@@ -336,6 +347,15 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
     dout[e] = (d_o * (1.f - og[e])) * og[e];
   }
   st4(q.dcarry + r, carry);
+  if (q.dg16) {
+    __bf16 *g16 = q.dg16 + (b * W + t) * (8 * H) + d * (4 * H);
+    const lstm_f4 gv[4] = {di, df, dg, dout};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      *reinterpret_cast<uint2 *>(g16 + k * H + j) =
+          make_uint2(pack_bf16x2(gv[k][0], gv[k][1]), pack_bf16x2(gv[k][2], gv[k][3]));
+    return;
+  }
   st4(g + j, di);
   st4(g + H + j, df);
   st4(g + 2 * H + j, dg);
@@ -375,13 +395,16 @@ __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) 
   (void)reduce_slab_block(q, blockIdx.x);
 }
 
+// xg16 (bf16 mode): the rows as bf16 instead of f32 (GEMM operands only)
 __global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
                                         const int32_t *__restrict__ rows, int b, int din,
-                                        float *__restrict__ xg) {
+                                        float *__restrict__ xg, __bf16 *__restrict__ xg16) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= static_cast<int64_t>(b) * din) return;
   const int64_t j = i / din;
-  xg[i] = states[static_cast<int64_t>(rows[j]) * din + (i - j * din)];
+  const float v = states[static_cast<int64_t>(rows[j]) * din + (i - j * din)];
+  if (xg16) xg16[i] = static_cast<__bf16>(v);
+  else xg[i] = v;
 }
 
 __global__ void add_inplace_kernel(float *__restrict__ a, const float *__restrict__ b, int64_t n) {
@@ -534,6 +557,10 @@ struct ppo_lstm_ctx {
   float *x;                          // [rows][W*O] gathered states
   float *g[2][PPO_MAX_LAYERS];       // [rows*W][8H]
   float *c[2][PPO_MAX_LAYERS], *y[2][PPO_MAX_LAYERS], *hp[2][PPO_MAX_LAYERS];  // [rows*W][2H]
+  // bf16 mode: the GEMM-only operands as bf16 (gathered states, dG, h_prev)
+  __bf16 *x16;                       // [rows][W*O]
+  __bf16 *dg16[2][PPO_MAX_LAYERS];   // [rows*W][8H]
+  __bf16 *hp16[2][PPO_MAX_LAYERS];   // [rows*W][2H]
   float *gh, *dhrec, *dcarry;        // [rows][8H], [rows][2H], [rows][2H]
   float *dy[2], *tmp;                // [rows*W][2H]
   float *feat_a, *feat_c;            // [rows][W*2H], [rows][2H]
@@ -639,16 +666,20 @@ int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int ma
 
 // LSTM net z forward over xin [b*W][O] (batch-major rows); fills g/c/y/hp of every layer and the
 // features of the top layer (actor: all steps, critic: t = W-1).
-int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st) {
+// xin16 (bf16 mode, nullable): the same rows as bf16 -- the input projection reads those.
+int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, int b,
+                 hipStream_t st) {
   const LstmNet &N = x->net[z];
   const int H = N.hidden, W = x->cfg.window;
   const float *P = x->params;
+  const bool b16 = x->prec == PPO_PREC_BF16;
   for (int l = 0; l < N.layers; ++l) {
     const LstmLayer &L = N.l[l];
     const float *in = l == 0 ? xin : x->y[z][l - 1];
     GemmProblem p[2] = {};
     for (int d = 0; d < 2; ++d) {
       p[d].a = in;
+      p[d].a16 = l == 0 ? xin16 : nullptr;
       p[d].lda = L.in;
       p[d].b = P + L.w_ih[d];
       p[d].ldb = L.in;
@@ -669,6 +700,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st
         a.cell.c = x->c[z][l];
         a.cell.y = x->y[z][l];
         a.cell.hp = x->hp[z][l];
+        a.cell.hp16 = b16 ? x->hp16[z][l] : nullptr;
         const bool top = l == N.layers - 1;
         a.cell.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
         a.cell.feat = z == 0 ? x->feat_a : x->feat_c;
@@ -682,8 +714,9 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st
         TimRec rec{KC_LSTM, "lstm_step_fwd_kernel", 0.0, 0.0};
         if (tim_active()) {
           rec.flops = 2.0 * 2 * b * 4.0 * H * H;
-          // W_hh and h_prev once, Gx / c_prev / h_prev in, gates / c / h / h_prev out (f32)
-          rec.bytes = 4.0 * (2 * 4.0 * H * H + 2.0 * b * H * (1 + 4 + 2 + 4 + 3));
+          // W_hh and h_prev once, Gx / c_prev / h_prev in, gates / c / h out (f32), h_prev out
+          // (bf16 in bf16 mode)
+          rec.bytes = 4.0 * 2 * 4.0 * H * H + 2.0 * b * H * (4.0 * (1 + 4 + 2 + 4 + 2) + (b16 ? 2.0 : 4.0));
         }
         launch_k(rec, lstm_step_fwd_kernel, dim3(ceil_div(b, kStepRows), H / kStepUnits, 2),
                  dim3(256), 0, st, a);
@@ -714,6 +747,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st
       a.c = x->c[z][l];
       a.y = x->y[z][l];
       a.hp = x->hp[z][l];
+      a.hp16 = b16 ? x->hp16[z][l] : nullptr;
       const bool top = l == N.layers - 1;
       a.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
       a.feat = z == 0 ? x->feat_a : x->feat_c;
@@ -818,11 +852,13 @@ int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm
 
 // BPTT of LSTM net z given dY of the top layer (actor: full [b*W][2H] in x->dy[0]; critic: the
 // [b][2H] gradient of h at t = W-1 in x->dy[0]); weight grads into the slabs.
-int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t st,
-                  const float *dy2 = nullptr) {
+// xin16 (bf16 mode): the gathered rows as bf16; dG and h_prev then come from dg16 / hp16.
+int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, int b,
+                  hipStream_t st, const float *dy2 = nullptr) {
   const LstmNet &N = x->net[z];
   const int H = N.hidden, W = x->cfg.window;
   const float *P = x->params;
+  const bool b16 = x->prec == PPO_PREC_BF16;
   int cur = 0;
   for (int l = N.layers - 1; l >= 0; --l) {
     const LstmLayer &L = N.l[l];
@@ -833,6 +869,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
         for (int d = 0; d < 2; ++d) {
           const int tn = d == 0 ? W - s : s - 1;  // the step back-propagated at s - 1
           p[d].a = x->g[z][l] + static_cast<int64_t>(tn) * 8 * H + d * 4 * H;
+          if (b16) p[d].a16 = x->dg16[z][l] + static_cast<int64_t>(tn) * 8 * H + d * 4 * H;
           p[d].lda = static_cast<int64_t>(W) * 8 * H;
           p[d].b = P + L.w_hh[d];
           p[d].ldb = H;
@@ -852,6 +889,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
       a.dy_last = x->dy[cur];
       a.dh_rec = s > 0 ? x->dhrec : nullptr;
       a.dcarry = x->dcarry;
+      a.dg16 = b16 ? x->dg16[z][l] : nullptr;
       a.b = b;
       a.w = W;
       a.h = H;
@@ -864,8 +902,10 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
     GemmProblem pi[2] = {}, ph[2] = {};
     for (int d = 0; d < 2; ++d) {
       pi[d].a = x->g[z][l] + d * 4 * H;
+      if (b16) pi[d].a16 = x->dg16[z][l] + d * 4 * H;
       pi[d].lda = 8 * H;
       pi[d].b = in;
+      pi[d].b16 = l == 0 ? xin16 : nullptr;
       pi[d].ldb = L.in;
       pi[d].c = x->slabs + L.w_ih[d];
       pi[d].ldc = L.in;
@@ -874,6 +914,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
       pi[d].n = L.in;
       ph[d] = pi[d];
       ph[d].b = x->hp[z][l] + d * H;
+      ph[d].b16 = b16 ? x->hp16[z][l] + d * H : nullptr;
       ph[d].ldb = 2 * H;
       ph[d].c = x->slabs + L.w_hh[d];
       ph[d].ldc = H;
@@ -887,6 +928,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, int b, hipStream_t s
       for (int d = 0; d < 2; ++d) {
         GemmProblem p{};
         p.a = x->g[z][l] + d * 4 * H;
+        if (b16) p.a16 = x->dg16[z][l] + d * 4 * H;
         p.lda = 8 * H;
         p.b = P + L.w_ih[d];
         p.ldb = L.in;
@@ -913,9 +955,9 @@ int check_rows(ppo_lstm_ctx *x, int b) {
   return 0;
 }
 
-int forward_all(ppo_lstm_ctx *x, const float *xin, int b, hipStream_t st) {
-  if (int rc = lstm_forward(x, 0, xin, b, st)) return rc;
-  if (int rc = lstm_forward(x, 1, xin, b, st)) return rc;
+int forward_all(ppo_lstm_ctx *x, const float *xin, const __bf16 *xin16, int b, hipStream_t st) {
+  if (int rc = lstm_forward(x, 0, xin, xin16, b, st)) return rc;
+  if (int rc = lstm_forward(x, 1, xin, xin16, b, st)) return rc;
   const Mlp *am[2] = {&x->mu, &x->ls};
   float *const *aa[2] = {x->act_mu, x->act_ls};
   if (int rc = mlp_forward(x, am, aa, 2, x->feat_a, b, st)) return rc;
@@ -975,14 +1017,17 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
     return at;
   };
   const int64_t o_x = take(R * W * O);
+  const int64_t o_x16 = take((R * W * O + 1) / 2);  // bf16 buffers: half the floats
   int64_t o_g[2][PPO_MAX_LAYERS], o_c[2][PPO_MAX_LAYERS], o_y[2][PPO_MAX_LAYERS],
-      o_hp[2][PPO_MAX_LAYERS];
+      o_hp[2][PPO_MAX_LAYERS], o_dg16[2][PPO_MAX_LAYERS], o_hp16[2][PPO_MAX_LAYERS];
   for (int z = 0; z < 2; ++z)
     for (int l = 0; l < x->net[z].layers; ++l) {
       o_g[z][l] = take(R * W * 8 * H);
       o_c[z][l] = take(R * W * 2 * H);
       o_y[z][l] = take(R * W * 2 * H);
       o_hp[z][l] = take(R * W * 2 * H);
+      o_dg16[z][l] = take(R * W * 4 * H);
+      o_hp16[z][l] = take(R * W * H);
     }
   const int64_t o_gh = take(R * 8 * H), o_dhrec = take(R * 2 * H), o_dcarry = take(R * 2 * H);
   const int64_t o_dy0 = take(R * W * 2 * H), o_dy1 = take(R * W * 2 * H);
@@ -1009,12 +1054,15 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   }
   float *w = x->ws;
   x->x = w + o_x;
+  x->x16 = reinterpret_cast<__bf16 *>(w + o_x16);
   for (int z = 0; z < 2; ++z)
     for (int l = 0; l < x->net[z].layers; ++l) {
       x->g[z][l] = w + o_g[z][l];
       x->c[z][l] = w + o_c[z][l];
       x->y[z][l] = w + o_y[z][l];
       x->hp[z][l] = w + o_hp[z][l];
+      x->dg16[z][l] = reinterpret_cast<__bf16 *>(w + o_dg16[z][l]);
+      x->hp16[z][l] = reinterpret_cast<__bf16 *>(w + o_hp16[z][l]);
     }
   x->gh = w + o_gh;
   x->dhrec = w + o_dhrec;
@@ -1100,7 +1148,7 @@ extern "C" int ppo_lstm_forward(ppo_lstm_ctx *x, const float *state_d, int n, fl
   PPO_HIP_TRY(hipSetDevice(x->device));
   TimingScope ts(x);
   hipStream_t st = as_stream(stream);
-  if (int rc = forward_all(x, state_d, n, st)) return rc;
+  if (int rc = forward_all(x, state_d, nullptr, n, st)) return rc;
   const int A = x->cfg.act_dim, W = x->cfg.window;
   const int64_t yb = sizeof(float) * static_cast<int64_t>(n) * W * 2 * x->cfg.latent;
   if (actor_lstm_out_d)
@@ -1137,7 +1185,7 @@ extern "C" int ppo_lstm_policy_step(ppo_lstm_ctx *x, const float *state_d, int n
   PPO_HIP_TRY(hipSetDevice(x->device));
   TimingScope ts(x);
   hipStream_t st = as_stream(stream);
-  if (int rc = forward_all(x, state_d, n, st)) return rc;
+  if (int rc = forward_all(x, state_d, nullptr, n, st)) return rc;
   const int nl = x->cfg.n_hidden;
   HeadArgs h{};
   h.mean = x->act_mu[nl];
@@ -1173,11 +1221,14 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   const ppo_lstm_cfg &c = x->cfg;
   const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
   const int din = W * O;
+  // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
+  // (rows of O values: the GEMMs' 8-B bf16 loads need O % 4 == 0, else the f32 rows as before)
+  const __bf16 *x16 = x->prec == PPO_PREC_BF16 && O % 4 == 0 ? x->x16 : nullptr;
   launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
            dim3(ceil_div(static_cast<int64_t>(b) * din, 256)), dim3(256), 0, st, states_d, rows_d,
-           b, din, x->x);
+           b, din, x->x, const_cast<__bf16 *>(x16));
   PPO_LAUNCHED();
-  if (int rc = forward_all(x, x->x, b, st)) return rc;
+  if (int rc = forward_all(x, x->x, x16, b, st)) return rc;
   HeadArgs h{};
   h.mean = x->act_mu[nl];
   h.u = x->act_ls[nl];
@@ -1213,7 +1264,7 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
     float *const *pp[2] = {x->dz[2], nullptr};
     if (int rc = mlp_backward(x, cm, ca, 1, x->feat_c, pp, x->dy[0], 2 * H, c.activation, b, st))
       return rc;
-    if (int rc = lstm_backward(x, 1, x->x, b, st)) return rc;
+    if (int rc = lstm_backward(x, 1, x->x, x16, b, st)) return rc;
   }
   {  // actor: both MLPs into one feature gradient, then BiLSTM
     const Mlp *am[2] = {&x->mu, &x->ls};
@@ -1222,7 +1273,7 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
     if (int rc = mlp_backward(x, am, aa, 2, x->feat_a, pp, x->dy[0],
                               static_cast<int64_t>(W) * 2 * H, c.activation, b, st, false))
       return rc;
-    if (int rc = lstm_backward(x, 0, x->x, b, st, x->tmp)) return rc;
+    if (int rc = lstm_backward(x, 0, x->x, x16, b, st, x->tmp)) return rc;
   }
   // slabs -> flat gradient, tensor by tensor in a fixed split order
   ReduceArgs r{};

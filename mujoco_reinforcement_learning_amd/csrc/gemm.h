@@ -37,6 +37,8 @@ struct GemmProblem {
   const float *aux;    // EPI_DX: layer input activations (same layout as c; c may alias it)
   float *colsum;       // EPI_PARTIAL: bias-gradient slab base, nullable
   int m, n;
+  // bf16 mode: the operand already bf16 in global memory (then a / b are unused), nullable
+  const __bf16 *a16, *b16;
 };
 
 struct GemmBatch {
@@ -342,15 +344,19 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 //   image [BK][R + 32] stored as it arrives (4 consecutive r of one k -> one 8-B store), and
 //   fragments come from ds_read_b64_tr_b16, the gfx950 transposing read (two per fragment).
 //   The 32-bf16 row padding makes a 32-lane half's 4 rows x 2 column groups cover all 64 banks.
-// V = 4: 16-B global loads.  sum4 (optional): f32 per-thread sums of the r-group's 4 values over
-// every k this thread staged (bias gradient of the wgrad A operand, before bf16 rounding).
-template <int R, int BK, int NT, int V, bool KC>
+// V = 4: 16-B global loads (8-B for a bf16 source).  sum4 (optional): f32 per-thread sums of the
+// r-group's 4 values over every k this thread staged (bias gradient of the wgrad A operand, before
+// bf16 rounding).  SRC16: the operand is already bf16 in global memory (a producer wrote the
+// RNE-rounded copy the f32 path would stage): its bits go to the image as loaded.
+template <int R, int BK, int NT, int V, bool KC, bool SRC16 = false>
 struct StageBF16 {
   static constexpr int NU = R * BK / (4 * NT);
   static_assert((R * BK) % (4 * NT) == 0, "tile/thread mismatch");
   static constexpr int ROW = KC ? BK + 8 : R + 32;  // image row stride (bf16)
   static constexpr int IMAGE = KC ? R * ROW : BK * ROW;
-  float v[NU][4];
+  using Src = typename std::conditional<SRC16, __bf16, float>::type;
+  float v[SRC16 ? 1 : NU][4];
+  uint2 raw[SRC16 ? NU : 1];  // SRC16: 4 bf16 per unit
 
   __device__ __forceinline__ static void coords(int e, int &rr, int &kk) {
     if (KC) {
@@ -372,15 +378,30 @@ struct StageBF16 {
       for (int j = 0; j < 4; ++j) out[j] = (full || first + j < lim) ? src[j] : 0.f;
     }
   }
+  // 4 consecutive bf16 of one global row starting at column `first` (limit `lim`), zero past it
+  __device__ __forceinline__ static uint2 quad16(const __bf16 *src, int first, int lim, bool full) {
+    if (V == 4 && (full || first + 3 < lim)) return *reinterpret_cast<const uint2 *>(src);
+    const uint16_t *s16 = reinterpret_cast<const uint16_t *>(src);
+    uint32_t h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[j] = (full || first + j < lim) ? s16[j] : 0u;
+    return make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  }
   template <bool FULL>
-  __device__ __forceinline__ void load(const float *base, int64_t ld, int r0, int rlim, int k0,
+  __device__ __forceinline__ void load(const Src *base, int64_t ld, int r0, int rlim, int k0,
                                        int kend, int tid) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       int rr, kk;
       coords(tid + u * NT, rr, kk);
       const int gr = r0 + rr, gk = k0 + kk;
-      if (KC) {
+      if constexpr (SRC16) {
+        const bool in = KC ? (FULL || gr < rlim) : (FULL || gk < kend);
+        raw[u] = !in ? make_uint2(0u, 0u)
+                     : KC ? quad16(base + static_cast<int64_t>(gr) * ld + gk, gk, kend, FULL)
+                          : quad16(base + static_cast<int64_t>(gk) * ld + gr, gr, rlim, FULL);
+        continue;
+      } else if (KC) {
         if (FULL || gr < rlim) quad(base + static_cast<int64_t>(gr) * ld + gk, gk, kend, FULL, v[u]);
         else
 #pragma unroll
@@ -395,9 +416,17 @@ struct StageBF16 {
   }
   __device__ __forceinline__ void sum4(float (&acc)[4]) const {  // !KC: rr is fixed per thread
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+    for (int u = 0; u < NU; ++u) {
+      if constexpr (SRC16) {  // bf16 -> f32 is exact: the sums of the values the MFMAs consume
+        acc[0] += __uint_as_float(raw[u].x << 16);
+        acc[1] += __uint_as_float(raw[u].x & 0xffff0000u);
+        acc[2] += __uint_as_float(raw[u].y << 16);
+        acc[3] += __uint_as_float(raw[u].y & 0xffff0000u);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += v[u][j];
+        for (int j = 0; j < 4; ++j) acc[j] += v[u][j];
+      }
+    }
   }
   __device__ __forceinline__ void store(__bf16 *s, int tid) const {
 #pragma unroll
@@ -405,8 +434,11 @@ struct StageBF16 {
       int rr, kk;
       coords(tid + u * NT, rr, kk);
       __bf16 *dst = KC ? s + rr * ROW + kk : s + kk * ROW + rr;
-      *reinterpret_cast<uint2 *>(dst) =
-          make_uint2(pack_bf16x2(v[u][0], v[u][1]), pack_bf16x2(v[u][2], v[u][3]));
+      if constexpr (SRC16)
+        *reinterpret_cast<uint2 *>(dst) = raw[u];
+      else
+        *reinterpret_cast<uint2 *>(dst) =
+            make_uint2(pack_bf16x2(v[u][0], v[u][1]), pack_bf16x2(v[u][2], v[u][3]));
     }
   }
   // MFMA 32x32x16 operand fragment of the 32-row block at tile-local row r0, k-step ks:
@@ -429,14 +461,15 @@ struct StageBF16 {
   }
 };
 
-template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI, int VA, int VB>
+template <int TM, int TN, int WM, int WN, int BK, int AMODE, int BMODE, int EPI, int VA, int VB,
+          bool A16 = false, bool B16 = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(GemmBatch gb) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 32 * TM * WM;
   constexpr int BN = 32 * TN * WN;
   static_assert(BK % 16 == 0, "BK must be a multiple of 16 for 32x32x16");
-  using StA = StageBF16<BM, BK, NT, VA, AMODE == A_MK>;
-  using StB = StageBF16<BN, BK, NT, VB, BMODE == B_NK>;
+  using StA = StageBF16<BM, BK, NT, VA, AMODE == A_MK, A16>;
+  using StB = StageBF16<BN, BK, NT, VB, BMODE == B_NK, B16>;
   constexpr int IMG = StA::IMAGE + StB::IMAGE;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * IMG];
 
@@ -464,12 +497,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(GemmBatch gb) {
 
   StA ta;
   StB tb;
+  const typename StA::Src *pa;
+  const typename StB::Src *pb;
+  if constexpr (A16) pa = P.a16; else pa = P.a;
+  if constexpr (B16) pb = P.b16; else pb = P.b;
   auto gload = [&](int k0) {
     const bool kfull = k0 + BK <= kend;
-    if (kfull && m0 + BM <= M) ta.template load<true>(P.a, P.lda, m0, M, k0, kend, tid);
-    else ta.template load<false>(P.a, P.lda, m0, M, k0, kend, tid);
-    if (kfull && n0 + BN <= N) tb.template load<true>(P.b, P.ldb, n0, N, k0, kend, tid);
-    else tb.template load<false>(P.b, P.ldb, n0, N, k0, kend, tid);
+    if (kfull && m0 + BM <= M) ta.template load<true>(pa, P.lda, m0, M, k0, kend, tid);
+    else ta.template load<false>(pa, P.lda, m0, M, k0, kend, tid);
+    if (kfull && n0 + BN <= N) tb.template load<true>(pb, P.ldb, n0, N, k0, kend, tid);
+    else tb.template load<false>(pb, P.ldb, n0, N, k0, kend, tid);
   };
   auto lstore = [&](int buf) {
     __bf16 *As = lds + buf * IMG;
@@ -591,22 +628,68 @@ static void launch_gemm_v(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t
 
 constexpr int kGemmBKBf16 = 64;
 
-template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int VA, int VB>
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int VA, int VB,
+          bool A16 = false, bool B16 = false>
 static void launch_gemm_bf16_v(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t st) {
   TimRec rec{EPI == EPI_FWD ? KC_GEMM_FWD : (EPI == EPI_DX ? KC_GEMM_DGRAD : KC_GEMM_WGRAD),
              nullptr, 0.0, 0.0};
   if (tim_active()) {
-    rec.name = intern_name("gemm_bf16_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", TM, TN,
-                           WM, WN, kGemmBKBf16, AMODE, BMODE, EPI, VA, VB);
+    rec.name = (A16 || B16)
+                   ? intern_name("gemm_bf16_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %s, %s>",
+                                 TM, TN, WM, WN, kGemmBKBf16, AMODE, BMODE, EPI, VA, VB,
+                                 A16 ? "true" : "false", B16 ? "true" : "false")
+                   : intern_name("gemm_bf16_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", TM, TN,
+                                 WM, WN, kGemmBKBf16, AMODE, BMODE, EPI, VA, VB);
     rec.flops = gemm_flops(gb, nprob, EPI);
-    for (int i = 0; i < nprob; ++i) {  // algorithmic: f32 A + B read once, C written once
+    // algorithmic: A + B read once (4 B, or 2 B for a bf16 operand), C written once (f32)
+    const double ea = A16 ? 2.0 : 4.0, eb = B16 ? 2.0 : 4.0;
+    for (int i = 0; i < nprob; ++i) {
       const GemmProblem &p = gb.p[i];
-      rec.bytes += 4.0 * (static_cast<double>(p.m) * gb.k + static_cast<double>(gb.k) * p.n +
-                          static_cast<double>(p.m) * p.n * (EPI == EPI_DX ? 2 : 1));
+      rec.bytes += ea * static_cast<double>(p.m) * gb.k + eb * static_cast<double>(gb.k) * p.n +
+                   4.0 * static_cast<double>(p.m) * p.n * (EPI == EPI_DX ? 2 : 1);
     }
   }
-  launch_k(rec, gemm_bf16_kernel<TM, TN, WM, WN, kGemmBKBf16, AMODE, BMODE, EPI, VA, VB>, grid,
-           dim3(64 * WM * WN), 0, st, gb);
+  launch_k(rec, gemm_bf16_kernel<TM, TN, WM, WN, kGemmBKBf16, AMODE, BMODE, EPI, VA, VB, A16, B16>,
+           grid, dim3(64 * WM * WN), 0, st, gb);
+}
+
+// 8-B vector loads of a bf16 operand: ld % 4 == 0 and an 8-B aligned base, every problem
+static bool vec4_ok16(const GemmBatch &gb, int nprob, bool operand_a) {
+  for (int i = 0; i < nprob; ++i) {
+    const GemmProblem &p = gb.p[i];
+    const int64_t ld = operand_a ? p.lda : p.ldb;
+    const void *base = operand_a ? static_cast<const void *>(p.a16) : static_cast<const void *>(p.b16);
+    if (ld % 4 || reinterpret_cast<uintptr_t>(base) % 8) return false;
+  }
+  return true;
+}
+
+// bf16 operands from global memory (the BiLSTM's dG, h_prev and gathered rows): A alone (FWD,
+// PARTIAL) or A and B (PARTIAL), vector loads only -- the producers keep those buffers
+// 8-B aligned with ld % 4 == 0, which the host checks
+template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
+static int launch_gemm_bf16_src(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t st) {
+  const bool a16 = gb.p[0].a16 != nullptr, b16 = gb.p[0].b16 != nullptr;
+  for (int i = 1; i < nprob; ++i)
+    PPO_REQUIRE((gb.p[i].a16 != nullptr) == a16 && (gb.p[i].b16 != nullptr) == b16,
+                "gemm: mixed bf16 / f32 operands in one batch");
+  PPO_REQUIRE(a16 && vec4_ok16(gb, nprob, true) && (!b16 || vec4_ok16(gb, nprob, false)),
+              "gemm: bf16-source operands need A in bf16 and 8-B aligned rows (ld %% 4 == 0)");
+  // an f32 B operand (weights, or rows of an odd width) may need scalar loads
+  const bool vb = b16 || vec4_ok(gb, nprob, false);
+  if constexpr (EPI == EPI_DX) {
+    PPO_REQUIRE(false, "gemm: no bf16-source DX variant");
+  } else {
+    PPO_REQUIRE(!b16 || EPI == EPI_PARTIAL, "gemm: bf16 B operand only in the weight-gradient GEMM");
+    if (EPI == EPI_PARTIAL && b16)
+      launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, true>(gb, nprob, grid, st);
+    else if (vb)
+      launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, false>(gb, nprob, grid, st);
+    else
+      launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 1, true, false>(gb, nprob, grid, st);
+  }
+  PPO_LAUNCHED();
+  return 0;
 }
 
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI, int NBUF = 2>
@@ -616,6 +699,18 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
   dim3 grid(tiles, EPI == EPI_PARTIAL ? gb.splits : 1, nprob);
   const bool va = vec4_ok(gb, nprob, true), vb = vec4_ok(gb, nprob, false);
   if (gb.prec == PPO_PREC_BF16) {
+    // bf16 operands already in global memory (every problem of the batch alike); compiled for
+    // the tiles launch_big / run_rowwise / run_partial pick for them only
+    if (gb.p[0].a16 || gb.p[0].b16) {
+      constexpr bool tile_ok = (TM == 2 && TN == 1 && WM == 2 && WN == 4) ||
+                               (TM == 1 && TN == 1 && WM == 1 && WN == 4) ||
+                               (TM == 1 && TN == 1 && WM == 4 && WN == 1);
+      if constexpr (tile_ok) {
+        return launch_gemm_bf16_src<TM, TN, WM, WN, AMODE, BMODE, EPI>(gb, nprob, grid, st);
+      } else {
+        PPO_REQUIRE(false, "gemm: no bf16-source variant of the %dx%d tile", BM, BN);
+      }
+    }
     // the bf16 kernel is always double-buffered; NBUF only selects among the f32 variants
     if (va && vb)
       launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4>(gb, nprob, grid, st);
@@ -628,6 +723,8 @@ static int launch_gemm(const GemmBatch &gb, int nprob, int max_m, int max_n, hip
     PPO_LAUNCHED();
     return 0;
   }
+  for (int i = 0; i < nprob; ++i)
+    PPO_REQUIRE(!gb.p[i].a16 && !gb.p[i].b16, "gemm: bf16 operands need precision bf16");
   if (va && vb)
     launch_gemm_v<TM, TN, WM, WN, AMODE, BMODE, EPI, NBUF, 4, 4>(gb, nprob, grid, st);
   else if (va)
@@ -656,6 +753,11 @@ static const int g_w8 = env_knob("PPO_GEMM_W8", 1);
 
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_big(const GemmBatch &gb, int nprob, int max_m, int max_n, hipStream_t st) {
+  if constexpr ((TM == 2 && TN == 2 && WM == 2 && WN == 2) || (TM == 2 && TN == 4 && WM == 2 && WN == 2)) {
+    // bf16-source batches take the 8-wave 128x128 tile whatever the experiment knobs say
+    if (gb.p[0].a16 || gb.p[0].b16)
+      return launch_gemm<2, 1, 2, 4, AMODE, BMODE, EPI, 2>(gb, nprob, max_m, max_n, st);
+  }
   if constexpr (TM == 2 && TN == 2 && WM == 2 && WN == 2) {
     if (g_w8) {
       if (g_nbuf == 1)

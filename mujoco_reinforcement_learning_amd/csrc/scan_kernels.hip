@@ -345,16 +345,18 @@ __global__ void synthetic_env_step_kernel(const float *__restrict__ base_obs,
                                           double *__restrict__ obs_out,
                                           double *__restrict__ reward_out,
                                           uint8_t *__restrict__ term_out) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= static_cast<int64_t>(n) * o) return;
-  const int env = static_cast<int>(i / o);
-  const int f = static_cast<int>(i % o);
-  const double act = static_cast<double>(action[static_cast<int64_t>(env) * a + (f % a)]);
+  // 32-bit index arithmetic (the host checks n * o < 2^31): a 64-bit divide is a long
+  // software sequence ahead of the first load
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= static_cast<uint32_t>(n) * static_cast<uint32_t>(o)) return;
+  const uint32_t env = i / static_cast<uint32_t>(o);
+  const uint32_t f = i - env * static_cast<uint32_t>(o);
+  const double act = static_cast<double>(action[env * a + (f % static_cast<uint32_t>(a))]);
   obs_out[i] = static_cast<double>(base_obs[i]) + 0.1 * act;
   if (f == 0) {
     double ctrl = 0.0;
     for (int j = 0; j < a; ++j) {
-      const double aj = static_cast<double>(action[static_cast<int64_t>(env) * a + j]);
+      const double aj = static_cast<double>(action[env * a + j]);
       ctrl = ctrl + aj * aj;
     }
     reward_out[env] = static_cast<double>(base_reward[env]) - 0.01 * ctrl;
@@ -752,7 +754,8 @@ extern "C" int ppo_synthetic_env_step(const float *base_obs_d, const float *base
                                       int o, int a, double *obs_out_d, double *reward_out_d,
                                       uint8_t *term_out_d, void *stream) {
   PPO_REQUIRE(base_obs_d && base_reward_d && base_term_d && action_d && obs_out_d &&
-                  reward_out_d && term_out_d && n > 0 && o > 0 && a > 0,
+                  reward_out_d && term_out_d && n > 0 && o > 0 && a > 0 &&
+                  static_cast<int64_t>(n) * std::max(o, a) < (int64_t{1} << 31),
               "ppo_synthetic_env_step: bad args");
   const int64_t total = static_cast<int64_t>(n) * o;
   FreeTimingScope timing_scope;
