@@ -28,6 +28,8 @@
 // f32 values.  act'(a1) for tanh / ELU uses the f32 a1, recomputed in the dgrad epilogue (the
 // image holds bf16(a1)); ReLU needs only its sign, which the bf16 image keeps.
 #include <cstdio>
+#include <cstdlib>
+#include <type_traits>
 
 #include "adam_elem.h"
 #include "fused_common.h"
@@ -270,9 +272,10 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackArgs a, int gen_
 // ============================================================================================
 // Optimizer-step tail: slab reduction + Adam + weight images, and the next rows' gather
 // ============================================================================================
-__device__ __forceinline__ void tail_gather(const TailArgs &t, int64_t blk, int tid) {
-  const int j = static_cast<int>((blk * 256 + tid) >> 3);
-  const int u = tid & 7;
+// thread index idx of the gather part: row idx / 8, 16-B unit idx % 8 of its record
+__device__ __forceinline__ void tail_gather(const TailArgs &t, int64_t idx) {
+  const int j = static_cast<int>(idx >> 3);
+  const int u = static_cast<int>(idx & 7);
   if (j >= t.b) return;
   const int64_t sr = t.rows[j];
   uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -320,15 +323,16 @@ __device__ __forceinline__ void adam_apply(const AdamPackArgs &a, int64_t i, flo
 
 // One parameter block of the tail: fold its slabs (reduce_slab_block_s, fixed order) or take
 // the gradient already in a.g, then Adam + the bf16 weight images on the chunk-0 threads.
+template <int G>
 __device__ __forceinline__ void tail_block(const ReduceArgs &r, const TailArgs &t, int64_t blk,
                                            RedScratch sc) {
   const int tid = threadIdx.x;
   const AdamPackArgs &a = t.a;
-  const int64_t i = blk * kRedParams + 4 * (tid % kRedGroups);
-  const bool lead = tid < kRedGroups;  // chunk 0: the threads that own the reduced sums
+  const int64_t i = blk * (4 * G) + 4 * (tid % G);
+  const bool lead = tid < G;  // chunk 0: the threads that own the reduced sums
   float4 g4;
   if (t.reduce) {
-    g4 = reduce_slab_block_s(r, blk, sc);
+    g4 = reduce_slab_block_s<G>(r, blk, sc);
     if (!lead || i >= r.total) return;
   } else {
     if (!lead || i >= a.n) return;
@@ -338,15 +342,21 @@ __device__ __forceinline__ void tail_block(const ReduceArgs &r, const TailArgs &
              *reinterpret_cast<const float4 *>(a.m + i), *reinterpret_cast<const float4 *>(a.v + i));
 }
 
-__global__ __launch_bounds__(kRedThreads) void step_tail_kernel(ReduceArgs r, TailArgs t, int red_blocks) {
-  __shared__ __attribute__((aligned(16))) char scratch[kRedScratchBytes];
+// Blocks of G float4 groups x kRedChunks chunks (the per-parameter order of every G is the
+// same, reduce_slabs.h).  G = 32 (512 threads, 128 parameters a block) by default.  At 69 VGPRs a
+// CU holds 3 such blocks, so the headline's 1,115 run in two rounds; smaller blocks that fit in
+// one were measured slower all the same (PPO_TAIL_GROUPS, round 5: 1.32 ms per iteration at
+// G = 32, 1.38 at 16, 1.67 at 8).
+template <int G>
+__global__ __launch_bounds__(G * kRedChunks) void step_tail_kernel(ReduceArgs r, TailArgs t, int red_blocks) {
+  __shared__ __attribute__((aligned(16))) char scratch[red_scratch_bytes<G>()];
+  constexpr int NT = G * kRedChunks;
   const int tid = threadIdx.x;
-  if (static_cast<int>(blockIdx.x) >= red_blocks) {  // 2 gather blocks of 256 rows' worth
-    const int64_t gb = 2 * (static_cast<int64_t>(blockIdx.x) - red_blocks) + (tid >> 8);
-    tail_gather(t, gb, tid & 255);
+  if (static_cast<int>(blockIdx.x) >= red_blocks) {  // the next minibatch's record gather
+    tail_gather(t, (static_cast<int64_t>(blockIdx.x) - red_blocks) * NT + tid);
     return;
   }
-  tail_block(r, t, blockIdx.x, red_scratch(scratch));
+  tail_block<G>(r, t, blockIdx.x, red_scratch<G>(scratch));
 }
 
 // ============================================================================================
@@ -1086,14 +1096,28 @@ int adam_pack_launch(const AdamPackArgs &a, const TimRec &rec, hipStream_t st) {
   return 0;
 }
 
+// PPO_TAIL_GROUPS=8|16|32: float4 groups per step-tail block (A/B knob; bitwise the same sums)
+static const int g_tail_groups = [] {
+  const char *v = getenv("PPO_TAIL_GROUPS");
+  return v ? atoi(v) : 32;
+}();
+
 int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, hipStream_t st) {
   PPO_REQUIRE(t.a.H % 4 == 0 && t.a.din >= 1 && t.a.din <= kFusedKX &&
                   (!t.reduce || r.total == t.a.n),
               "step tail: H=%d din=%d", t.a.H, t.a.din);
-  const int red_blocks = static_cast<int>(ceil_div(t.a.n, kRedParams));
-  const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, 2 * 256));
-  launch_k(rec, step_tail_kernel, dim3(red_blocks + gather_blocks), dim3(kRedThreads), 0, st, r,
-           t, red_blocks);
+  auto go = [&](auto gc) {
+    constexpr int G = decltype(gc)::value, NT = G * kRedChunks;
+    const int red_blocks = static_cast<int>(ceil_div(t.a.n, 4 * G));
+    const int gather_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(t.b) * 8, NT));
+    TimRec named = rec;  // the launched instantiation's name (rocprof's, for the agreement check)
+    if (tim_active()) named.name = intern_name("step_tail_kernel<%d>", G);
+    launch_k(named, step_tail_kernel<G>, dim3(red_blocks + gather_blocks), dim3(NT), 0, st, r, t,
+             red_blocks);
+  };
+  if (g_tail_groups == 8) go(std::integral_constant<int, 8>{});
+  else if (g_tail_groups == 16) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 32>{});
   PPO_LAUNCHED();
   return 0;
 }

@@ -41,23 +41,31 @@ struct ReduceArgs {
 // step_tail_kernel share this exact order, so their results are bitwise equal.
 // Returns, on the chunk-0 threads (i < total), the final sums of parameters i..i+3 (also stored
 // to q.grad); other threads get zeros.
+// The group count G (float4 groups per block) sets only which parameters a block covers: the
+// per-parameter order (kRedChunks chunks in order) and the loss tree (kLossSlots virtual slots)
+// are the same for every G, so blocks of any G give bitwise the same sums.
 constexpr int kRedGroups = 32;
 constexpr int kRedChunks = 16;
 constexpr int kRedThreads = kRedGroups * kRedChunks;
 constexpr int kRedParams = 4 * kRedGroups;  // parameters per block
-// LDS scratch of one block reduction: part [kRedChunks][kRedGroups], lred [2][kRedThreads],
-// sseg [kMaxSegs] (the kernels declare it as one __shared__ array).
+constexpr int kLossSlots = 512;             // the loss tree's fixed shape
+// LDS scratch of one block reduction: part [kRedChunks][G], lred [2][kLossSlots], sseg
+// [kMaxSegs] (the kernels declare it as one __shared__ array).
 struct RedScratch {
   float4 *part;
   float *lred;
   ReduceSeg *sseg;
 };
-constexpr int kRedScratchBytes =
-    (kRedChunks * kRedGroups) * 16 + 2 * kRedThreads * 4 + kMaxSegs * static_cast<int>(sizeof(ReduceSeg));
+template <int G = kRedGroups>
+constexpr int red_scratch_bytes() {
+  return (kRedChunks * G) * 16 + 2 * kLossSlots * 4 + kMaxSegs * static_cast<int>(sizeof(ReduceSeg));
+}
+constexpr int kRedScratchBytes = red_scratch_bytes<kRedGroups>();
+template <int G = kRedGroups>
 __device__ __forceinline__ RedScratch red_scratch(char *lds) {
   return RedScratch{reinterpret_cast<float4 *>(lds),
-                    reinterpret_cast<float *>(lds + kRedChunks * kRedGroups * 16),
-                    reinterpret_cast<ReduceSeg *>(lds + kRedChunks * kRedGroups * 16 + 2 * kRedThreads * 4)};
+                    reinterpret_cast<float *>(lds + kRedChunks * G * 16),
+                    reinterpret_cast<ReduceSeg *>(lds + kRedChunks * G * 16 + 2 * kLossSlots * 4)};
 }
 
 // The segment holding parameter i: the last one with dst <= i (dst ascending).
@@ -140,23 +148,28 @@ __device__ __forceinline__ float4 chunk_combine(const float4 *part, int stride, 
   return out;
 }
 
-// The minibatch loss scalars from the per-split partials (fixed-shape tree over kRedThreads
-// threads; every thread of the block must call it).
+// The minibatch loss scalars from the per-split partials: slot v (of kLossSlots) sums partials
+// v, v + kLossSlots, ... in order, then a fixed-shape tree over the slots -- the same order for
+// any block size NT (every thread of the block must call it).
+template <int NT = kRedThreads>
 __device__ __forceinline__ void reduce_loss_block(const ReduceArgs &q, float *lred_flat) {
-  float (*lred)[kRedThreads] = reinterpret_cast<float (*)[kRedThreads]>(lred_flat);
+  static_assert(kLossSlots % NT == 0, "loss slots per thread");
+  float (*lred)[kLossSlots] = reinterpret_cast<float (*)[kLossSlots]>(lred_flat);
   const int tid = threadIdx.x;
-  float la = 0.f, lc = 0.f;
-  for (int k = tid; k < q.loss_splits; k += kRedThreads) {
-    la += q.loss_part[2 * k];
-    lc += q.loss_part[2 * k + 1];
+  for (int v = tid; v < kLossSlots; v += NT) {
+    float la = 0.f, lc = 0.f;
+    for (int k = v; k < q.loss_splits; k += kLossSlots) {
+      la += q.loss_part[2 * k];
+      lc += q.loss_part[2 * k + 1];
+    }
+    lred[0][v] = la;
+    lred[1][v] = lc;
   }
-  lred[0][tid] = la;
-  lred[1][tid] = lc;
   __syncthreads();
-  for (int w = kRedThreads / 2; w > 0; w >>= 1) {
-    if (tid < w) {
-      lred[0][tid] += lred[0][tid + w];
-      lred[1][tid] += lred[1][tid + w];
+  for (int w = kLossSlots / 2; w > 0; w >>= 1) {
+    for (int v = tid; v < w; v += NT) {
+      lred[0][v] += lred[0][v + w];
+      lred[1][v] += lred[1][v + w];
     }
     __syncthreads();
   }
@@ -171,22 +184,23 @@ __device__ __forceinline__ void reduce_loss_block(const ReduceArgs &q, float *lr
   }
 }
 
+template <int G = kRedGroups>
 __device__ __forceinline__ float4 reduce_slab_block_s(const ReduceArgs &q, int64_t block,
                                                       RedScratch sc) {
-  const int tid = threadIdx.x, grp = tid % kRedGroups, chunk = tid / kRedGroups;
-  const int64_t i = block * kRedParams + 4 * grp;
+  const int tid = threadIdx.x, grp = tid % G, chunk = tid / G;
+  const int64_t i = block * (4 * G) + 4 * grp;
   // The segment table, staged once per block: a per-lane lookup straight from the kernel
   // arguments compiled to a chain of dependent loads (one round trip per probe and per field).
   if (tid < q.nseg) sc.sseg[tid] = q.seg[tid];
   __syncthreads();
-  sc.part[chunk * kRedGroups + grp] = slab_item_sum(q, sc.sseg, i, chunk);
+  sc.part[chunk * G + grp] = slab_item_sum(q, sc.sseg, i, chunk);
   __syncthreads();
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
   if (chunk == 0 && i < q.total) {
-    out = chunk_combine(sc.part, kRedGroups, grp);
+    out = chunk_combine(sc.part, G, grp);
     *reinterpret_cast<float4 *>(q.grad + i) = out;
   }
-  if (block == 0 && q.loss_out) reduce_loss_block(q, sc.lred);
+  if (block == 0 && q.loss_out) reduce_loss_block<G * kRedChunks>(q, sc.lred);
   return out;
 }
 

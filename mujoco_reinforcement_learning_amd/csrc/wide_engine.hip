@@ -88,7 +88,8 @@ int wide_alloc(ppo_ctx *ctx) {
     return o;
   };
   struct Off {
-    int64_t h[PPO_MAX_LAYERS], w[PPO_MAX_LAYERS + 1], wt[PPO_MAX_LAYERS + 1], cs[PPO_MAX_LAYERS];
+    int64_t h[PPO_MAX_LAYERS], dh[PPO_MAX_LAYERS], w[PPO_MAX_LAYERS + 1], wt[PPO_MAX_LAYERS + 1],
+        cs[PPO_MAX_LAYERS];
     int64_t dz, z;
   } off[2];
   const int64_t ox = take(R * w->ldx * 2);
@@ -99,6 +100,7 @@ int wide_alloc(ppo_ctx *ctx) {
     for (int l = 0; l < nd.n_hidden; ++l) {
       wn.ldh[l] = static_cast<int>(rup(nd.layer[l].out, 64));
       off[z].h[l] = take(R * wn.ldh[l] * 2);
+      off[z].dh[l] = take(R * wn.ldh[l] * 2);
       off[z].cs[l] = take((R / 64) * nd.layer[l].out * 4);
     }
     off[z].dz = take(R * 64 * 2);
@@ -167,6 +169,7 @@ int wide_alloc(ppo_ctx *ctx) {
     WideNetWork &wn = w->net[z];
     for (int l = 0; l < nd.n_hidden; ++l) {
       wn.h[l] = reinterpret_cast<__bf16 *>(base + off[z].h[l]);
+      wn.dh[l] = reinterpret_cast<__bf16 *>(base + off[z].dh[l]);
       wn.colsum[l] = reinterpret_cast<float *>(base + off[z].cs[l]);
     }
     for (int l = 0; l <= nd.n_hidden; ++l) {
@@ -1406,7 +1409,9 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
     PPO_LAUNCHED();
   }
 
-  // ---- backward, deepest layer first: WGRAD of layer l (needs its input), then DGRAD into it --
+  // ---- backward, deepest layer first: layer l's WGRAD (dZ_l^T H_{l-1}) and DGRAD (dZ_{l-1} =
+  // act'(H_{l-1}) * dZ_l W_l, into dh[l-1]) both read dZ_l and not each other's output, so
+  // wide::run_pair issues them as one launch where the tiles allow (the hidden layers)
   int colsum_rows[2][PPO_MAX_LAYERS] = {};
   int splits_of[2][PPO_MAX_LAYERS + 1] = {};
   const int depth = std::max(NA.n_hidden, NC.n_hidden);
@@ -1422,7 +1427,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
       const LayerDesc &L = nd.layer[l];
       const WideNetWork &wn = W.net[z];
       WideProblem &Q = wg.p[np++];
-      Q.a = l == nd.n_hidden ? wn.dz : wn.h[l];
+      Q.a = l == nd.n_hidden ? wn.dz : wn.dh[l];
       Q.lda = l == nd.n_hidden ? 64 : wn.ldh[l];
       Q.b = l == 0 ? W.x : wn.h[l - 1];
       Q.ldb = l == 0 ? W.ldx : wn.ldh[l - 1];
@@ -1435,13 +1440,13 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
       max_m = std::max(max_m, L.out);
       max_n = std::max(max_n, L.in);
     }
-    if (np) {
+    const int np_w = np, max_m_w = max_m, max_n_w = max_n;
+    if (np_w) {
       wg.splits = s == 0 ? kWideHeadSplits : g_wide_splits;
       for (int z = 0; z < 2; ++z)
         if (ctx->net[z].n_hidden - s >= 0) splits_of[z][ctx->net[z].n_hidden - s] = wg.splits;
-      if (int rc = wide::run(wide::WK_WGRAD, wg, np, max_m, max_n, b, st)) return rc;
     }
-    // input gradient of layer l into h[l-1] (l >= 1)
+    // input gradient of layer l into dh[l-1] (l >= 1)
     WideBatch dg{};
     dg.rows_n = count_d;
     dg.act = ctx->cfg.activation;
@@ -1454,11 +1459,11 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
       const LayerDesc &L = nd.layer[l];
       const WideNetWork &wn = W.net[z];
       WideProblem &Q = dg.p[np++];
-      Q.a = l == nd.n_hidden ? wn.dz : wn.h[l];
+      Q.a = l == nd.n_hidden ? wn.dz : wn.dh[l];
       Q.lda = l == nd.n_hidden ? 64 : wn.ldh[l];
       Q.b = wn.wt[l];
       Q.ldb = wn.ldwt[l];
-      Q.c = wn.h[l - 1];
+      Q.c = wn.dh[l - 1];
       Q.aux = wn.h[l - 1];
       Q.ldc = wn.ldh[l - 1];
       Q.colsum = nd.layer[l - 1].b_off >= 0 ? wn.colsum[l - 1] : nullptr;
@@ -1474,7 +1479,14 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
         const int l = ctx->net[z].n_hidden - s;
         if (l >= 1) colsum_rows[z][l - 1] = ceil_div(rows_pad, tile);
       }
-      if (int rc = wide::run(wide::WK_DGRAD, dg, np, rows_pad, max_n, 0, st)) return rc;
+      if (np_w) {
+        if (int rc = wide::run_pair(wg, np_w, max_m_w, max_n_w, b, dg, np, rows_pad, max_n, st))
+          return rc;
+      } else if (int rc = wide::run(wide::WK_DGRAD, dg, np, rows_pad, max_n, 0, st)) {
+        return rc;
+      }
+    } else if (np_w) {
+      if (int rc = wide::run(wide::WK_WGRAD, wg, np_w, max_m_w, max_n_w, b, st)) return rc;
     }
   }
 

@@ -209,13 +209,14 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   }
 }
 
+// One workgroup's tile: bx / bz stand for blockIdx.x / .z of a launch of this kind alone, lds
+// is the block's C::LDS bytes.
 template <int TM, int TN, int WM, int WN, int KIND, int NS>
-__global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
+__device__ __forceinline__ void wide_gemm_body(const WideBatch &wb, int bx, int bz, char *lds) {
   using C = WideCfg<TM, TN, WM, WN, KIND, NS>;
   constexpr int NW = C::NW, NT = C::NT, BM = C::BM, BN = C::BN;
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
 
-  const WideProblem P = (blockIdx.z == 0) ? wb.p[0] : wb.p[1];
+  const WideProblem P = (bz == 0) ? wb.p[0] : wb.p[1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_m = (P.m + BM - 1) / BM, tiles_n = (P.n + BN - 1) / BN;
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
     // both operands, so all of them go to one XCD (blocks b, b + 8, ... share an XCD and its L2):
     // split s on XCD s % 8, its rows fetched from HBM once instead of once per XCD holding one of
     // its tiles.  Bijective when the split count is a multiple of 8; otherwise split-major.
-    const int b = static_cast<int>(blockIdx.x);
+    const int b = bx;
     if (b >= tiles * wb.splits) return;
     if (wb.splits % 8 == 0) {
       const int x = b % 8, j = b / 8;
@@ -237,8 +238,8 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
       id = b % tiles;
     }
   } else {
-    if (static_cast<int>(blockIdx.x) >= tiles) return;
-    xcd_map(blockIdx.x, tiles, id);
+    if (bx >= tiles) return;
+    xcd_map(bx, tiles, id);
   }
   const int tile_m = id / tiles_n, tile_n = id % tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -456,6 +457,27 @@ __global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
     if (KIND == WK_DGRAD && P.colsum && tid < BN && n0 + tid < P.n)
       P.colsum[static_cast<int64_t>(tile_m) * P.n_colsum + n0 + tid] = csum;
   }
+}
+
+template <int TM, int TN, int WM, int WN, int KIND, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void wide_gemm_kernel(WideBatch wb) {
+  __shared__ __attribute__((aligned(16))) char lds[WideCfg<TM, TN, WM, WN, KIND, NS>::LDS];
+  wide_gemm_body<TM, TN, WM, WN, KIND, NS>(wb, blockIdx.x, blockIdx.z, lds);
+}
+
+// A layer's WGRAD and DGRAD in one launch (the backward's per-layer pair: both read the layer's dZ,
+// neither writes what the other reads -- DGRAD writes the next layer's dZ to its own buffer):
+// blocks [0, wg_blocks) run the WGRAD grid, the rest the DGRAD grid, each with the block index it
+// has in a launch of its own (wg_blocks a multiple of 8 keeps both XCD maps).
+template <int TM, int TN, int WM, int WN, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void wide_pair_kernel(WideBatch wg, WideBatch dg,
+                                                                 int wg_blocks) {
+  constexpr int LW = WideCfg<TM, TN, WM, WN, WK_WGRAD, NS>::LDS;
+  constexpr int LD = WideCfg<TM, TN, WM, WN, WK_DGRAD, NS>::LDS;
+  __shared__ __attribute__((aligned(16))) char lds[LW > LD ? LW : LD];
+  const int b = static_cast<int>(blockIdx.x);
+  if (b < wg_blocks) wide_gemm_body<TM, TN, WM, WN, WK_WGRAD, NS>(wg, b, blockIdx.z, lds);
+  else wide_gemm_body<TM, TN, WM, WN, WK_DGRAD, NS>(dg, b - wg_blocks, blockIdx.z, lds);
 }
 
 }  // namespace wide

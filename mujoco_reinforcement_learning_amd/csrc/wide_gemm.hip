@@ -97,6 +97,40 @@ int run(int kind, const WideBatch &wb, int nprob, int max_m, int max_n, int kflo
   }
 }
 
+int run_pair(const WideBatch &wg, int np_w, int max_m_w, int max_n_w, int kflops,
+             const WideBatch &dg, int np_d, int rows_d, int max_n_d, hipStream_t st) {
+  // the default tiles of both kinds (run_kind): WGRAD with max_m > 32, DGRAD at minibatch rows
+  const bool forced = getenv("PPO_WIDE_CFG") != nullptr || getenv("PPO_WIDE_PAIR0") != nullptr;
+  if (forced || np_w != np_d || max_m_w <= 32 || rows_d <= 4096) {
+    if (int rc = run(WK_WGRAD, wg, np_w, max_m_w, max_n_w, kflops, st)) return rc;
+    return run(WK_DGRAD, dg, np_d, rows_d, max_n_d, 0, st);
+  }
+  using CW = WideCfg<2, 1, 2, 4, WK_WGRAD, 2>;
+  using CD = WideCfg<2, 1, 2, 4, WK_DGRAD, 2>;
+  static_assert(CW::NT == CD::NT, "one block size");
+  const int wg_blocks = ceil_div(max_m_w, CW::BM) * ceil_div(max_n_w, CW::BN) * wg.splits;
+  const int dg_blocks = ceil_div(rows_d, CD::BM) * ceil_div(max_n_d, CD::BN);
+  PPO_REQUIRE(wg_blocks % 8 == 0 || wg.splits % 8 != 0, "wide pair: WGRAD grid %d", wg_blocks);
+  TimRec rec{KC_GEMM_WGRAD, "wide_pair_kernel<2, 1, 2, 4, 2>", 0.0, 0.0};
+  if (tim_active()) {  // both kinds' algorithmic work, as their own launches would count it
+    for (int i = 0; i < np_w; ++i) {
+      const WideProblem &p = wg.p[i];
+      rec.flops += 2.0 * p.m * p.n * kflops;
+      rec.bytes += 2.0 * (static_cast<double>(p.m) + p.n) * kflops +
+                   4.0 * static_cast<double>(p.m) * p.n * wg.splits;
+    }
+    for (int i = 0; i < np_d; ++i) {
+      const WideProblem &p = dg.p[i];
+      rec.flops += 2.0 * p.m * p.n * p.k;
+      rec.bytes += 2.0 * (static_cast<double>(p.m) + p.n) * p.k + 4.0 * static_cast<double>(p.m) * p.n;
+    }
+  }
+  launch_k(rec, wide_pair_kernel<2, 1, 2, 4, 2>, dim3(wg_blocks + dg_blocks, 1, np_w), dim3(CW::NT),
+           0, st, wg, dg, wg_blocks);
+  PPO_LAUNCHED();
+  return 0;
+}
+
 int row_tile(int kind, int max_m, int max_n) {
   if (kind == WK_F32 || (kind == WK_FWD && max_n <= 32)) return 128;
   if (max_m <= 4096) return 64;

@@ -15,7 +15,8 @@
 namespace ppo {
 
 struct WideNetWork {
-  __bf16 *h[PPO_MAX_LAYERS];       // [rpad][ldh] hidden outputs; backward overwrites them with dZ
+  __bf16 *h[PPO_MAX_LAYERS];       // [rpad][ldh] hidden outputs (kept through the backward)
+  __bf16 *dh[PPO_MAX_LAYERS];      // [rpad][ldh] dZ of hidden layer l (DGRAD of layer l + 1)
   int ldh[PPO_MAX_LAYERS];         // round_up(width, 64), pad columns stay zero
   __bf16 *w[PPO_MAX_LAYERS + 1];   // W image [round_up(out, 128)][round_up(in, 64)] (head: l = L)
   __bf16 *wt[PPO_MAX_LAYERS + 1];  // W^T image [round_up(in, 128)][round_up(out, 64)]

@@ -161,7 +161,7 @@ def test_local_dp_two_ranks_fused_replicas_agree(gpu, shape):
     # into the flat gradient, the all-reduce,
     # then ONE tail launch: Adam + weight images + the next minibatch's gather
     assert any(k.startswith("fused_update_kernel") for k in kernels), kernels
-    assert "step_tail_kernel" in kernels, kernels
+    assert any(k.startswith("step_tail_kernel") for k in kernels), kernels
     assert "reduce_slabs_kernel" in kernels, kernels
 
 
