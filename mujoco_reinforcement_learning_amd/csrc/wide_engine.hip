@@ -36,12 +36,14 @@ using wide::WideProblem;
 
 static inline int64_t rup(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 constexpr int kWideSplits = 16;      // WGRAD split-K slabs of the hidden layers (at most)
-// Split-K slabs of the hidden-layer WGRAD: PPO_WIDE_SPLITS (1 .. 16, default 16).  Every slab is
+// Split-K slabs of the hidden-layer WGRAD: PPO_WIDE_SPLITS (1 .. 16, default 8).  Every slab is
 // a full f32 copy of the layer's gradient written by WGRAD and read by wide_reduce_kernel, so at
-// small minibatches (8,192 rows per rank) fewer, longer splits move fewer bytes.
+// small minibatches (8,192 rows per rank) fewer, longer splits move fewer bytes; since the WGRAD
+// shares its launch with the layer's DGRAD (wide_pair_kernel) its own block count matters less,
+// and with 8-split slabs on the fold's fast path the Humanoid shard went 37.0 -> 36.1 ms.
 static const int g_wide_splits = [] {
   const char *v = getenv("PPO_WIDE_SPLITS");
-  const int n = v ? atoi(v) : kWideSplits;
+  const int n = v ? atoi(v) : kWideSplits / 2;
   return n < 1 ? 1 : (n > kWideSplits ? kWideSplits : n);
 }();
 constexpr int kWideHeadSplits = 64;  // ... of the heads (few output tiles)
@@ -196,6 +198,83 @@ void wide_free(ppo_ctx *ctx) {
 }
 
 // ============================================================================================
+// Row staging: x[j][0:ldx] = bf16(states[rows ? rows[j] : j][0:din]) for j < count, zero rows
+// for count <= j < rows_pad (the padding contract of wide_gemm.h).
+// ============================================================================================
+struct GatherArgs {
+  const float *states;
+  const int32_t *rows, *rows_n;
+  int n, rows_pad, din, ldx;
+  __bf16 *x;
+};
+
+__device__ __forceinline__ void gather_block(const GatherArgs &g, int blk) {
+  const float *__restrict__ states = g.states;
+  const int32_t *__restrict__ rows = g.rows;
+  const int din = g.din, ldx = g.ldx, rows_pad = g.rows_pad;
+  __bf16 *__restrict__ x = g.x;
+  const int count = g.rows_n ? *g.rows_n : g.n;
+  const int per_row = ldx / 8;
+  const int64_t i = static_cast<int64_t>(blk) * 256 + threadIdx.x;
+  if (i >= static_cast<int64_t>(rows_pad) * per_row) return;
+  const int j = static_cast<int>(i / per_row), c0 = static_cast<int>(i % per_row) * 8;
+  const bool live = j < count;
+  const int64_t sr = rows ? rows[live ? j : 0] : j;
+  const float *src = states + (live ? sr : 0) * din;
+  float v[8];
+  if ((din & 3) == 0 && (reinterpret_cast<uintptr_t>(states) & 15) == 0) {
+    // two 16-B loads from clamped addresses (din % 4 == 0: a 4-group is wholly in or out)
+    const bool in0 = live && c0 < din, in1 = live && c0 + 4 < din;
+    const float4 x0 = *reinterpret_cast<const float4 *>(src + (in0 ? c0 : 0));
+    const float4 x1 = *reinterpret_cast<const float4 *>(src + (in1 ? c0 + 4 : 0));
+    v[0] = in0 ? x0.x : 0.f, v[1] = in0 ? x0.y : 0.f, v[2] = in0 ? x0.z : 0.f, v[3] = in0 ? x0.w : 0.f;
+    v[4] = in1 ? x1.x : 0.f, v[5] = in1 ? x1.y : 0.f, v[6] = in1 ? x1.z : 0.f, v[7] = in1 ? x1.w : 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool in = live && c0 + e < din;
+      const float u = src[in ? c0 + e : 0];
+      v[e] = in ? u : 0.f;
+    }
+  }
+  *reinterpret_cast<uint4 *>(x + static_cast<int64_t>(j) * ldx + c0) =
+      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
+                 wide::pack2(v[6], v[7]));
+}
+
+__global__ __launch_bounds__(256) void wide_gather_kernel(GatherArgs g) { gather_block(g, blockIdx.x); }
+
+static GatherArgs gather_args(ppo_ctx *ctx, const float *states, const int32_t *rows,
+                              const int32_t *count_d, int n, int rows_pad) {
+  WideWork &W = *ctx->wide;
+  GatherArgs g{};
+  g.states = states;
+  g.rows = rows;
+  g.rows_n = count_d;
+  g.n = n;
+  g.rows_pad = rows_pad;
+  g.din = ctx->cfg.obs_dim * ctx->cfg.window;
+  g.ldx = W.ldx;
+  g.x = W.x;
+  return g;
+}
+static int gather_blocks(const GatherArgs &g) {
+  return static_cast<int>(ceil_div(static_cast<int64_t>(g.rows_pad) * (g.ldx / 8), 256));
+}
+static double gather_bytes(const GatherArgs &g) {
+  return static_cast<double>(g.n) * g.din * 4.0 + static_cast<double>(g.rows_pad) * g.ldx * 2.0;
+}
+
+static int stage_rows(ppo_ctx *ctx, const float *states, const int32_t *rows,
+                      const int32_t *count_d, int n, int rows_pad, hipStream_t st) {
+  const GatherArgs g = gather_args(ctx, states, rows, count_d, n, rows_pad);
+  launch_k(TimRec{KC_GATHER, "wide_gather_kernel", 0.0, gather_bytes(g)}, wide_gather_kernel,
+           dim3(gather_blocks(g)), dim3(256), 0, st, g);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// ============================================================================================
 // Weight images: dst[r][c] = bf16(W[r][c]) (or W^T), zero outside the tensor.  One 64 x 64 tile
 // of one image per block: the f32 master tile is read row-coalesced (64 consecutive `in` columns
 // per wave row) into LDS, then every thread writes 8 consecutive image columns as one 16-B store,
@@ -314,9 +393,17 @@ __device__ __forceinline__ void pack_frag(const FragArgs &q, int b) {
 // One launch for every image an optimizer step refreshes: blocks [0, frag_blocks) the
 // fragment-major images (fused forward / rollout), the rest the 64x64 tiles of the W^T (and, for
 // the layered forward, W) images.
-__global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q, FragArgs fq, int frag_blocks) {
+// A minibatch step's prep (wide_minibatch_grad) adds the row gather as the last blocks, so the
+// weight refresh and the row staging -- independent work -- are one launch.
+struct PrepGather {
+  GatherArgs g;
+  int first;  // first gather block (blocks before it pack), gridDim.x when there is none
+};
+__global__ __launch_bounds__(256) void wide_pack_kernel(PackArgs q, FragArgs fq, int frag_blocks,
+                                                        PrepGather pg) {
   const int b = static_cast<int>(blockIdx.x);
-  if (b < frag_blocks) pack_frag(fq, b);
+  if (b >= pg.first) gather_block(pg.g, b - pg.first);
+  else if (b < frag_blocks) pack_frag(fq, b);
   else pack_tile(q, b - frag_blocks);
 }
 
@@ -343,7 +430,8 @@ static int frag_args(ppo_ctx *ctx, FragArgs &q, double &elems) {
   return blocks;
 }
 
-int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
+// gather (nullable): the minibatch rows to stage in the same launch
+int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag, const GatherArgs *gather) {
   WideWork &W = *ctx->wide;
   FragArgs fq{};
   double elems = 0;
@@ -374,62 +462,21 @@ int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag) {
       }
     }
   }
-  launch_k(TimRec{KC_GATHER, "wide_pack_kernel", 0.0, elems * (4.0 + 2.0)}, wide_pack_kernel,
-           dim3(frag_blocks + blocks), dim3(256), 0, st, q, fq, frag_blocks);
-  PPO_LAUNCHED();
-  return 0;
-}
-
-// ============================================================================================
-// Row staging: x[j][0:ldx] = bf16(states[rows ? rows[j] : j][0:din]) for j < count, zero rows
-// for count <= j < rows_pad (the padding contract of wide_gemm.h).
-// ============================================================================================
-__global__ __launch_bounds__(256) void wide_gather_kernel(const float *__restrict__ states,
-                                                          const int32_t *__restrict__ rows,
-                                                          const int32_t *__restrict__ rows_n,
-                                                          int n, int rows_pad, int din, int ldx,
-                                                          __bf16 *__restrict__ x) {
-  const int count = rows_n ? *rows_n : n;
-  const int per_row = ldx / 8;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= static_cast<int64_t>(rows_pad) * per_row) return;
-  const int j = static_cast<int>(i / per_row), c0 = static_cast<int>(i % per_row) * 8;
-  const bool live = j < count;
-  const int64_t sr = rows ? rows[live ? j : 0] : j;
-  const float *src = states + (live ? sr : 0) * din;
-  float v[8];
-  if ((din & 3) == 0 && (reinterpret_cast<uintptr_t>(states) & 15) == 0) {
-    // two 16-B loads from clamped addresses (din % 4 == 0: a 4-group is wholly in or out)
-    const bool in0 = live && c0 < din, in1 = live && c0 + 4 < din;
-    const float4 x0 = *reinterpret_cast<const float4 *>(src + (in0 ? c0 : 0));
-    const float4 x1 = *reinterpret_cast<const float4 *>(src + (in1 ? c0 + 4 : 0));
-    v[0] = in0 ? x0.x : 0.f, v[1] = in0 ? x0.y : 0.f, v[2] = in0 ? x0.z : 0.f, v[3] = in0 ? x0.w : 0.f;
-    v[4] = in1 ? x1.x : 0.f, v[5] = in1 ? x1.y : 0.f, v[6] = in1 ? x1.z : 0.f, v[7] = in1 ? x1.w : 0.f;
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const bool in = live && c0 + e < din;
-      const float u = src[in ? c0 + e : 0];
-      v[e] = in ? u : 0.f;
-    }
+  PrepGather pg{};
+  pg.first = frag_blocks + blocks;
+  int gblocks = 0;
+  if (gather) {
+    pg.g = *gather;
+    gblocks = gather_blocks(*gather);
   }
-  *reinterpret_cast<uint4 *>(x + static_cast<int64_t>(j) * ldx + c0) =
-      make_uint4(wide::pack2(v[0], v[1]), wide::pack2(v[2], v[3]), wide::pack2(v[4], v[5]),
-                 wide::pack2(v[6], v[7]));
-}
-
-static int stage_rows(ppo_ctx *ctx, const float *states, const int32_t *rows,
-                      const int32_t *count_d, int n, int rows_pad, hipStream_t st) {
-  WideWork &W = *ctx->wide;
-  const int din = ctx->cfg.obs_dim * ctx->cfg.window;
-  const int64_t items = static_cast<int64_t>(rows_pad) * (W.ldx / 8);
-  launch_k(TimRec{KC_GATHER, "wide_gather_kernel", 0.0,
-                  static_cast<double>(n) * din * 4.0 + static_cast<double>(rows_pad) * W.ldx * 2.0},
-           wide_gather_kernel, dim3(ceil_div(items, 256)), dim3(256), 0, st, states, rows,
-           count_d, n, rows_pad, din, W.ldx, W.x);
+  launch_k(TimRec{KC_GATHER, "wide_pack_kernel", 0.0,
+                  elems * (4.0 + 2.0) + (gather ? gather_bytes(*gather) : 0.0)},
+           wide_pack_kernel, dim3(frag_blocks + blocks + gblocks), dim3(256), 0, st, q, fq,
+           frag_blocks, pg);
   PPO_LAUNCHED();
   return 0;
 }
+
 
 // ============================================================================================
 // Forward through the hidden layers and the head pre-activations (both nets per launch)
@@ -1254,8 +1301,33 @@ struct WideRedPlan {
   int bprefix[kMaxSegs + 1];      // cumulative block counts of the runs
 };
 
-__device__ __forceinline__ bool fast_seg(const ReduceSeg &g) {
-  return g.nsplit == kRedChunks && g.stride % 4 == 0 && reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
+// fast segments: 16 or 8 splits (at most one split per reduce_slab_block chunk), aligned
+__host__ __device__ __forceinline__ bool fast_seg(const ReduceSeg &g) {
+  return (g.nsplit == kRedChunks || g.nsplit == kRedChunks / 2) && g.stride % 4 == 0 &&
+         reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
+}
+
+// The fast path's sum of S <= kRedChunks splits in reduce_slab_block's order: chunk c holds split
+// S c / 16 when S (c + 1) / 16 exceeds it (one split, summed as (0 + v) + 0), else nothing (0);
+// the chunks are added in order, every addition kept (adding +0 can change a -0).
+template <int S>
+__device__ __forceinline__ float4 fast_split_sum(const ReduceSeg &g, int64_t off) {
+  float4 v[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) v[k] = *reinterpret_cast<const float4 *>(g.src + off + k * g.stride);
+  auto chunk = [&](int c) {
+    const int k0 = (S * c) / kRedChunks, k1 = (S * (c + 1)) / kRedChunks;
+    if (k1 == k0) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 a = v[k0];
+    return make_float4((0.f + a.x) + 0.f, (0.f + a.y) + 0.f, (0.f + a.z) + 0.f, (0.f + a.w) + 0.f);
+  };
+  float4 out = chunk(0);
+#pragma unroll
+  for (int c = 1; c < kRedChunks; ++c) {
+    const float4 b = chunk(c);
+    out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
+  }
+  return out;
 }
 
 // splits [k0, k1) of parameters i..i+3 (i - g.dst = off >= 0): slab_item_sum's arithmetic (two
@@ -1309,20 +1381,8 @@ __global__ __launch_bounds__(kRedThreads) void wide_reduce_kernel(ReduceArgs q, 
       if (off < 0 || off >= g.len) {  // between tensors: padding
         *reinterpret_cast<float4 *>(q.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       } else if (fast_seg(g) && off + 3 < g.len) {
-        float4 v[kRedChunks];
-#pragma unroll
-        for (int c = 0; c < kRedChunks; ++c)
-          v[c] = *reinterpret_cast<const float4 *>(g.src + off + c * g.stride);
-        // a one-split chunk's sum is (0 + v) + 0 (the two partial sums), then chunk order
-        auto one = [](float4 a) {
-          return make_float4((0.f + a.x) + 0.f, (0.f + a.y) + 0.f, (0.f + a.z) + 0.f, (0.f + a.w) + 0.f);
-        };
-        float4 out = one(v[0]);
-#pragma unroll
-        for (int c = 1; c < kRedChunks; ++c) {
-          const float4 b = one(v[c]);
-          out = make_float4(out.x + b.x, out.y + b.y, out.z + b.z, out.w + b.w);
-        }
+        const float4 out = g.nsplit == kRedChunks ? fast_split_sum<kRedChunks>(g, off)
+                                                  : fast_split_sum<kRedChunks / 2>(g, off);
         *reinterpret_cast<float4 *>(q.grad + i) = out;
       }
     }
@@ -1366,8 +1426,10 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   const int64_t P = ctx->total_params;
   const int A = ctx->cfg.act_dim;
   NetDesc &NA = ctx->net[0], &NC = ctx->net[1];
-  if (int rc = wide_pack(ctx, st, W.fused_rollout)) return rc;
-  if (int rc = stage_rows(ctx, states_d, rows_d, count_d, b, rows_pad, st)) return rc;
+  {  // weight images + the minibatch's rows, one launch
+    const GatherArgs g = gather_args(ctx, states_d, rows_d, count_d, b, rows_pad);
+    if (int rc = wide_pack(ctx, st, W.fused_rollout, &g)) return rc;
+  }
   const bool both[2] = {true, true};
   if (W.fused_rollout) {  // one launch: hidden layers + heads, activations LDS-resident
     if (int rc = wide_forward_fused(ctx, rows_pad, b, count_d, st)) return rc;
@@ -1556,8 +1618,7 @@ int wide_minibatch_grad(ppo_ctx *ctx, const float *states_d, const float *action
   };
   for (int i = 0; i < ns; ++i) {
     const ReduceSeg &g = r.seg[i];
-    const bool fast = g.nsplit == kRedChunks && g.stride % 4 == 0 &&
-                      reinterpret_cast<uintptr_t>(g.src) % 16 == 0;
+    const bool fast = fast_seg(g);
     if (!fast) {
       if (int rc = add_run(i, g.dst, ceil_div(g.len, 4))) return rc;
     } else if (g.len % 4) {  // the partial last group

@@ -55,7 +55,8 @@ int wide_alloc(ppo_ctx *ctx);
 void wide_free(ppo_ctx *ctx);
 // refresh the bf16 weight images from the f32 master parameters
 // frag: also the fragment-major images of the fused rollout (before a rollout / policy step)
-int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag = true);
+struct GatherArgs;  // wide_engine.hip: a minibatch's row staging, run in the same launch
+int wide_pack(ppo_ctx *ctx, hipStream_t st, bool frag = true, const GatherArgs *gather = nullptr);
 int wide_policy_step(ppo_ctx *ctx, const float *state_d, int n, const float *eps_d, uint64_t seed,
                      uint64_t offset, float *action_d, float *logp_d, float *value_d,
                      float *mean_d, bool pack, hipStream_t st,
