@@ -46,7 +46,7 @@ namespace ppo {
 namespace lstm {
 
 constexpr int kMaxA = 32;
-constexpr int kSplits = 32;           // split-K slabs of the weight gradients
+constexpr int kSplits = 32;           // split-K slabs of the weight gradients (at most)
 constexpr int64_t kAlign = 16;        // floats: every flat tensor starts 64-B aligned
 constexpr int64_t kWsAlign = 64;
 
@@ -363,29 +363,44 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(CellBwdArgs q) {
 }
 
 // The slab fold when every tensor is float4-aligned (the usual case): one thread per float4
-// group, its 32 split loads issued 16 at a time, summed in reduce_slab_block's order (chunk c =
-// splits 2c, 2c + 1 as (0 + v_2c) + (0 + v_2c+1), chunks in order) -- bitwise that kernel's
-// result, with 16 loads in flight per thread instead of 2.
-static_assert(kSplits == 2 * kRedChunks, "lstm_reduce_fast_kernel: two splits per chunk");
+// group, its S split loads issued up to 16 at a time, summed in reduce_slab_block's order -- chunk
+// c holds splits [S c / 16, S (c + 1) / 16): two as (0 + v_a) + (0 + v_b), one as (0 + v) + 0,
+// none as 0 + 0, the chunks added in order -- bitwise that kernel's result, with up to 16 loads in
+// flight per thread instead of 2.
+template <int S>
 __global__ __launch_bounds__(256) void lstm_reduce_fast_kernel(float *__restrict__ grad,
                                                                const float *__restrict__ slabs,
                                                                int64_t total) {
+  static_assert(S == 8 || S == 16 || S == 32, "split count");
+  constexpr int PER = S / kRedChunks > 0 ? S / kRedChunks : 1;  // splits in a non-empty chunk
+  constexpr int HALVES = S > 16 ? 2 : 1, CH = kRedChunks / HALVES;  // chunks per load batch
   const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
   if (i >= total) return;
   const float *src = slabs + i;
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    float4 v[16];
+  for (int half = 0; half < HALVES; ++half) {
+    constexpr int NV = S / HALVES;
+    float4 v[NV];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      v[j] = *reinterpret_cast<const float4 *>(src + (16 * half + j) * total);
+    for (int j = 0; j < NV; ++j)
+      v[j] = *reinterpret_cast<const float4 *>(src + (NV * half + j) * total);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float4 a = v[2 * c], b = v[2 * c + 1];
-      const float4 p = make_float4((0.f + a.x) + (0.f + b.x), (0.f + a.y) + (0.f + b.y),
-                                   (0.f + a.z) + (0.f + b.z), (0.f + a.w) + (0.f + b.w));
-      out = (half == 0 && c == 0) ? p : make_float4(out.x + p.x, out.y + p.y, out.z + p.z, out.w + p.w);
+    for (int cc = 0; cc < CH; ++cc) {
+      const int c = CH * half + cc;
+      const int k0 = (S * c) / kRedChunks - NV * half, k1 = (S * (c + 1)) / kRedChunks - NV * half;
+      float4 p;
+      if (PER == 2) {
+        const float4 a = v[k0], b = v[k0 + 1];
+        p = make_float4((0.f + a.x) + (0.f + b.x), (0.f + a.y) + (0.f + b.y),
+                        (0.f + a.z) + (0.f + b.z), (0.f + a.w) + (0.f + b.w));
+      } else if (k1 > k0) {
+        const float4 a = v[k0];
+        p = make_float4((0.f + a.x) + 0.f, (0.f + a.y) + 0.f, (0.f + a.z) + 0.f, (0.f + a.w) + 0.f);
+      } else {
+        p = make_float4(0.f + 0.f, 0.f + 0.f, 0.f + 0.f, 0.f + 0.f);
+      }
+      out = (c == 0) ? p : make_float4(out.x + p.x, out.y + p.y, out.z + p.z, out.w + p.w);
     }
   }
   *reinterpret_cast<float4 *>(grad + i) = out;
@@ -566,7 +581,8 @@ struct ppo_lstm_ctx {
   float *feat_a, *feat_c;            // [rows][W*2H], [rows][2H]
   float *act_mu[PPO_MAX_LAYERS + 1], *act_ls[PPO_MAX_LAYERS + 1], *act_v[PPO_MAX_LAYERS + 1];
   float *dz[3][2];                   // ping-pong gradient buffers [rows][maxw]: mu, ls, critic
-  float *slabs;                      // [kSplits][total]
+  float *slabs;                      // [kSplits][total] (the first `splits` used)
+  int splits;                        // weight-gradient split-K slabs (PPO_LSTM_SPLITS)
   float *row_part;                   // [rows][3]
   int maxw;
   int fused_step;  // bf16 forward steps as lstm_step_fwd_kernel (ppo_lstm_fused_step)
@@ -580,6 +596,18 @@ namespace {
 const int g_lstm_fused_step = [] {
   const char *v = getenv("PPO_LSTM_FUSED_STEP");
   return v ? atoi(v) : 1;
+}();
+
+// weight-gradient split-K slabs: PPO_LSTM_SPLITS = 8 | 16 | 32 (default 32).  Each split writes
+// an f32 copy of every weight gradient that the fold reads back; fewer splits starve the
+// weight-gradient GEMMs of workgroups instead (round 5, main.py line: 500 / 503 / 545 ms at 32 /
+// 16 / 8).  Measured and dropped the same round: the backward step as one launch (recurrent
+// gradient GEMM + cell, the forward step's decomposition) -- 136 us per step against 44 + 67 for
+// the pair, its MFMA-layout epilogue touching the gates and states 4 B per lane.
+const int g_lstm_splits = [] {
+  const char *v = getenv("PPO_LSTM_SPLITS");
+  const int n = v ? atoi(v) : 32;
+  return (n == 8 || n == 16) ? n : 32;
 }();
 
 struct TimingScope {
@@ -658,7 +686,7 @@ int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int ma
   GemmBatch gb{};
   for (int i = 0; i < np; ++i) gb.p[i] = p[i];
   gb.k = rows;
-  gb.splits = kSplits;
+  gb.splits = x->splits;
   gb.slab_stride = x->total;
   gb.prec = x->prec;
   return gemm_wgrad_partial(gb, np, max_m, max_n, st);
@@ -993,6 +1021,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   x->prec = PPO_PREC_F32;
   x->ent_log_share = 1.f;
   x->fused_step = g_lstm_fused_step;
+  x->splits = g_lstm_splits;
   const int H = c.latent, W = c.window, O = c.obs_dim, A = c.act_dim;
   int64_t off = 0;
   // LSTMActor.parameters(): feature_extractor, actor, actor_logstd (lstm_actor.py:12-38)
@@ -1285,7 +1314,7 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
     g.len = (i + 1 < x->offsets.size() ? x->offsets[i + 1] : x->total) - x->offsets[i];
     g.src = x->slabs + x->offsets[i];
     g.stride = x->total;
-    g.nsplit = kSplits;
+    g.nsplit = x->splits;
   }
   r.nseg = ns;
   r.total = x->total;
@@ -1293,11 +1322,16 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   bool aligned = x->total % 4 == 0 && reinterpret_cast<uintptr_t>(x->slabs) % 16 == 0 &&
                  reinterpret_cast<uintptr_t>(grad_d) % 16 == 0;
   for (size_t i = 0; i < x->offsets.size(); ++i) aligned = aligned && x->offsets[i] % 4 == 0;
-  if (aligned)
-    launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 4.0 * (kSplits + 1.0) * x->total},
-             lstm_reduce_fast_kernel, dim3(ceil_div(x->total, 4 * 256)), dim3(256), 0, st, grad_d,
-             x->slabs, x->total);
-  else
+  if (aligned) {
+    const TimRec rec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 4.0 * (x->splits + 1.0) * x->total};
+    const dim3 grid(ceil_div(x->total, 4 * 256));
+    if (x->splits == 8)
+      launch_k(rec, lstm_reduce_fast_kernel<8>, grid, dim3(256), 0, st, grad_d, x->slabs, x->total);
+    else if (x->splits == 16)
+      launch_k(rec, lstm_reduce_fast_kernel<16>, grid, dim3(256), 0, st, grad_d, x->slabs, x->total);
+    else
+      launch_k(rec, lstm_reduce_fast_kernel<32>, grid, dim3(256), 0, st, grad_d, x->slabs, x->total);
+  } else
     launch_k(TimRec{KC_REDUCE, "reduce_slabs_kernel", 0.0, 0.0}, lstm_reduce_kernel,
              dim3(ceil_div(x->total, kRedParams)), dim3(kRedThreads), 0, st, r);
   PPO_LAUNCHED();
