@@ -479,13 +479,28 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(GemmBatch gb) {
     if (EPI == EPI_PARTIAL) K = *gb.rows_n;
     else M = *gb.rows_n;
   }
-  int tile_m, tile_n;
-  if (!xcd_tile(static_cast<int>(blockIdx.x), (M + BM - 1) / BM, (N + BN - 1) / BN, tile_m, tile_n))
-    return;  // uniform per block
+  int tile_m, tile_n, split = 0;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  if (EPI == EPI_PARTIAL && gb.splits % kXcds == 0) {
+    // split-K weight gradients: every tile of a split on one XCD (workgroups are dealt to the
+    // XCDs by linear id mod 8), so the split's k-rows of both operands are fetched into one L2
+    // and reused by all its tiles instead of once per XCD holding one of them
+    const int X = static_cast<int>(gridDim.x);
+    const int lin = static_cast<int>(blockIdx.x) + X * static_cast<int>(blockIdx.y);
+    const int j = lin / kXcds;
+    split = lin % kXcds + kXcds * (j / X);
+    const int id = j % X;
+    if (id >= tiles_m * tiles_n) return;  // uniform per block
+    tile_m = id / tiles_n;
+    tile_n = id - tile_m * tiles_n;
+  } else {
+    if (!xcd_tile(static_cast<int>(blockIdx.x), tiles_m, tiles_n, tile_m, tile_n))
+      return;  // uniform per block
+    if (EPI == EPI_PARTIAL) split = static_cast<int>(blockIdx.y);
+  }
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   if (m0 >= M || n0 >= N) return;  // uniform per block
   int kbeg = 0, kend = K;
-  const int split = (EPI == EPI_PARTIAL) ? static_cast<int>(blockIdx.y) : 0;
   if (EPI == EPI_PARTIAL) {
     kbeg = static_cast<int>((static_cast<int64_t>(split) * K) / gb.splits);
     kend = static_cast<int>((static_cast<int64_t>(split + 1) * K) / gb.splits);
