@@ -152,11 +152,13 @@ constexpr int kStepRows = 64, kStepUnits = 64, kStepBK = 32;
 struct StepArgs {
   CellArgs cell;
   const float *whh[2];  // W_hh per direction, [4H][H] f32 (torch layout)
+  const __bf16 *whh16[2];  // W16 instantiation: the same rows as bf16 (the ctx's weight copy)
 };
 
 typedef __bf16 lstm_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
 
+template <bool W16>
 __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
   constexpr int AP = kStepBK + 8;                 // bf16 image row pitch (16 B of padding)
   constexpr int AIMG = kStepRows * AP, BIMG = 4 * kStepUnits * AP;
@@ -175,6 +177,8 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
   // staging: A 64 rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63) x
   // 32 k (8 float4 per thread); rows past b load row b-1 (clamped, results discarded)
   float4 va[2], vb[8];
+  uint2 vb16[8];
+  const __bf16 *wb16 = W16 ? q.whh16[d] : nullptr;
   auto gload = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -186,7 +190,9 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
       const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
-      vb[u] = *reinterpret_cast<const float4 *>(wb + static_cast<int64_t>(gate * H + j0 + jj) * H + k0 + kk);
+      const int64_t off = static_cast<int64_t>(gate * H + j0 + jj) * H + k0 + kk;
+      if constexpr (W16) vb16[u] = *reinterpret_cast<const uint2 *>(wb16 + off);
+      else vb[u] = *reinterpret_cast<const float4 *>(wb + off);
     }
   };
   auto lstore = [&](int buf) {
@@ -201,7 +207,7 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
       *reinterpret_cast<uint2 *>(bi + nn * AP + kk) =
-          make_uint2(pack_bf16x2(vb[u].x, vb[u].y), pack_bf16x2(vb[u].z, vb[u].w));
+          W16 ? vb16[u] : make_uint2(pack_bf16x2(vb[u].x, vb[u].y), pack_bf16x2(vb[u].z, vb[u].w));
     }
   };
 
@@ -406,6 +412,18 @@ __global__ __launch_bounds__(256) void lstm_reduce_fast_kernel(float *__restrict
   *reinterpret_cast<float4 *>(grad + i) = out;
 }
 
+// bf16 copy of the parameters, 4 per thread (the RNE rounding the GEMMs' staging applies)
+__global__ __launch_bounds__(256) void lstm_params_bf16_kernel(const float *__restrict__ p,
+                                                               __bf16 *__restrict__ o, int64_t n) {
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const float4 v = *reinterpret_cast<const float4 *>(p + i);
+    *reinterpret_cast<uint2 *>(o + i) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  } else {
+    for (int64_t k = i; k < n; ++k) o[k] = static_cast<__bf16>(p[k]);
+  }
+}
+
 __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) {
   (void)reduce_slab_block(q, blockIdx.x);
 }
@@ -576,6 +594,9 @@ struct ppo_lstm_ctx {
   __bf16 *x16;                       // [rows][W*O]
   __bf16 *dg16[2][PPO_MAX_LAYERS];   // [rows*W][8H]
   __bf16 *hp16[2][PPO_MAX_LAYERS];   // [rows*W][2H]
+  __bf16 *p16;                       // [total] bf16 copy of the parameters (minibatch steps)
+  const __bf16 *w16;                 // p16 while a bf16 minibatch step runs (its GEMMs' weight
+                                     // operands), else null
   float *gh, *dhrec, *dcarry;        // [rows][8H], [rows][2H], [rows][2H]
   float *dy[2], *tmp;                // [rows*W][2H]
   float *feat_a, *feat_c;            // [rows][W*2H], [rows][2H]
@@ -708,6 +729,8 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
     for (int d = 0; d < 2; ++d) {
       p[d].a = in;
       p[d].a16 = l == 0 ? xin16 : nullptr;
+      // bf16 rows and the bf16 weight copy (rows of L.in values: 8-B loads need L.in % 4 == 0)
+      p[d].b16 = (p[d].a16 && x->w16 && L.in % 4 == 0) ? x->w16 + L.w_ih[d] : nullptr;
       p[d].lda = L.in;
       p[d].b = P + L.w_ih[d];
       p[d].ldb = L.in;
@@ -746,8 +769,14 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
           // (bf16 in bf16 mode)
           rec.bytes = 4.0 * 2 * 4.0 * H * H + 2.0 * b * H * (4.0 * (1 + 4 + 2 + 4 + 2) + (b16 ? 2.0 : 4.0));
         }
-        launch_k(rec, lstm_step_fwd_kernel, dim3(ceil_div(b, kStepRows), H / kStepUnits, 2),
-                 dim3(256), 0, st, a);
+        const dim3 grid(ceil_div(b, kStepRows), H / kStepUnits, 2);
+        if (x->w16) {
+          a.whh16[0] = x->w16 + L.w_hh[0];
+          a.whh16[1] = x->w16 + L.w_hh[1];
+          launch_k(rec, lstm_step_fwd_kernel<true>, grid, dim3(256), 0, st, a);
+        } else {
+          launch_k(rec, lstm_step_fwd_kernel<false>, grid, dim3(256), 0, st, a);
+        }
         PPO_LAUNCHED();
         continue;
       }
@@ -898,6 +927,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
           const int tn = d == 0 ? W - s : s - 1;  // the step back-propagated at s - 1
           p[d].a = x->g[z][l] + static_cast<int64_t>(tn) * 8 * H + d * 4 * H;
           if (b16) p[d].a16 = x->dg16[z][l] + static_cast<int64_t>(tn) * 8 * H + d * 4 * H;
+          if (b16 && x->w16) p[d].b16 = x->w16 + L.w_hh[d];
           p[d].lda = static_cast<int64_t>(W) * 8 * H;
           p[d].b = P + L.w_hh[d];
           p[d].ldb = H;
@@ -957,6 +987,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
         GemmProblem p{};
         p.a = x->g[z][l] + d * 4 * H;
         if (b16) p.a16 = x->dg16[z][l] + d * 4 * H;
+        if (b16 && x->w16 && L.in % 4 == 0) p.b16 = x->w16 + L.w_ih[d];
         p.lda = 8 * H;
         p.b = P + L.w_ih[d];
         p.ldb = L.in;
@@ -1047,6 +1078,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   };
   const int64_t o_x = take(R * W * O);
   const int64_t o_x16 = take((R * W * O + 1) / 2);  // bf16 buffers: half the floats
+  const int64_t o_p16 = take((x->total + 1) / 2);
   int64_t o_g[2][PPO_MAX_LAYERS], o_c[2][PPO_MAX_LAYERS], o_y[2][PPO_MAX_LAYERS],
       o_hp[2][PPO_MAX_LAYERS], o_dg16[2][PPO_MAX_LAYERS], o_hp16[2][PPO_MAX_LAYERS];
   for (int z = 0; z < 2; ++z)
@@ -1084,6 +1116,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   float *w = x->ws;
   x->x = w + o_x;
   x->x16 = reinterpret_cast<__bf16 *>(w + o_x16);
+  x->p16 = reinterpret_cast<__bf16 *>(w + o_p16);
   for (int z = 0; z < 2; ++z)
     for (int l = 0; l < x->net[z].layers; ++l) {
       x->g[z][l] = w + o_g[z][l];
@@ -1250,6 +1283,19 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   const ppo_lstm_cfg &c = x->cfg;
   const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
   const int din = W * O;
+  // bf16 mode: the LSTM GEMMs read a bf16 copy of the parameters made once per minibatch step
+  // (the rounding their staging applied to the f32 masters per workgroup) -- cleared on return
+  struct W16Scope {
+    ppo_lstm_ctx *x;
+    ~W16Scope() { x->w16 = nullptr; }
+  } w16_scope{x};
+  if (x->prec == PPO_PREC_BF16) {
+    launch_k(TimRec{KC_GATHER, "lstm_params_bf16_kernel", 0.0, 6.0 * x->total},
+             lstm_params_bf16_kernel, dim3(ceil_div(x->total, 4 * 256)), dim3(256), 0, st,
+             x->params, x->p16, x->total);
+    PPO_LAUNCHED();
+    x->w16 = x->p16;
+  }
   // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
   // (rows of O values: the GEMMs' 8-B bf16 loads need O % 4 == 0, else the f32 rows as before)
   const __bf16 *x16 = x->prec == PPO_PREC_BF16 && O % 4 == 0 ? x->x16 : nullptr;

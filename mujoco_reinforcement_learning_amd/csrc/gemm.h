@@ -679,9 +679,9 @@ static bool vec4_ok16(const GemmBatch &gb, int nprob, bool operand_a) {
   return true;
 }
 
-// bf16 operands from global memory (the BiLSTM's dG, h_prev and gathered rows): A alone (FWD,
-// PARTIAL) or A and B (PARTIAL), vector loads only -- the producers keep those buffers
-// 8-B aligned with ld % 4 == 0, which the host checks
+// bf16 operands from global memory (the BiLSTM's dG, h_prev and gathered rows, and its bf16
+// weight copy): A alone or A and B (FWD, PARTIAL), vector loads for the bf16 operands -- the
+// producers keep those buffers 8-B aligned with ld % 4 == 0, which the host checks
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_gemm_bf16_src(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t st) {
   const bool a16 = gb.p[0].a16 != nullptr, b16 = gb.p[0].b16 != nullptr;
@@ -695,8 +695,7 @@ static int launch_gemm_bf16_src(const GemmBatch &gb, int nprob, dim3 grid, hipSt
   if constexpr (EPI == EPI_DX) {
     PPO_REQUIRE(false, "gemm: no bf16-source DX variant");
   } else {
-    PPO_REQUIRE(!b16 || EPI == EPI_PARTIAL, "gemm: bf16 B operand only in the weight-gradient GEMM");
-    if (EPI == EPI_PARTIAL && b16)
+    if (b16)
       launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, true>(gb, nprob, grid, st);
     else if (vb)
       launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, false>(gb, nprob, grid, st);
