@@ -151,10 +151,10 @@ def roofline(name, c, traffic, force_hbm=False):
     (bytes / 8 TB/s); achieved = that work per launch / mean launch duration."""
     launches = max(c["launches"], 1)
     avg_s = c["ms"] * 1e-3 / launches
-    # the fused update kernel, the wide path's GEMMs and the pixel encoder's LDS-staged
+    # the fused update kernel, the wide path's GEMMs (wide_gemm / wide_pair) and the pixel encoder's LDS-staged
     # convolutions (conv_pixel.h, conv_lds.h) are bf16-only; the layered GEMMs and conv_kernel
     # carry their dtype in the name
-    bf16 = ("bf16" in name or "wide_gemm" in name or c["class"] == "fused_update"
+    bf16 = ("bf16" in name or name.startswith("wide_") or c["class"] == "fused_update"
             or "_lds_kernel" in name or name.startswith("pixel_"))
     peak_f = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
     t_mfma = c["flops"] / (peak_f * 1e12)

@@ -762,7 +762,9 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         a.cell.s = s;
         a.whh[0] = P + L.w_hh[0];
         a.whh[1] = P + L.w_hh[1];
-        TimRec rec{KC_LSTM, "lstm_step_fwd_kernel", 0.0, 0.0};
+        // the launched instantiation's name (rocprof's, for the traffic table)
+        TimRec rec{KC_LSTM, x->w16 ? "lstm_step_fwd_kernel<true>" : "lstm_step_fwd_kernel<false>",
+                   0.0, 0.0};
         if (tim_active()) {
           rec.flops = 2.0 * 2 * b * 4.0 * H * H;
           // W_hh and h_prev once, Gx / c_prev / h_prev in, gates / c / h out (f32), h_prev out
