@@ -76,7 +76,7 @@ def test_policy_step_large_nets(gpu, shape, n):
 
 
 # --------------------------------------------------------------- minibatch gradient (A11-A13)
-def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
+def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4, bf16_bar=None):
     obs, act, w = shape["obs"], shape["act"], shape.get("window", 1)
     eng, ref = _agent_pair(gpu, seed, rows_total, b, obs, act, shape["hidden"],
                            shape.get("critic_hidden"), w, precision=precision)
@@ -111,7 +111,7 @@ def _minibatch_case(gpu, shape, rows_total, b, precision, seed=4):
     worst, worst_l2, off, bad = 0.0, 0.0, 0, []
     # f32: summation order only.  bf16 vs the f64-accumulated emulation: bf16 rounding flips of
     # intermediates (1 bf16 ulp = 2^-8 relative) through 3 hidden layers of 512
-    bar, bar_l2 = (2e-5, 2e-5) if precision == "f32" else BF16_GRAD_BAR
+    bar, bar_l2 = (2e-5, 2e-5) if precision == "f32" else (bf16_bar or BF16_GRAD_BAR)
     for name, r_ in ref_g:
         k = r_.numel()
         a = gd[off:off + k]
@@ -162,6 +162,38 @@ def test_minibatch_grad_humanoid(gpu, precision):
 
 def test_minibatch_grad_main_py_network(gpu):
     _minibatch_case(gpu, MAIN_PY, 1000, 500, "f32")
+
+
+def test_minibatch_grad_humanoid_bf16_paired_launches(gpu, monkeypatch):
+    """At minibatch sizes above 4,096 rows the wide path runs each hidden layer's WGRAD and DGRAD
+    as one wide_pair_kernel launch (DGRAD writing dZ to its own buffer): held to the
+    f64-accumulated bf16 emulation at the bench's B_local = 8,192, and bitwise equal to the two
+    separate launches (PPO_WIDE_PAIR0=1) -- gradient and losses.  The emulation bar's max-element
+    part is 1.5e-2 here (1e-2 at 2,048 rows): four times the rows in every weight-gradient column
+    sum, four times the bf16 rounding flips of intermediates behind one element (observed
+    1.1e-2 on one critic element; the rel-L2 bar stays 5e-3, observed <= 1.9e-3)."""
+    _minibatch_case(gpu, HUMANOID, 16384, 8192, "bf16", bf16_bar=(1.5e-2, 5e-3))
+    eng, _ = _agent_pair(gpu, 4, 16384, 8192, HUMANOID["obs"], HUMANOID["act"],
+                         HUMANOID["hidden"], None, 1, precision="bf16")
+    g = torch.Generator().manual_seed(11)
+    n, b, obs, act = 16384, 8192, HUMANOID["obs"], HUMANOID["act"]
+    args = [t.to(gpu) for t in (torch.randn(n, obs, generator=g),
+                                torch.randn(n, act, generator=g) * 0.5,
+                                torch.randn(n, generator=g) - 3, torch.randn(n, generator=g),
+                                torch.randn(n, generator=g))]
+    rows = torch.randperm(n, generator=g)[:b].to(torch.int32).to(gpu)
+    outs = []
+    for pair0 in (False, True):
+        if pair0:
+            monkeypatch.setenv("PPO_WIDE_PAIR0", "1")
+        grad, loss = torch.empty(eng.engine.n_params, device=gpu), torch.empty(2, device=gpu)
+        eng.engine.minibatch_grad(*args, rows, b, grad, loss, 0.9, 1.1, 1e-4, 1.0 / b,
+                                  1.0 / (b * act))
+        torch.cuda.synchronize()
+        outs.append((grad.clone(), loss.clone()))
+    monkeypatch.delenv("PPO_WIDE_PAIR0")
+    assert torch.equal(outs[0][0], outs[1][0]), int((outs[0][0] != outs[1][0]).sum())
+    assert torch.equal(outs[0][1], outs[1][1])
 
 
 # ----------------------------------------------------------------- full iteration vs oracle
