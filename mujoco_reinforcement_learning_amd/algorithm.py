@@ -18,6 +18,7 @@ scaling its loss by the global minibatch size.
 from __future__ import annotations
 
 import time
+import warnings
 from typing import Callable, Optional
 
 import torch
@@ -416,7 +417,8 @@ class PPOEngine:
                                  eng.n_actor, sched, 1 - beta1, beta2, 1 - beta2, eps)
 
         if (self.dp.active and not self.dp.graph_safe or self.dp.rehearse and not self.dp.comm
-                or not getattr(self.run.engine_config, "train_graph", True)):
+                or not getattr(self.run.engine_config, "train_graph", True)
+                or getattr(self, "_tg_capture_failed", False)):
             body()  # torch.distributed (gloo) collectives and the no-op rehearsal stay eager
             return self._loss_buf
         if self._tg_graph is None:
@@ -429,8 +431,20 @@ class PPOEngine:
             # the native RCCL all-reduce (DataParallel.comm) is recorded like a kernel; its proxy
             # threads keep running during capture, so only this thread's calls are checked
             mode = "thread_local" if self.dp.comm is not None else "global"
-            with torch.cuda.graph(g, capture_error_mode=mode):
+            try:
+                with torch.cuda.graph(g, capture_error_mode=mode):
+                    body()
+            except RuntimeError as err:
+                if self.dp.comm is None:
+                    raise
+                # a collective the RCCL build cannot record: nothing ran during the capture and
+                # body() depends on no host state it changes, so the step runs eagerly from here on
+                warnings.warn(f"capturing the data-parallel step with the native RCCL all-reduce "
+                              f"failed ({err}); the update loop runs eagerly")
+                self._tg_capture_failed = True
+                torch.cuda.synchronize(dev)
                 body()
+                return self._loss_buf
             self._tg_graph = g
         self._tg_graph.replay()
         return self._loss_buf

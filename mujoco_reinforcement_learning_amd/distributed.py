@@ -25,6 +25,7 @@ all-reduce").  gloo process groups (CPU tests) keep torch.distributed.all_reduce
 from __future__ import annotations
 
 import os
+import warnings
 from typing import Optional, Tuple
 
 import torch
@@ -120,7 +121,6 @@ class DataParallel:
         if self.rehearse_rccl and self.backend != "nccl":
             raise RuntimeError("PPO_DP_REHEARSE=rccl needs an initialised nccl process group")
         if self.rehearse:
-            import warnings
             how = ("native RCCL exchange, graph-captured" if self.rehearse_rccl
                    else "no-op exchange, eager")
             warnings.warn(f"PPO_DP_REHEARSE={rehearse}: running the data-parallel kernel sequence "
@@ -146,7 +146,12 @@ class DataParallel:
             engine.loss_entropy_share(1.0 if self.rank == 0 else 0.0)
         if self.comm is None and (self.backend == "nccl" and (self.world > 1 or self.rehearse_rccl)):
             if os.environ.get("PPO_DP_NATIVE", "1") == "1":
-                self.comm = NativeComm(self.pg, device, self.world, self.rank)
+                try:
+                    self.comm = NativeComm(self.pg, device, self.world, self.rank)
+                except RuntimeError as err:  # _lib.EngineError: no usable RCCL in this process
+                    warnings.warn(f"native RCCL communicator unavailable ({err}); the gradient "
+                                  f"all-reduce goes through torch.distributed, eagerly")
+                    self.comm = None
         if self.comm is not None and hasattr(engine, "set_comm"):
             engine.set_comm(self.comm)
 
