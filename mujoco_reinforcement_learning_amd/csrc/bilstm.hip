@@ -41,6 +41,8 @@
 #include "gemm_ops.h"
 #include "reduce_slabs.h"
 #include "timing.h"
+#include "wide_gemm.h"
+#include "wide_ops.h"
 
 namespace ppo {
 namespace lstm {
@@ -428,16 +430,38 @@ __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) 
   (void)reduce_slab_block(q, blockIdx.x);
 }
 
-// xg16 (bf16 mode): the rows as bf16 instead of f32 (GEMM operands only)
+// xg16 (bf16 mode): the rows as bf16 instead of f32 (GEMM operands only), one (row, step) of O
+// values per ld16-wide row
 __global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
                                         const int32_t *__restrict__ rows, int b, int din,
-                                        float *__restrict__ xg, __bf16 *__restrict__ xg16) {
+                                        float *__restrict__ xg, __bf16 *__restrict__ xg16, int o,
+                                        int ld16) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= static_cast<int64_t>(b) * din) return;
   const int64_t j = i / din;
-  const float v = states[static_cast<int64_t>(rows[j]) * din + (i - j * din)];
-  if (xg16) xg16[i] = static_cast<__bf16>(v);
-  else xg[i] = v;
+  const int64_t within = i - j * din;
+  const float v = states[static_cast<int64_t>(rows[j]) * din + within];
+  if (xg16) {
+    const int64_t rw = j * (din / o) + within / o;  // row (j, t) of the [b*W][O] view
+    xg16[rw * ld16 + within % o] = static_cast<__bf16>(v);
+  } else {
+    xg[i] = v;
+  }
+}
+
+// The layer-0 W_ih images of both nets and directions as bf16 [4H][ld16] (pad columns stay zero)
+struct WihImages {
+  const float *src[4];
+  __bf16 *dst[4];
+  int rows, in, ld16;
+};
+__global__ __launch_bounds__(256) void lstm_wih_image_kernel(WihImages q) {
+  const int64_t per = static_cast<int64_t>(q.rows) * q.in;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= 4 * per) return;
+  const int img = static_cast<int>(i / per);
+  const int64_t e = i - img * per, r = e / q.in, c = e - r * q.in;
+  q.dst[img][r * q.ld16 + c] = static_cast<__bf16>(q.src[img][e]);
 }
 
 __global__ void add_inplace_kernel(float *__restrict__ a, const float *__restrict__ b, int64_t n) {
@@ -591,7 +615,9 @@ struct ppo_lstm_ctx {
   float *g[2][PPO_MAX_LAYERS];       // [rows*W][8H]
   float *c[2][PPO_MAX_LAYERS], *y[2][PPO_MAX_LAYERS], *hp[2][PPO_MAX_LAYERS];  // [rows*W][2H]
   // bf16 mode: the GEMM-only operands as bf16 (gathered states, dG, h_prev)
-  __bf16 *x16;                       // [rows][W*O]
+  __bf16 *x16;                       // [rows*W + 128][ldx16] (pad columns zero)
+  int ldx16;                         // round_up(O, 64): the wide GEMM's k extent
+  __bf16 *wih16[2][2];               // layer-0 W_ih per net / direction, [4H][ldx16] bf16
   __bf16 *dg16[2][PPO_MAX_LAYERS];   // [rows*W][8H]
   __bf16 *hp16[2][PPO_MAX_LAYERS];   // [rows*W][2H]
   __bf16 *p16;                       // [total] bf16 copy of the parameters (minibatch steps)
@@ -715,7 +741,12 @@ int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int ma
 
 // LSTM net z forward over xin [b*W][O] (batch-major rows); fills g/c/y/hp of every layer and the
 // features of the top layer (actor: all steps, critic: t = W-1).
-// xin16 (bf16 mode, nullable): the same rows as bf16 -- the input projection reads those.
+static const float *P_bias_ih(const ppo_lstm_ctx *x, const LstmLayer &L, int d) {
+  return x->params + L.b_ih[d];
+}
+
+// xin16 (bf16 mode, nullable): the same rows as bf16, [b*W][ldx16] -- the input projection
+// reads those.
 int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, int b,
                  hipStream_t st) {
   const LstmNet &N = x->net[z];
@@ -728,9 +759,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
     GemmProblem p[2] = {};
     for (int d = 0; d < 2; ++d) {
       p[d].a = in;
-      p[d].a16 = l == 0 ? xin16 : nullptr;
-      // bf16 rows and the bf16 weight copy (rows of L.in values: 8-B loads need L.in % 4 == 0)
-      p[d].b16 = (p[d].a16 && x->w16 && L.in % 4 == 0) ? x->w16 + L.w_ih[d] : nullptr;
+      // (bf16 minibatch rows go through the wide GEMM below; this form reads f32 rows)
       p[d].lda = L.in;
       p[d].b = P + L.w_ih[d];
       p[d].ldb = L.in;
@@ -740,7 +769,28 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
       p[d].m = b * W;
       p[d].n = 4 * H;
     }
-    if (int rc = gemm_fwd(x, p, 2, L.in, b * W, 4 * H, PPO_ACT_IDENTITY, false, st)) return rc;
+    if (l == 0 && xin16 && x->w16 && (4 * H) % 128 == 0) {
+      // the bf16 minibatch rows (padded to 64-deep k-tiles) through the wide path's LDS-DMA GEMM
+      // into f32 Gx + b_ih: the same k-steps in the same order over the same bf16 operands (zeros
+      // past O), the bias added as the layered epilogue adds it -- bitwise gemm_bf16_kernel's Gx
+      wide::WideBatch wb{};
+      for (int d = 0; d < 2; ++d) {
+        wide::WideProblem &P = wb.p[d];
+        P.a = xin16;
+        P.lda = x->ldx16;
+        P.b = x->wih16[z][d];
+        P.ldb = x->ldx16;
+        P.c = x->g[z][l] + d * 4 * H;
+        P.ldc = 8 * H;
+        P.bias = P_bias_ih(x, L, d);
+        P.m = b * W;
+        P.n = 4 * H;
+        P.k = x->ldx16;
+      }
+      if (int rc = wide::run(wide::WK_F32, wb, 2, b * W, 4 * H, 0, st)) return rc;
+    } else if (int rc = gemm_fwd(x, p, 2, L.in, b * W, 4 * H, PPO_ACT_IDENTITY, false, st)) {
+      return rc;
+    }
     const bool fused_step = x->prec == PPO_PREC_BF16 && x->fused_step && H % kStepUnits == 0;
     for (int s = 0; s < W; ++s) {
       if (s > 0 && fused_step) {
@@ -966,7 +1016,7 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
       pi[d].lda = 8 * H;
       pi[d].b = in;
       pi[d].b16 = l == 0 ? xin16 : nullptr;
-      pi[d].ldb = L.in;
+      pi[d].ldb = (l == 0 && xin16) ? x->ldx16 : L.in;
       pi[d].c = x->slabs + L.w_ih[d];
       pi[d].ldc = L.in;
       pi[d].colsum = x->slabs + L.b_ih[d];
@@ -1079,7 +1129,13 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
     return at;
   };
   const int64_t o_x = take(R * W * O);
-  const int64_t o_x16 = take((R * W * O + 1) / 2);  // bf16 buffers: half the floats
+  // bf16 buffers: half the floats; the gathered rows padded to the wide GEMM's 64-deep k-tiles
+  // and 128-row tiles (its A operand reads whole tiles)
+  const int ldx16 = static_cast<int>(align_up(O, 64));
+  const int64_t o_x16 = take(((R * W + 128) * ldx16 + 1) / 2);
+  int64_t o_wih16[2][2];
+  for (int z = 0; z < 2; ++z)
+    for (int d = 0; d < 2; ++d) o_wih16[z][d] = take((4LL * H * ldx16 + 1) / 2);
   const int64_t o_p16 = take((x->total + 1) / 2);
   int64_t o_g[2][PPO_MAX_LAYERS], o_c[2][PPO_MAX_LAYERS], o_y[2][PPO_MAX_LAYERS],
       o_hp[2][PPO_MAX_LAYERS], o_dg16[2][PPO_MAX_LAYERS], o_hp16[2][PPO_MAX_LAYERS];
@@ -1118,6 +1174,9 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   float *w = x->ws;
   x->x = w + o_x;
   x->x16 = reinterpret_cast<__bf16 *>(w + o_x16);
+  x->ldx16 = ldx16;
+  for (int z = 0; z < 2; ++z)
+    for (int d = 0; d < 2; ++d) x->wih16[z][d] = reinterpret_cast<__bf16 *>(w + o_wih16[z][d]);
   x->p16 = reinterpret_cast<__bf16 *>(w + o_p16);
   for (int z = 0; z < 2; ++z)
     for (int l = 0; l < x->net[z].layers; ++l) {
@@ -1144,8 +1203,13 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   for (int k = 0; k < 3; ++k)
     for (int p = 0; p < 2; ++p) x->dz[k][p] = w + o_dz[k][p];
   x->slabs = w + o_slabs;
-  // the alignment padding between tensors is never written by a GEMM: zero slabs reduce to 0
+  // the alignment padding between tensors is never written by a GEMM: zero slabs reduce to 0;
+  // the padded bf16 rows / images keep zero pad columns (only their first O are ever written)
   e = hipMemset(x->slabs, 0, sizeof(float) * kSplits * x->total);
+  if (e == hipSuccess) e = hipMemset(x->x16, 0, sizeof(__bf16) * (R * W + 128) * ldx16);
+  for (int z = 0; z < 2 && e == hipSuccess; ++z)
+    for (int d = 0; d < 2 && e == hipSuccess; ++d)
+      e = hipMemset(x->wih16[z][d], 0, sizeof(__bf16) * 4LL * H * ldx16);
   if (e != hipSuccess) {
     set_error("ppo_lstm_ctx_create: hipMemset failed: %s", hipGetErrorString(e));
     (void)hipFree(x->ws);
@@ -1297,13 +1361,26 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
              x->params, x->p16, x->total);
     PPO_LAUNCHED();
     x->w16 = x->p16;
+    WihImages wi{};  // the input projection's B operands, at the padded row stride
+    int k = 0;
+    for (int z = 0; z < 2; ++z)
+      for (int d = 0; d < 2; ++d, ++k) {
+        wi.src[k] = x->params + x->net[z].l[0].w_ih[d];
+        wi.dst[k] = x->wih16[z][d];
+      }
+    wi.rows = 4 * H;
+    wi.in = O;
+    wi.ld16 = x->ldx16;
+    launch_k(TimRec{KC_GATHER, "lstm_wih_image_kernel", 0.0, 4.0 * 4 * H * O * 6.0},
+             lstm_wih_image_kernel, dim3(ceil_div(4LL * 4 * H * O, 256)), dim3(256), 0, st, wi);
+    PPO_LAUNCHED();
   }
   // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
-  // (rows of O values: the GEMMs' 8-B bf16 loads need O % 4 == 0, else the f32 rows as before)
-  const __bf16 *x16 = x->prec == PPO_PREC_BF16 && O % 4 == 0 ? x->x16 : nullptr;
+  // (rows of O values at a stride of ldx16, a multiple of 64: the wide GEMM's k-tiles)
+  const __bf16 *x16 = x->prec == PPO_PREC_BF16 ? x->x16 : nullptr;
   launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
            dim3(ceil_div(static_cast<int64_t>(b) * din, 256)), dim3(256), 0, st, states_d, rows_d,
-           b, din, x->x, const_cast<__bf16 *>(x16));
+           b, din, x->x, const_cast<__bf16 *>(x16), O, x->ldx16);
   PPO_LAUNCHED();
   if (int rc = forward_all(x, x->x, x16, b, st)) return rc;
   HeadArgs h{};

@@ -12,7 +12,8 @@
 //                   DGRAD bf16 act'(aux) * C          (input gradient, written over aux) and the
 //                                                     f32 column sums of the result per row tile
 //                                                     (bias gradient partials)
-//                   F32   f32 C                       (head pre-activations)
+//                   F32   f32 C (+ bias)              (head pre-activations; the BiLSTM's
+//                                                     input projection)
 //   TT   slab[split][m][n] = sum_{k in split} A[k][m] B[k][n]   (weight gradient dY^T X, split-K
 //                                                 over minibatch rows; both operands k-outer)
 //
@@ -386,7 +387,7 @@ __device__ __forceinline__ void wide_gemm_body(const WideBatch &wb, int bx, int 
     float bias[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias[e] = 0.f;
-    if (KIND == WK_FWD && P.bias && ncol) {
+    if ((KIND == WK_FWD || KIND == WK_F32) && P.bias && ncol) {
       const float4 b0 = *reinterpret_cast<const float4 *>(P.bias + n);
       const float4 b1 = *reinterpret_cast<const float4 *>(P.bias + n + 4);
       bias[0] = b0.x, bias[1] = b0.y, bias[2] = b0.z, bias[3] = b0.w;
@@ -409,6 +410,9 @@ __device__ __forceinline__ void wide_gemm_body(const WideBatch &wb, int bx, int 
         const bool live = m < count;
         if (!ncol) continue;
         if constexpr (KIND == WK_F32) {
+          if (P.bias)  // f32 C + bias (the BiLSTM's input projection); the heads pass none
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] + bias[e];
           float *dst = static_cast<float *>(P.c) + static_cast<int64_t>(m) * P.ldc + n;
           *reinterpret_cast<float4 *>(dst) =
               live ? make_float4(v[0], v[1], v[2], v[3]) : make_float4(0.f, 0.f, 0.f, 0.f);

@@ -54,6 +54,10 @@ static int run_kind(const WideBatch &wb, int nprob, int max_m, int max_n, int kf
       default: return launch_cfg<2, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
     }
   }
+  // F32 outputs wider than the heads (the BiLSTM's input projection, 4H columns): the
+  // minibatch tile
+  if (KIND == WK_F32 && max_n > 128 && max_m > 4096)
+    return launch_cfg<2, 1, 2, 4, KIND, 2>(wb, nprob, max_m, max_n, kflops, st);
   if (KIND == WK_F32 || (KIND == WK_FWD && max_n <= 32))
     return launch_cfg<1, 1, 4, 1, KIND, 8>(wb, nprob, max_m, max_n, kflops, st);
   if (max_m <= 4096) {

@@ -9,7 +9,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-PHASES = ["prologue: obs / param / eps loads issued, Philox noise", "LDS images + raw window out",
+PHASES = ["prologue: obs / param / eps loads issued (Philox noise when no eps is given)", "LDS images + raw window out",
           "per-(row, slice) f64 mean / std (lane-parallel butterflies)", "standardised states -> X image + state out",
           "L0 MFMA + act -> A1", "L1 MFMA pass (issue)", "act -> A2 image",
           "heads (tanh, sample, logp / value) + writes"]
@@ -29,9 +29,11 @@ def main():
     obs = torch.randn(n, 17, device=dev, dtype=torch.float64)
     st = torch.empty(n, 17, device=dev)
     a, lp, v = torch.empty(n, 6, device=dev), torch.empty(n, device=dev), torch.empty(n, device=dev)
+    eps = torch.randn(n, 6, device=dev)
     for rep in range(3):
         e.phase_stamps(True)
-        e.observe_act(win, st, obs=obs, seed=1, offset=rep, action=a, logp=lp, value=v)
+        # the bench's form: the rollout's noise drawn ahead of the steps (eps given)
+        e.observe_act(win, st, obs=obs, eps=eps, seed=1, offset=rep, action=a, logp=lp, value=v)
         # the policy kernel writes 11 slots per workgroup (phase_stamps views them as 13)
         s = e.phase_stamps(False).flatten()[:2 * 128 * 11].view(2, 128, 11).double()
     g = n // 32  # 32-row workgroups
