@@ -1031,8 +1031,34 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
       ph[d].colsum = x->slabs + L.b_hh[d];
       ph[d].n = H;
     }
+    // dW_hh on the wide path's split-K WGRAD (LDS-DMA, both bf16 operands k-outer) when the
+    // rows fill whole 64-row k-tiles: it has no column sums, so dW_ih's GEMM writes the bias
+    // gradient partials for b_hh too (the same column sums of dG, the same order)
+    const bool wide_ph = b16 && xin16 && (static_cast<int64_t>(b) * W) % 64 == 0 &&
+                         (4 * H) % 128 == 0 && H % 8 == 0;
+    if (wide_ph)
+      for (int d = 0; d < 2; ++d) pi[d].colsum2 = x->slabs + L.b_hh[d];
     if (int rc = gemm_partial(x, pi, 2, b * W, 4 * H, L.in, st)) return rc;
-    if (int rc = gemm_partial(x, ph, 2, b * W, 4 * H, H, st)) return rc;
+    if (wide_ph) {
+      wide::WideBatch wb{};
+      for (int d = 0; d < 2; ++d) {
+        wide::WideProblem &Q = wb.p[d];
+        Q.a = x->dg16[z][l] + d * 4 * H;
+        Q.lda = 8 * H;
+        Q.b = x->hp16[z][l] + d * H;
+        Q.ldb = 2 * H;
+        Q.c = x->slabs + L.w_hh[d];
+        Q.ldc = H;
+        Q.m = 4 * H;
+        Q.n = H;
+        Q.k = b * W;
+        Q.slab_stride = x->total;
+      }
+      wb.splits = x->splits;
+      if (int rc = wide::run(wide::WK_WGRAD, wb, 2, 4 * H, H, b * W, st)) return rc;
+    } else if (int rc = gemm_partial(x, ph, 2, b * W, 4 * H, H, st)) {
+      return rc;
+    }
     if (l > 0) {  // dY of the layer below = sum_d dG_d W_ih_d (no activation between layers)
       const int nxt = cur ^ 1;
       for (int d = 0; d < 2; ++d) {

@@ -36,6 +36,7 @@ struct GemmProblem {
   const float *bias;   // EPI_FWD, nullable
   const float *aux;    // EPI_DX: layer input activations (same layout as c; c may alias it)
   float *colsum;       // EPI_PARTIAL: bias-gradient slab base, nullable
+  float *colsum2;      // bf16 kernel: a second slab base receiving the same column sums, nullable
   int m, n;
   // bf16 mode: the operand already bf16 in global memory (then a / b are unused), nullable
   const __bf16 *a16, *b16;
@@ -593,6 +594,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_bf16_kernel(GemmBatch gb) {
       float s = 0.f;
       for (int q = 0; q < PARTS; ++q) s += red[q * BM + tid];
       P.colsum[static_cast<int64_t>(split) * gb.slab_stride + m0 + tid] = s;
+      if (P.colsum2) P.colsum2[static_cast<int64_t>(split) * gb.slab_stride + m0 + tid] = s;
     }
   }
 }
