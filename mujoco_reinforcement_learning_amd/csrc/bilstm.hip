@@ -741,7 +741,7 @@ int gemm_partial(ppo_lstm_ctx *x, const GemmProblem *p, int np, int rows, int ma
 
 // LSTM net z forward over xin [b*W][O] (batch-major rows); fills g/c/y/hp of every layer and the
 // features of the top layer (actor: all steps, critic: t = W-1).
-static const float *P_bias_ih(const ppo_lstm_ctx *x, const LstmLayer &L, int d) {
+static const float *ih_bias(const ppo_lstm_ctx *x, const LstmLayer &L, int d) {
   return x->params + L.b_ih[d];
 }
 
@@ -782,7 +782,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         P.ldb = x->ldx16;
         P.c = x->g[z][l] + d * 4 * H;
         P.ldc = 8 * H;
-        P.bias = P_bias_ih(x, L, d);
+        P.bias = ih_bias(x, L, d);
         P.m = b * W;
         P.n = 4 * H;
         P.k = x->ldx16;
@@ -1031,33 +1031,50 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
       ph[d].colsum = x->slabs + L.b_hh[d];
       ph[d].n = H;
     }
-    // dW_hh on the wide path's split-K WGRAD (LDS-DMA, both bf16 operands k-outer) when the
-    // rows fill whole 64-row k-tiles: it has no column sums, so dW_ih's GEMM writes the bias
-    // gradient partials for b_hh too (the same column sums of dG, the same order)
-    const bool wide_ph = b16 && xin16 && (static_cast<int64_t>(b) * W) % 64 == 0 &&
-                         (4 * H) % 128 == 0 && H % 8 == 0;
-    if (wide_ph)
-      for (int d = 0; d < 2; ++d) pi[d].colsum2 = x->slabs + L.b_hh[d];
-    if (int rc = gemm_partial(x, pi, 2, b * W, 4 * H, L.in, st)) return rc;
-    if (wide_ph) {
+    // bf16 mode, rows filling whole 64-row k-tiles: dW_ih (layer 0: the padded bf16 rows) and
+    // dW_hh on the wide path's split-K WGRAD (LDS-DMA, both bf16 operands k-outer); dW_ih's
+    // launch also sums dG's columns per split (wide_gemm.h acol) into the b_ih and b_hh slabs --
+    // the same column sums gemm_bf16_kernel's COLSUM took, in its own fixed order
+    const bool wide_w = b16 && xin16 && (static_cast<int64_t>(b) * W) % 64 == 0 &&
+                        (4 * H) % 128 == 0 && H % 8 == 0;
+    if (wide_w) {
       wide::WideBatch wb{};
       for (int d = 0; d < 2; ++d) {
+        const bool ih = l == 0;  // layer 0: x16 is the k-outer bf16 B operand
         wide::WideProblem &Q = wb.p[d];
         Q.a = x->dg16[z][l] + d * 4 * H;
         Q.lda = 8 * H;
+        Q.b = ih ? xin16 : nullptr;
+        Q.ldb = x->ldx16;
+        Q.c = x->slabs + L.w_ih[d];
+        Q.ldc = L.in;
+        Q.m = 4 * H;
+        Q.n = L.in;
+        Q.k = b * W;
+        Q.slab_stride = x->total;
+        Q.acol = x->slabs + L.b_ih[d];
+        Q.acol2 = x->slabs + L.b_hh[d];
+      }
+      wb.splits = x->splits;
+      if (l == 0) {
+        if (int rc = wide::run(wide::WK_WGRAD, wb, 2, 4 * H, L.in, b * W, st)) return rc;
+      } else {  // stacked layers' f32 inputs: the bf16-source GEMM, bias partials for both
+        for (int d = 0; d < 2; ++d) pi[d].colsum2 = x->slabs + L.b_hh[d];
+        if (int rc = gemm_partial(x, pi, 2, b * W, 4 * H, L.in, st)) return rc;
+      }
+      for (int d = 0; d < 2; ++d) {
+        wide::WideProblem &Q = wb.p[d];
         Q.b = x->hp16[z][l] + d * H;
         Q.ldb = 2 * H;
         Q.c = x->slabs + L.w_hh[d];
         Q.ldc = H;
-        Q.m = 4 * H;
         Q.n = H;
-        Q.k = b * W;
-        Q.slab_stride = x->total;
+        Q.acol = Q.acol2 = nullptr;
       }
-      wb.splits = x->splits;
       if (int rc = wide::run(wide::WK_WGRAD, wb, 2, 4 * H, H, b * W, st)) return rc;
-    } else if (int rc = gemm_partial(x, ph, 2, b * W, 4 * H, H, st)) {
-      return rc;
+    } else {
+      if (int rc = gemm_partial(x, pi, 2, b * W, 4 * H, L.in, st)) return rc;
+      if (int rc = gemm_partial(x, ph, 2, b * W, 4 * H, H, st)) return rc;
     }
     if (l > 0) {  // dY of the layer below = sum_d dG_d W_ih_d (no activation between layers)
       const int nxt = cur ^ 1;

@@ -71,6 +71,9 @@ struct WideProblem {
   int64_t n_colsum;
   int m, n, k;          // m, n: extents (m: row upper bound); k: NT reduction (multiple of 64)
   int64_t slab_stride;  // WGRAD: floats between split slabs
+  // WGRAD, nullable: per split, the column sums of A over the split's k rows (the bias gradient
+  // of a dY^T X product), at acol[split * slab_stride + m]; acol2 receives the same values
+  float *acol, *acol2;
 };
 
 struct WideBatch {
@@ -298,6 +301,14 @@ __device__ __forceinline__ void wide_gemm_body(const WideBatch &wb, int bx, int 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // WGRAD column sums of A (acol): the wn == 0 waves of the tile_n == 0 blocks add the 8 bf16
+  // k-values of each A fragment they feed the MFMA (lane l: column l & 31 of its 32-column tile,
+  // k-rows 8 (l >> 5) .. +7 of each 16-deep k-step) in a fixed order
+  const bool do_acol = C::TT && P.acol && tile_n == 0 && wn == 0;
+  float csum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) csum[i] = 0.f;
+
   // NS-stage LDS ring: tiles kt+1 .. kt+NS-1 in flight while tile kt is computed
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -331,8 +342,32 @@ __device__ __forceinline__ void wide_gemm_body(const WideBatch &wb, int bx, int 
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      if constexpr (C::TT) {
+        if (do_acol) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const uint4 u = __builtin_bit_cast(uint4, av[i]);
+            csum[i] += ((bf_lo(u.x) + bf_hi(u.x)) + (bf_lo(u.y) + bf_hi(u.y))) +
+                       ((bf_lo(u.z) + bf_hi(u.z)) + (bf_lo(u.w) + bf_hi(u.w)));
+          }
+        }
+      }
     }
     buf = buf + 1 == NS ? 0 : buf + 1;
+  }
+  if constexpr (C::TT) {
+    if (do_acol) {  // the two lane halves hold the same columns' other k-rows
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float s = csum[i] + __shfl_xor(csum[i], 32, 64);
+        const int mcol = m0 + (wm * TM + i) * 32 + lane;
+        if (lane < 32 && mcol < P.m) {
+          const int64_t o = static_cast<int64_t>(split) * P.slab_stride + mcol;
+          P.acol[o] = s;
+          if (P.acol2) P.acol2[o] = s;
+        }
+      }
+    }
   }
   __syncthreads();  // the staging buffers become the epilogue tile
 
