@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kRedThreads) void lstm_reduce_kernel(ReduceArgs q) 
 }
 
 // xg16 (bf16 mode): the rows as bf16 instead of f32 (GEMM operands only), one (row, step) of O
-// values per ld16-wide row
+// values per ld16-wide row; rows == nullptr: the states in order (the rollout's windows)
 __global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
                                         const int32_t *__restrict__ rows, int b, int din,
                                         float *__restrict__ xg, __bf16 *__restrict__ xg16, int o,
@@ -440,7 +440,7 @@ __global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
   if (i >= static_cast<int64_t>(b) * din) return;
   const int64_t j = i / din;
   const int64_t within = i - j * din;
-  const float v = states[static_cast<int64_t>(rows[j]) * din + within];
+  const float v = states[(rows ? static_cast<int64_t>(rows[j]) : j) * din + within];
   if (xg16) {
     const int64_t rw = j * (din / o) + within / o;  // row (j, t) of the [b*W][O] view
     xg16[rw * ld16 + within % o] = static_cast<__bf16>(v);
@@ -1310,6 +1310,54 @@ extern "C" int ppo_lstm_set_precision(ppo_lstm_ctx *x, int prec) {
   return 0;
 }
 
+// bf16 mode: the LSTM GEMMs read a bf16 copy of the parameters made once per call (the rounding
+// their staging applied to the f32 masters per workgroup) and layer 0's W_ih as padded images for
+// the wide projection; x->w16 is cleared again when the caller's W16Scope ends
+struct W16Scope {
+  ppo_lstm_ctx *x;
+  ~W16Scope() { x->w16 = nullptr; }
+};
+int prep_w16(ppo_lstm_ctx *x, hipStream_t st) {
+  if (x->prec != PPO_PREC_BF16) return 0;
+  const int H = x->cfg.latent, O = x->cfg.obs_dim;
+  launch_k(TimRec{KC_GATHER, "lstm_params_bf16_kernel", 0.0, 6.0 * x->total},
+           lstm_params_bf16_kernel, dim3(ceil_div(x->total, 4 * 256)), dim3(256), 0, st,
+           x->params, x->p16, x->total);
+  PPO_LAUNCHED();
+  x->w16 = x->p16;
+  WihImages wi{};  // the input projection's B operands, at the padded row stride
+  int k = 0;
+  for (int z = 0; z < 2; ++z)
+    for (int d = 0; d < 2; ++d, ++k) {
+      wi.src[k] = x->params + x->net[z].l[0].w_ih[d];
+      wi.dst[k] = x->wih16[z][d];
+    }
+  wi.rows = 4 * H;
+  wi.in = O;
+  wi.ld16 = x->ldx16;
+  launch_k(TimRec{KC_GATHER, "lstm_wih_image_kernel", 0.0, 4.0 * 4 * H * O * 6.0},
+           lstm_wih_image_kernel, dim3(ceil_div(4LL * 4 * H * O, 256)), dim3(256), 0, st, wi);
+  PPO_LAUNCHED();
+  return 0;
+}
+
+// The rollout's forward (policy step / forward) in bf16 mode on the minibatch step's operands:
+// the parameter images, the window rows as padded bf16 (the gather kernel, rows in order), the
+// wide projection and the W16 step kernels -- the same arithmetic as the layered f32-staged form
+// (RNE-rounded operands, the same k order), so rollout and update forwards stay bitwise equal
+int forward_rollout(ppo_lstm_ctx *x, const float *state_d, int n, hipStream_t st) {
+  if (x->prec != PPO_PREC_BF16) return forward_all(x, state_d, nullptr, n, st);
+  W16Scope w16_scope{x};
+  if (int rc = prep_w16(x, st)) return rc;
+  const int din = x->cfg.window * x->cfg.obs_dim;
+  launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
+           dim3(ceil_div(static_cast<int64_t>(n) * din, 256)), dim3(256), 0, st, state_d,
+           static_cast<const int32_t *>(nullptr), n, din, static_cast<float *>(nullptr), x->x16,
+           x->cfg.obs_dim, x->ldx16);
+  PPO_LAUNCHED();
+  return forward_all(x, state_d, x->x16, n, st);
+}
+
 extern "C" int ppo_lstm_forward(ppo_lstm_ctx *x, const float *state_d, int n, float *mean_d,
                                 float *std_d, float *value_d, float *actor_lstm_out_d,
                                 float *critic_lstm_out_d, void *stream) {
@@ -1319,7 +1367,7 @@ extern "C" int ppo_lstm_forward(ppo_lstm_ctx *x, const float *state_d, int n, fl
   PPO_HIP_TRY(hipSetDevice(x->device));
   TimingScope ts(x);
   hipStream_t st = as_stream(stream);
-  if (int rc = forward_all(x, state_d, nullptr, n, st)) return rc;
+  if (int rc = forward_rollout(x, state_d, n, st)) return rc;
   const int A = x->cfg.act_dim, W = x->cfg.window;
   const int64_t yb = sizeof(float) * static_cast<int64_t>(n) * W * 2 * x->cfg.latent;
   if (actor_lstm_out_d)
@@ -1356,7 +1404,7 @@ extern "C" int ppo_lstm_policy_step(ppo_lstm_ctx *x, const float *state_d, int n
   PPO_HIP_TRY(hipSetDevice(x->device));
   TimingScope ts(x);
   hipStream_t st = as_stream(stream);
-  if (int rc = forward_all(x, state_d, nullptr, n, st)) return rc;
+  if (int rc = forward_rollout(x, state_d, n, st)) return rc;
   const int nl = x->cfg.n_hidden;
   HeadArgs h{};
   h.mean = x->act_mu[nl];
@@ -1392,32 +1440,8 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   const ppo_lstm_cfg &c = x->cfg;
   const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
   const int din = W * O;
-  // bf16 mode: the LSTM GEMMs read a bf16 copy of the parameters made once per minibatch step
-  // (the rounding their staging applied to the f32 masters per workgroup) -- cleared on return
-  struct W16Scope {
-    ppo_lstm_ctx *x;
-    ~W16Scope() { x->w16 = nullptr; }
-  } w16_scope{x};
-  if (x->prec == PPO_PREC_BF16) {
-    launch_k(TimRec{KC_GATHER, "lstm_params_bf16_kernel", 0.0, 6.0 * x->total},
-             lstm_params_bf16_kernel, dim3(ceil_div(x->total, 4 * 256)), dim3(256), 0, st,
-             x->params, x->p16, x->total);
-    PPO_LAUNCHED();
-    x->w16 = x->p16;
-    WihImages wi{};  // the input projection's B operands, at the padded row stride
-    int k = 0;
-    for (int z = 0; z < 2; ++z)
-      for (int d = 0; d < 2; ++d, ++k) {
-        wi.src[k] = x->params + x->net[z].l[0].w_ih[d];
-        wi.dst[k] = x->wih16[z][d];
-      }
-    wi.rows = 4 * H;
-    wi.in = O;
-    wi.ld16 = x->ldx16;
-    launch_k(TimRec{KC_GATHER, "lstm_wih_image_kernel", 0.0, 4.0 * 4 * H * O * 6.0},
-             lstm_wih_image_kernel, dim3(ceil_div(4LL * 4 * H * O, 256)), dim3(256), 0, st, wi);
-    PPO_LAUNCHED();
-  }
+  W16Scope w16_scope{x};
+  if (int rc = prep_w16(x, st)) return rc;
   // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
   // (rows of O values at a stride of ldx16, a multiple of 64: the wide GEMM's k-tiles)
   const __bf16 *x16 = x->prec == PPO_PREC_BF16 ? x->x16 : nullptr;
