@@ -464,6 +464,22 @@ __global__ __launch_bounds__(256) void lstm_wih_image_kernel(WihImages q) {
   q.dst[img][r * q.ld16 + c] = static_cast<__bf16>(q.src[img][e]);
 }
 
+// W_hh^T images [H][4H] bf16 of every net / layer / direction (the recurrent-gradient GEMM's
+// k-inner B operand on the wide path); one thread per destination element
+struct WhhTImages {
+  const float *src[2 * 2 * PPO_MAX_LAYERS];
+  __bf16 *dst[2 * 2 * PPO_MAX_LAYERS];
+  int n, h;
+};
+__global__ __launch_bounds__(256) void lstm_whh_t_image_kernel(WhhTImages q) {
+  const int64_t per = 4LL * q.h * q.h;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= q.n * per) return;
+  const int img = static_cast<int>(i / per);
+  const int64_t e = i - img * per, j = e / (4 * q.h), k = e - j * (4 * q.h);
+  q.dst[img][e] = static_cast<__bf16>(q.src[img][k * q.h + j]);
+}
+
 __global__ void add_inplace_kernel(float *__restrict__ a, const float *__restrict__ b, int64_t n) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n) a[i] += b[i];
@@ -618,7 +634,8 @@ struct ppo_lstm_ctx {
   __bf16 *x16;                       // [rows*W + 128][ldx16] (pad columns zero)
   int ldx16;                         // round_up(O, 64): the wide GEMM's k extent
   __bf16 *wih16[2][2];               // layer-0 W_ih per net / direction, [4H][ldx16] bf16
-  __bf16 *dg16[2][PPO_MAX_LAYERS];   // [rows*W][8H]
+  __bf16 *dg16[2][PPO_MAX_LAYERS];   // [(rows + 128)*W][8H] (128 rows: the wide GEMM's A tiles)
+  __bf16 *whht16[2][PPO_MAX_LAYERS][2];  // W_hh^T per net / layer / direction, [H][4H] bf16
   __bf16 *hp16[2][PPO_MAX_LAYERS];   // [rows*W][2H]
   __bf16 *p16;                       // [total] bf16 copy of the parameters (minibatch steps)
   const __bf16 *w16;                 // p16 while a bf16 minibatch step runs (its GEMMs' weight
@@ -968,6 +985,10 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
   const int H = N.hidden, W = x->cfg.window;
   const float *P = x->params;
   const bool b16 = x->prec == PPO_PREC_BF16;
+  // the recurrent gradient on the wide path (W_hh^T images made by prep_w16); PPO_LSTM_DHREC=0
+  // keeps gemm_bf16_kernel (the bitwise test's reference)
+  const char *dv = getenv("PPO_LSTM_DHREC");
+  const bool wide_rec = b16 && x->w16 && H % 64 == 0 && !(dv && atoi(dv) == 0);
   int cur = 0;
   for (int l = N.layers - 1; l >= 0; --l) {
     const LstmLayer &L = N.l[l];
@@ -988,7 +1009,26 @@ int lstm_backward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16,
           p[d].m = b;
           p[d].n = H;
         }
-        if (int rc = gemm_fwd(x, p, 2, 4 * H, b, H, PPO_ACT_IDENTITY, true, st)) return rc;
+        if (wide_rec) {
+          // the wide path's LDS-DMA GEMM over the same bf16 operands (dG rows k-inner, W_hh^T
+          // images), the same k-steps of 16 in order: bitwise the layered dh_rec
+          wide::WideBatch wb{};
+          for (int d = 0; d < 2; ++d) {
+            wide::WideProblem &Q = wb.p[d];
+            Q.a = p[d].a16;
+            Q.lda = p[d].lda;
+            Q.b = x->whht16[z][l][d];
+            Q.ldb = 4 * H;
+            Q.c = p[d].c;
+            Q.ldc = p[d].ldc;
+            Q.m = b;
+            Q.n = H;
+            Q.k = 4 * H;
+          }
+          if (int rc = wide::run(wide::WK_F32, wb, 2, b, H, 0, st)) return rc;
+        } else if (int rc = gemm_fwd(x, p, 2, 4 * H, b, H, PPO_ACT_IDENTITY, true, st)) {
+          return rc;
+        }
       }
       CellBwdArgs a{};
       a.g = x->g[z][l];
@@ -1181,14 +1221,16 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
     for (int d = 0; d < 2; ++d) o_wih16[z][d] = take((4LL * H * ldx16 + 1) / 2);
   const int64_t o_p16 = take((x->total + 1) / 2);
   int64_t o_g[2][PPO_MAX_LAYERS], o_c[2][PPO_MAX_LAYERS], o_y[2][PPO_MAX_LAYERS],
-      o_hp[2][PPO_MAX_LAYERS], o_dg16[2][PPO_MAX_LAYERS], o_hp16[2][PPO_MAX_LAYERS];
+      o_hp[2][PPO_MAX_LAYERS], o_dg16[2][PPO_MAX_LAYERS], o_hp16[2][PPO_MAX_LAYERS],
+      o_whht16[2][PPO_MAX_LAYERS][2];
   for (int z = 0; z < 2; ++z)
     for (int l = 0; l < x->net[z].layers; ++l) {
       o_g[z][l] = take(R * W * 8 * H);
       o_c[z][l] = take(R * W * 2 * H);
       o_y[z][l] = take(R * W * 2 * H);
       o_hp[z][l] = take(R * W * 2 * H);
-      o_dg16[z][l] = take(R * W * 4 * H);
+      o_dg16[z][l] = take((R + 128) * W * 4 * H);
+      for (int d = 0; d < 2; ++d) o_whht16[z][l][d] = take(2LL * H * H);
       o_hp16[z][l] = take(R * W * H);
     }
   const int64_t o_gh = take(R * 8 * H), o_dhrec = take(R * 2 * H), o_dcarry = take(R * 2 * H);
@@ -1228,6 +1270,8 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
       x->y[z][l] = w + o_y[z][l];
       x->hp[z][l] = w + o_hp[z][l];
       x->dg16[z][l] = reinterpret_cast<__bf16 *>(w + o_dg16[z][l]);
+      for (int d = 0; d < 2; ++d)
+        x->whht16[z][l][d] = reinterpret_cast<__bf16 *>(w + o_whht16[z][l][d]);
       x->hp16[z][l] = reinterpret_cast<__bf16 *>(w + o_hp16[z][l]);
     }
   x->gh = w + o_gh;
@@ -1312,12 +1356,13 @@ extern "C" int ppo_lstm_set_precision(ppo_lstm_ctx *x, int prec) {
 
 // bf16 mode: the LSTM GEMMs read a bf16 copy of the parameters made once per call (the rounding
 // their staging applied to the f32 masters per workgroup) and layer 0's W_ih as padded images for
-// the wide projection; x->w16 is cleared again when the caller's W16Scope ends
+// the wide projection (bwd: and the W_hh^T images of the recurrent-gradient GEMM); x->w16 is
+// cleared again when the caller's W16Scope ends
 struct W16Scope {
   ppo_lstm_ctx *x;
   ~W16Scope() { x->w16 = nullptr; }
 };
-int prep_w16(ppo_lstm_ctx *x, hipStream_t st) {
+int prep_w16(ppo_lstm_ctx *x, hipStream_t st, bool bwd) {
   if (x->prec != PPO_PREC_BF16) return 0;
   const int H = x->cfg.latent, O = x->cfg.obs_dim;
   launch_k(TimRec{KC_GATHER, "lstm_params_bf16_kernel", 0.0, 6.0 * x->total},
@@ -1338,6 +1383,18 @@ int prep_w16(ppo_lstm_ctx *x, hipStream_t st) {
   launch_k(TimRec{KC_GATHER, "lstm_wih_image_kernel", 0.0, 4.0 * 4 * H * O * 6.0},
            lstm_wih_image_kernel, dim3(ceil_div(4LL * 4 * H * O, 256)), dim3(256), 0, st, wi);
   PPO_LAUNCHED();
+  if (!bwd || H % 64 != 0) return 0;
+  WhhTImages wt{};
+  for (int z = 0; z < 2; ++z)
+    for (int l = 0; l < x->net[z].layers; ++l)
+      for (int d = 0; d < 2; ++d, ++wt.n) {
+        wt.src[wt.n] = x->params + x->net[z].l[l].w_hh[d];
+        wt.dst[wt.n] = x->whht16[z][l][d];
+      }
+  wt.h = H;
+  launch_k(TimRec{KC_GATHER, "lstm_whh_t_image_kernel", 0.0, 0.0}, lstm_whh_t_image_kernel,
+           dim3(ceil_div(wt.n * 4LL * H * H, 256)), dim3(256), 0, st, wt);
+  PPO_LAUNCHED();
   return 0;
 }
 
@@ -1348,7 +1405,7 @@ int prep_w16(ppo_lstm_ctx *x, hipStream_t st) {
 int forward_rollout(ppo_lstm_ctx *x, const float *state_d, int n, hipStream_t st) {
   if (x->prec != PPO_PREC_BF16) return forward_all(x, state_d, nullptr, n, st);
   W16Scope w16_scope{x};
-  if (int rc = prep_w16(x, st)) return rc;
+  if (int rc = prep_w16(x, st, false)) return rc;
   const int din = x->cfg.window * x->cfg.obs_dim;
   launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
            dim3(ceil_div(static_cast<int64_t>(n) * din, 256)), dim3(256), 0, st, state_d,
@@ -1441,7 +1498,7 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
   const int din = W * O;
   W16Scope w16_scope{x};
-  if (int rc = prep_w16(x, st)) return rc;
+  if (int rc = prep_w16(x, st, true)) return rc;
   // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
   // (rows of O values at a stride of ldx16, a multiple of 64: the wide GEMM's k-tiles)
   const __bf16 *x16 = x->prec == PPO_PREC_BF16 ? x->x16 : nullptr;

@@ -332,6 +332,29 @@ def test_fused_forward_step_bitwise_equals_layered(gpu):
     assert torch.equal(out[True][1][1], out[False][1][1])
 
 
+@pytest.mark.parametrize("b", [200, 4096 + 72])
+def test_wide_recurrent_gradient_bitwise_equals_layered(gpu, monkeypatch, b):
+    """bf16 mode: the backward steps' recurrent gradient dh_rec = dG W_hh on the wide path's
+    LDS-DMA GEMM (W_hh^T images) reproduces gemm_bf16_kernel's bitwise -- the whole minibatch
+    gradient and loss on the main.py network, both row tiles (<= 4096 rows and above) with a
+    partial last tile."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=33)
+    agent.engine.set_precision("bf16")
+    gen = torch.Generator().manual_seed(8)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    old_logp = torch.randn(b, generator=gen) - 10.0
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PPO_LSTM_DHREC", mode)
+        out[mode] = _grad(agent, x, actions, old_logp, adv, vt)
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
+
+
 @pytest.mark.parametrize("kw", [{"latent": 8, "window": 3, "hidden": (32, 32)},
                                 {"latent": 12, "window": 2, "hidden": (24, 16), "extractor_layers": 2,
                                  "activation": "tanh"}])
