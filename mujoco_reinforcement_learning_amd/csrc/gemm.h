@@ -175,6 +175,18 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[TM][TN], const
         const int col = n0 + (wn * TN + j) * 32 + (lane & 31);
         float bias = 0.f;
         if (EPI == EPI_FWD && P.bias && (!checked || col < N)) bias = P.bias[col];
+        // DX: the block's 16 aux loads first, then the stores -- c may alias aux, so a load after
+        // a store waited for it (one memory round trip per element); each lane reads exactly
+        // the elements it writes, so the order change is safe under aliasing
+        float ax[16];
+        if (EPI == EPI_DX) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            ax[r] = (!checked || (row < M && col < N)) ? P.aux[static_cast<int64_t>(row) * P.ldc + col]
+                                                       : 0.f;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -182,7 +194,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[TM][TN], const
             const int64_t off = static_cast<int64_t>(row) * P.ldc + col;
             const float v = acc[i][j][r];
             if (EPI == EPI_FWD) cbase[off] = act_forward(P.bias ? v + bias : v, gb.act);
-            else if (EPI == EPI_DX) cbase[off] = act_backward(v, P.aux[off], gb.act);
+            else if (EPI == EPI_DX) cbase[off] = act_backward(v, ax[r], gb.act);
             else cbase[off] = v;
           }
         }
