@@ -130,10 +130,16 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
   *reinterpret_cast<float4 *>(g + 3 * H + j) = make_float4(og[0], og[1], og[2], og[3]);
   *reinterpret_cast<float4 *>(q.c + o) = make_float4(c[0], c[1], c[2], c[3]);
   *reinterpret_cast<float4 *>(q.y + o) = make_float4(h[0], h[1], h[2], h[3]);
-  if (q.hp16)
+  if (q.hp16) {
     *reinterpret_cast<uint2 *>(q.hp16 + o) =
         make_uint2(pack_bf16x2(hp4.x, hp4.y), pack_bf16x2(hp4.z, hp4.w));
-  else
+    // the next step's h_prev row as well: the W16 step kernel stages its A operand from it
+    if (q.s + 1 < W) {
+      const int tn = d == 0 ? t + 1 : t - 1;
+      *reinterpret_cast<uint2 *>(q.hp16 + (b * W + tn) * (2 * H) + d * H + j) =
+          make_uint2(pack_bf16x2(h[0], h[1]), pack_bf16x2(h[2], h[3]));
+    }
+  } else
     *reinterpret_cast<float4 *>(q.hp + o) = hp4;
   if (q.feat_mode == 1 || (q.feat_mode == 2 && t == W - 1)) {
     float *f = q.feat_mode == 1 ? q.feat + o : q.feat + b * (2 * H) + d * H + j;
@@ -173,20 +179,24 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
   const int t = d == 0 ? c.s : W - 1 - c.s;
   const int tp = d == 0 ? t - 1 : t + 1;
   const float *arow = c.y + static_cast<int64_t>(tp) * 2 * H + d * H;  // + row * W * 2H + k
+  // W16: h_prev as bf16 from hp16's row t (the previous step wrote it there: bf16(h(tp)), the
+  // rounding the f32 staging applies)
+  const __bf16 *arow16 = W16 ? c.hp16 + static_cast<int64_t>(t) * 2 * H + d * H : nullptr;
   const int64_t lda = static_cast<int64_t>(W) * 2 * H;
   const float *wb = q.whh[d];
 
   // staging: A 64 rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63) x
   // 32 k (8 float4 per thread); rows past b load row b-1 (clamped, results discarded)
   float4 va[2], vb[8];
-  uint2 vb16[8];
+  uint2 va16[2], vb16[8];
   const __bf16 *wb16 = W16 ? q.whh16[d] : nullptr;
   auto gload = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
       const int row = min(r0 + rr, c.b - 1);
-      va[u] = *reinterpret_cast<const float4 *>(arow + row * lda + k0 + kk);
+      if constexpr (W16) va16[u] = *reinterpret_cast<const uint2 *>(arow16 + row * lda + k0 + kk);
+      else va[u] = *reinterpret_cast<const float4 *>(arow + row * lda + k0 + kk);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
     for (int u = 0; u < 2; ++u) {
       const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
       *reinterpret_cast<uint2 *>(ai + rr * AP + kk) =
-          make_uint2(pack_bf16x2(va[u].x, va[u].y), pack_bf16x2(va[u].z, va[u].w));
+          W16 ? va16[u] : make_uint2(pack_bf16x2(va[u].x, va[u].y), pack_bf16x2(va[u].z, va[u].w));
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -262,7 +272,7 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
       for (int k = 0; k < 4; ++k) gx[u][k] = g[k * H + j];
       const int64_t op = (bc * W + tp) * (2 * H) + d * H + j;
       cpv[u] = c.c[op];
-      hpv[u] = c.y[op];
+      if constexpr (!W16) hpv[u] = c.y[op];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -284,8 +294,17 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
       g[3 * H + j] = og;
       c.c[o] = cn;
       c.y[o] = h;
-      if (c.hp16) c.hp16[o] = static_cast<__bf16>(hpv[u]);
-      else c.hp[o] = hpv[u];
+      if constexpr (W16) {
+        // row t's h_prev is already there; h goes to the next step's row
+        if (c.s + 1 < W) {
+          const int tn = d == 0 ? t + 1 : t - 1;
+          c.hp16[(bb * W + tn) * (2 * H) + d * H + j] = static_cast<__bf16>(h);
+        }
+      } else if (c.hp16) {
+        c.hp16[o] = static_cast<__bf16>(hpv[u]);
+      } else {
+        c.hp[o] = hpv[u];
+      }
       if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
       else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
     }
@@ -446,6 +465,27 @@ __global__ void lstm_gather_rows_kernel(const float *__restrict__ states,
     xg16[rw * ld16 + within % o] = static_cast<__bf16>(v);
   } else {
     xg[i] = v;
+  }
+}
+
+// The same gather four values a thread (O % 4 == 0: a float4 never straddles a step's O values,
+// and the bf16 rows stay 8-B aligned)
+__global__ void lstm_gather_rows4_kernel(const float *__restrict__ states,
+                                         const int32_t *__restrict__ rows, int b, int din,
+                                         float *__restrict__ xg, __bf16 *__restrict__ xg16, int o,
+                                         int ld16) {
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (i >= static_cast<int64_t>(b) * din) return;
+  const int64_t j = i / din;
+  const int64_t within = i - j * din;
+  const float4 v = *reinterpret_cast<const float4 *>(
+      states + (rows ? static_cast<int64_t>(rows[j]) : j) * din + within);
+  if (xg16) {
+    const int64_t rw = j * (din / o) + within / o;
+    *reinterpret_cast<uint2 *>(xg16 + rw * ld16 + within % o) =
+        make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  } else {
+    *reinterpret_cast<float4 *>(xg + i) = v;
   }
 }
 
@@ -835,8 +875,10 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         if (tim_active()) {
           rec.flops = 2.0 * 2 * b * 4.0 * H * H;
           // W_hh and h_prev once, Gx / c_prev / h_prev in, gates / c / h out (f32), h_prev out
-          // (bf16 in bf16 mode)
-          rec.bytes = 4.0 * 2 * 4.0 * H * H + 2.0 * b * H * (4.0 * (1 + 4 + 2 + 4 + 2) + (b16 ? 2.0 : 4.0));
+          // (bf16 in bf16 mode); W16: W_hh and the staged h_prev in bf16, no f32 h_prev read
+          rec.bytes = x->w16 ? 2.0 * 2 * 4.0 * H * H + 2.0 * b * H * (2.0 + 4.0 * (4 + 1 + 4 + 2) + 2.0)
+                             : 4.0 * 2 * 4.0 * H * H +
+                                   2.0 * b * H * (4.0 * (1 + 4 + 2 + 4 + 2) + (b16 ? 2.0 : 4.0));
         }
         const dim3 grid(ceil_div(b, kStepRows), H / kStepUnits, 2);
         if (x->w16) {
@@ -1398,6 +1440,24 @@ int prep_w16(ppo_lstm_ctx *x, hipStream_t st, bool bwd) {
   return 0;
 }
 
+// rows of [W*O] state windows -> xg (f32) or xg16 (bf16, padded stride); rows == nullptr: in order
+int gather_rows(ppo_lstm_ctx *x, const float *states, const int32_t *rows, int b, float *xg,
+                __bf16 *xg16, hipStream_t st) {
+  const int O = x->cfg.obs_dim, din = x->cfg.window * O;
+  const int64_t n = static_cast<int64_t>(b) * din;
+  if (O % 4 == 0 && reinterpret_cast<uintptr_t>(states) % 16 == 0) {
+    launch_k(TimRec{KC_GATHER, "lstm_gather_rows4_kernel", 0.0, 0.0}, lstm_gather_rows4_kernel,
+             dim3(ceil_div(n / 4, 256)), dim3(256), 0, st, states, rows, b, din, xg, xg16, O,
+             x->ldx16);
+  } else {
+    launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
+             dim3(ceil_div(n, 256)), dim3(256), 0, st, states, rows, b, din, xg, xg16, O,
+             x->ldx16);
+  }
+  PPO_LAUNCHED();
+  return 0;
+}
+
 // The rollout's forward (policy step / forward) in bf16 mode on the minibatch step's operands:
 // the parameter images, the window rows as padded bf16 (the gather kernel, rows in order), the
 // wide projection and the W16 step kernels -- the same arithmetic as the layered f32-staged form
@@ -1406,12 +1466,7 @@ int forward_rollout(ppo_lstm_ctx *x, const float *state_d, int n, hipStream_t st
   if (x->prec != PPO_PREC_BF16) return forward_all(x, state_d, nullptr, n, st);
   W16Scope w16_scope{x};
   if (int rc = prep_w16(x, st, false)) return rc;
-  const int din = x->cfg.window * x->cfg.obs_dim;
-  launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
-           dim3(ceil_div(static_cast<int64_t>(n) * din, 256)), dim3(256), 0, st, state_d,
-           static_cast<const int32_t *>(nullptr), n, din, static_cast<float *>(nullptr), x->x16,
-           x->cfg.obs_dim, x->ldx16);
-  PPO_LAUNCHED();
+  if (int rc = gather_rows(x, state_d, nullptr, n, nullptr, x->x16, st)) return rc;
   return forward_all(x, state_d, x->x16, n, st);
 }
 
@@ -1495,17 +1550,13 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
   TimingScope ts(x);
   hipStream_t st = as_stream(stream);
   const ppo_lstm_cfg &c = x->cfg;
-  const int W = c.window, O = c.obs_dim, A = c.act_dim, H = c.latent, nl = c.n_hidden;
-  const int din = W * O;
+  const int W = c.window, A = c.act_dim, H = c.latent, nl = c.n_hidden;
   W16Scope w16_scope{x};
   if (int rc = prep_w16(x, st, true)) return rc;
   // bf16 mode: the gathered rows only feed GEMMs, so they are staged as bf16
   // (rows of O values at a stride of ldx16, a multiple of 64: the wide GEMM's k-tiles)
   const __bf16 *x16 = x->prec == PPO_PREC_BF16 ? x->x16 : nullptr;
-  launch_k(TimRec{KC_GATHER, "lstm_gather_rows_kernel", 0.0, 0.0}, lstm_gather_rows_kernel,
-           dim3(ceil_div(static_cast<int64_t>(b) * din, 256)), dim3(256), 0, st, states_d, rows_d,
-           b, din, x->x, const_cast<__bf16 *>(x16), O, x->ldx16);
-  PPO_LAUNCHED();
+  if (int rc = gather_rows(x, states_d, rows_d, b, x->x, const_cast<__bf16 *>(x16), st)) return rc;
   if (int rc = forward_all(x, x->x, x16, b, st)) return rc;
   HeadArgs h{};
   h.mean = x->act_mu[nl];
