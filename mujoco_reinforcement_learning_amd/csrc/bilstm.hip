@@ -167,7 +167,7 @@ typedef __bf16 lstm_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
 
 template <bool W16>
-__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
+__device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   constexpr int AP = kStepBK + 8;                 // bf16 image row pitch (16 B of padding)
   constexpr int AIMG = kStepRows * AP, BIMG = 4 * kStepUnits * AP;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * (AIMG + BIMG)];
@@ -309,6 +309,16 @@ __global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
       else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
     }
   }
+}
+
+template <bool W16>
+__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
+  lstm_step_fwd_body<W16>(q);
+}
+// the rollout's launches (1,024-row windows): the same body under its own name, so the traffic /
+// roofline rows of the minibatch kernel stay per-launch comparable
+__global__ __launch_bounds__(256) void lstm_step_fwd_rollout_kernel(StepArgs q) {
+  lstm_step_fwd_body<true>(q);
 }
 
 struct CellBwdArgs {
@@ -690,6 +700,7 @@ struct ppo_lstm_ctx {
   float *row_part;                   // [rows][3]
   int maxw;
   int fused_step;  // bf16 forward steps as lstm_step_fwd_kernel (ppo_lstm_fused_step)
+  int rollout;     // inside forward_rollout: the step launches take the rollout kernel
   Timing tim;
 };
 
@@ -870,7 +881,9 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         a.whh[0] = P + L.w_hh[0];
         a.whh[1] = P + L.w_hh[1];
         // the launched instantiation's name (rocprof's, for the traffic table)
-        TimRec rec{KC_LSTM, x->w16 ? "lstm_step_fwd_kernel<true>" : "lstm_step_fwd_kernel<false>",
+        TimRec rec{KC_LSTM,
+                   x->w16 ? (x->rollout ? "lstm_step_fwd_rollout_kernel" : "lstm_step_fwd_kernel<true>")
+                          : "lstm_step_fwd_kernel<false>",
                    0.0, 0.0};
         if (tim_active()) {
           rec.flops = 2.0 * 2 * b * 4.0 * H * H;
@@ -884,7 +897,8 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         if (x->w16) {
           a.whh16[0] = x->w16 + L.w_hh[0];
           a.whh16[1] = x->w16 + L.w_hh[1];
-          launch_k(rec, lstm_step_fwd_kernel<true>, grid, dim3(256), 0, st, a);
+          if (x->rollout) launch_k(rec, lstm_step_fwd_rollout_kernel, grid, dim3(256), 0, st, a);
+          else launch_k(rec, lstm_step_fwd_kernel<true>, grid, dim3(256), 0, st, a);
         } else {
           launch_k(rec, lstm_step_fwd_kernel<false>, grid, dim3(256), 0, st, a);
         }
@@ -1229,6 +1243,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   x->prec = PPO_PREC_F32;
   x->ent_log_share = 1.f;
   x->fused_step = g_lstm_fused_step;
+  x->rollout = 0;
   x->splits = g_lstm_splits;
   const int H = c.latent, W = c.window, O = c.obs_dim, A = c.act_dim;
   int64_t off = 0;
@@ -1465,6 +1480,11 @@ int gather_rows(ppo_lstm_ctx *x, const float *states, const int32_t *rows, int b
 int forward_rollout(ppo_lstm_ctx *x, const float *state_d, int n, hipStream_t st) {
   if (x->prec != PPO_PREC_BF16) return forward_all(x, state_d, nullptr, n, st);
   W16Scope w16_scope{x};
+  struct RolloutScope {
+    ppo_lstm_ctx *x;
+    ~RolloutScope() { x->rollout = 0; }
+  } rollout_scope{x};
+  x->rollout = 1;
   if (int rc = prep_w16(x, st, false)) return rc;
   if (int rc = gather_rows(x, state_d, nullptr, n, nullptr, x->x16, st)) return rc;
   return forward_all(x, state_d, x->x16, n, st);
