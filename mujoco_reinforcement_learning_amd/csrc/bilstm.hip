@@ -593,11 +593,12 @@ __global__ __launch_bounds__(256) void lstm_update_head_kernel(HeadArgs q) {
   const int A = q.a;
   const int64_t src = q.rows[n];
   float lp = 0.f, ent = 0.f;
-  float mu[kMaxA], sd[kMaxA], dd[kMaxA];
+  float mu[kMaxA], sd[kMaxA], dd[kMaxA], uv[kMaxA];
   for (int k = 0; k < A; ++k) {
     const int64_t idx = static_cast<int64_t>(n) * A + k;
     mu[k] = q.mean[idx];
-    sd[k] = 0.2f * expf(q.u[idx]);
+    uv[k] = q.u[idx];  // kept: a reload behind the dz stores below waited for each of them
+    sd[k] = 0.2f * expf(uv[k]);
     dd[k] = q.actions[src * A + k] - mu[k];
     const float ls = logf(sd[k]);
     lp += (((-(dd[k] * dd[k])) / (2.f * (sd[k] * sd[k]))) - ls) - kLogSqrt2Pi;
@@ -623,7 +624,7 @@ __global__ __launch_bounds__(256) void lstm_update_head_kernel(HeadArgs q) {
     const float dstd = dlogp * ((dd[k] * dd[k]) / (var * sd[k]) - 1.f / sd[k]) -
                        q.ent_coef * q.inv_ba / sd[k];
     const float du = dstd * sd[k];  // std = 0.2 * exp(u)
-    const float uu = q.u[idx];
+    const float uu = uv[k];
     q.dzm[idx] = dmu * (1.f - mu[k] * mu[k]);
     q.dzs[idx] = du * (1.f - uu * uu);
   }
