@@ -374,14 +374,21 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, timeout: float = None) -> int:
     """``bench.py --gpus N`` started as one plain process: start N rank processes of this same
     command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their env,
     as torch.distributed.run would set them), forward rank 0's JSON line, and return non-zero if
     any rank fails.  This parent never touches the GPU (no HIP call before or after the
     children start), and when one rank dies the others are terminated by their own PIDs rather
-    than left waiting in a collective."""
+    than left waiting in a collective.
+
+    Wall-clock bound (PPO_BENCH_RANK_TIMEOUT seconds, default 1200): a rank blocked inside a
+    collective never exits on its own, so on expiry every rank still alive is terminated (then
+    killed), ONE JSON line with ``error`` and the ranks still alive is printed, and the exit
+    status is 124.  Nothing is re-executed."""
     import subprocess
+    if timeout is None:
+        timeout = float(os.environ.get("PPO_BENCH_RANK_TIMEOUT", "1200"))
     port = str(_free_port())
     procs = []
     for r in range(n):
@@ -394,6 +401,8 @@ def launch_ranks(n: int) -> int:
     reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
     reader.start()
     rcs = [None] * n
+    deadline = time.monotonic() + timeout
+    timed_out = None
     # reap in completion order; after the first failure terminate the rest
     while any(rc is None for rc in rcs):
         for i, p in enumerate(procs):
@@ -403,10 +412,31 @@ def launch_ranks(n: int) -> int:
                     for q in procs:
                         if q.poll() is None:
                             q.terminate()
+        if timed_out is None and time.monotonic() > deadline and any(rc is None for rc in rcs):
+            timed_out = [i for i, rc in enumerate(rcs) if rc is None]
+            _progress(f"ranks {timed_out} still running after {timeout:.0f} s: terminating them")
+            for i in timed_out:
+                procs[i].terminate()
+            for i in timed_out:
+                try:
+                    procs[i].wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    procs[i].kill()
+                    procs[i].wait()
+                rcs[i] = procs[i].returncode
         time.sleep(0.05)
     reader.join(timeout=10)
     # rank 0's JSON line to stdout; library chatter (e.g. gloo's connection lines) to stderr
-    for ln in b"".join(chunks).decode().splitlines():
+    out = b"".join(chunks).decode(errors="replace").splitlines()
+    if timed_out is not None:
+        for ln in out:
+            print(ln, file=sys.stderr)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": n,
+                          "error": f"rank processes still running after {timeout:.0f} s "
+                                   f"(PPO_BENCH_RANK_TIMEOUT); terminated",
+                          "alive_ranks": timed_out, "exit_codes": rcs}), flush=True)
+        return 124
+    for ln in out:
         print(ln, file=sys.stdout if ln.startswith("{") else sys.stderr)
     sys.stdout.flush()
     bad = [(i, rc) for i, rc in enumerate(rcs) if rc != 0]
@@ -420,17 +450,59 @@ def launch_check(args, world, rank) -> None:
     """PPO_BENCH_LAUNCH_CHECK=1 (CPU tests of the launcher): the rank plumbing of main() -- gloo
     rendezvous, barrier-bracketed timing, max over ranks, rank 0's JSON line -- with no GPU work.
     PPO_BENCH_LAUNCH_CHECK_FAIL_RANK=r makes rank r exit with status 3 before the rendezvous (the
-    launcher must then stop the other ranks and fail)."""
+    launcher must then stop the other ranks and fail); PPO_BENCH_LAUNCH_CHECK_HANG_RANK=r makes
+    rank r block after the rendezvous, so the others wait in the next collective (the launcher's
+    wall-clock bound must end the run); PPO_BENCH_LAUNCH_CHECK_CAPTURE_FAIL_RANK=r runs the
+    update-loop capture agreement (DataParallel.capture_agreed) with a stand-in communicator whose
+    capture fails on rank r only, then the exchanges of the eager fallback, and reports the
+    resulting ``comm`` and whether the ranks' results agree bitwise."""
+    from mujoco_reinforcement_learning_amd.distributed import DataParallel
     if os.environ.get("PPO_BENCH_LAUNCH_CHECK_FAIL_RANK") == str(rank):
         sys.exit(3)
     torch.distributed.init_process_group("gloo")
     t0 = time.perf_counter()
     torch.distributed.barrier()
+    if os.environ.get("PPO_BENCH_LAUNCH_CHECK_HANG_RANK") == str(rank):
+        while True:
+            time.sleep(1)
     tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    line = {"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "launch_check": True}
+    fail_rank = os.environ.get("PPO_BENCH_LAUNCH_CHECK_CAPTURE_FAIL_RANK")
+    if fail_rank is not None:
+        dp = DataParallel()
+
+        class _StandIn:  # the native communicator's interface over the gloo group
+            retired = False
+
+            def retire(self):
+                self.retired = True
+
+            def allreduce(self, t):
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
+
+        comm = dp.comm = _StandIn()
+
+        def capture():
+            if str(rank) == fail_rank:
+                raise RuntimeError(f"operation not permitted when stream is capturing (rank {rank})")
+
+        reason = dp.capture_agreed(capture)
+        # the eager fallback's exchanges: three all-reduces of rank-dependent gradients
+        g = torch.arange(8, dtype=torch.float32) * (rank + 1) / 7.0
+        for _ in range(3):
+            dp.allreduce_grad(g)
+            g.mul_(0.5)
+        gathered = [torch.empty_like(g) for _ in range(world)]
+        torch.distributed.all_gather(gathered, g)
+        line["capture"] = {"fallback": reason is not None, "reason": reason,
+                           "native_retired": comm.retired,
+                           "replicas_bitwise_equal": all(torch.equal(gathered[0], x)
+                                                         for x in gathered)}
+        line["comm"] = dp.comm_info()
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "launch_check": True}), flush=True)
+        print(json.dumps(line), flush=True)
     torch.distributed.destroy_process_group()
 
 
@@ -627,6 +699,13 @@ def main():
     elapsed = time_iterations(algo, args.steps, args.warmup, world, dev)
     if rank == 0:
         _progress(f"timed: {1000 * elapsed / args.steps:.2f} ms per iteration")
+    comm = None
+    if hasattr(algo, "dp"):
+        # the exchange as it ran: the native communicator's own rank count (ppo_comm_query), the
+        # process group's backend, and whether the update loop was replayed as one hipGraph
+        comm = dict(algo.dp.comm_info(),
+                    graph_captured=getattr(algo, "_tg_graph", None) is not None,
+                    capture_failed=bool(getattr(algo, "_tg_capture_failed", False)))
     classes, kernels = {}, {}
     if not args.no_timing:
         # Per-kernel durations: HIP event pairs on each dispatch packet, over --timing-iters
@@ -660,7 +739,8 @@ def main():
                        "env": ("device (synthetic dynamics on the GPU)" if args.env == "device"
                                else f"host pool ({args.env_workers} worker processes, page-locked "
                                     "device-mapped shared memory, ppo_host_rollout)"),
-                       "parallelism": parallelism_label(world)}}
+                       "parallelism": parallelism_label(world)},
+            "comm": comm}
     if kernels:
         traffic = load_traffic(args.traffic, traffic_workload(args))
         name, c = max(kernels.items(), key=lambda kv: kv[1]["ms"])

@@ -515,6 +515,8 @@ int ppo_synthetic_pixel_step(uint32_t seed, int t, const float *action_d, int n,
  *   ppo_comm_create      every rank, with the same id, its rank and its device (collective call)
  *   ppo_comm_allreduce   buf_d[0, n) f32 := SUM over ranks, in place, ordered on `stream`
  *   ppo_comm_check       the communicator's asynchronous error state (0 = healthy)
+ *   ppo_comm_query       what RCCL itself reports: rank count (ncclCommCount), this rank
+ *                        (ncclCommUserRank) and the device the communicator was built on
  *   ppo_ctx_set_comm / ppo_allreduce_grads   SURVEY.md s8(b)'s ctx-owned form: the ctx keeps the
  *                        communicator (not owned: ppo_comm_destroy after the ctx) and
  *                        ppo_allreduce_grads(ctx, flat, n, stream) sums n <= ppo_param_count(ctx, -1)
@@ -527,6 +529,7 @@ int ppo_comm_create(const uint8_t *id, int nranks, int rank, int device, ppo_com
 int ppo_comm_destroy(ppo_comm *comm);
 int ppo_comm_allreduce(ppo_comm *comm, float *buf_d, int64_t n, void *stream);
 int ppo_comm_check(ppo_comm *comm);
+int ppo_comm_query(ppo_comm *comm, int *nranks_out, int *rank_out, int *device_out);
 int ppo_ctx_set_comm(ppo_ctx *ctx, ppo_comm *comm);
 int ppo_allreduce_grads(ppo_ctx *ctx, float *flat_d, int64_t n, void *stream);
 

@@ -216,6 +216,7 @@ _SIGNATURES = {
     "ppo_comm_destroy": (c_int, [c_void_p]),
     "ppo_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ppo_comm_check": (c_int, [c_void_p]),
+    "ppo_comm_query": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "ppo_ctx_set_comm": (c_int, [c_void_p, c_void_p]),
     "ppo_allreduce_grads": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ppo_ctx_loss_entropy_share": (c_int, [c_void_p, c_float]),

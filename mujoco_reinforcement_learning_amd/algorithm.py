@@ -431,16 +431,20 @@ class PPOEngine:
             # the native RCCL all-reduce (DataParallel.comm) is recorded like a kernel; its proxy
             # threads keep running during capture, so only this thread's calls are checked
             mode = "thread_local" if self.dp.comm is not None else "global"
-            try:
+
+            def capture():
                 with torch.cuda.graph(g, capture_error_mode=mode):
                     body()
-            except RuntimeError as err:
-                if self.dp.comm is None:
-                    raise
-                # a collective the RCCL build cannot record: nothing ran during the capture and
-                # body() depends on no host state it changes, so the step runs eagerly from here on
+
+            # every rank agrees on the outcome (DataParallel.capture_agreed): if the capture
+            # failed on ANY rank (a collective the RCCL build cannot record), all ranks leave the
+            # native communicator together and run this and every later update loop eagerly over
+            # torch.distributed -- the same collective sequence everywhere.  Nothing ran during
+            # the capture and body() depends on no host state it changes.
+            reason = self.dp.capture_agreed(capture, eng)
+            if reason is not None:
                 warnings.warn(f"capturing the data-parallel step with the native RCCL all-reduce "
-                              f"failed ({err}); the update loop runs eagerly")
+                              f"failed ({reason}); the update loop runs eagerly on every rank")
                 self._tg_capture_failed = True
                 torch.cuda.synchronize(dev)
                 body()

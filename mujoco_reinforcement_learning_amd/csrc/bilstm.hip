@@ -828,8 +828,14 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
     GemmProblem p[2] = {};
     for (int d = 0; d < 2; ++d) {
       p[d].a = in;
-      // (bf16 minibatch rows go through the wide GEMM below; this form reads f32 rows)
       p[d].lda = L.in;
+      if (l == 0 && xin16) {
+        // bf16 mode: the minibatch gather writes only the bf16 rows (xin holds no data then), so
+        // the layered fallback below reads those too -- the same RNE-rounded operand the f32-staged
+        // form would make, through the bf16-source FWD variant
+        p[d].a16 = xin16;
+        p[d].lda = x->ldx16;
+      }
       p[d].b = P + L.w_ih[d];
       p[d].ldb = L.in;
       p[d].c = x->g[z][l] + d * 4 * H;

@@ -44,6 +44,8 @@ struct RcclApi {
   ncclResult_t (*async_error)(ncclComm_t, ncclResult_t *) = nullptr;
   const char *(*error_string)(ncclResult_t) = nullptr;
   ncclResult_t (*get_version)(int *) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int *) = nullptr;
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int *) = nullptr;
   char err[256] = {0};
 };
 
@@ -83,6 +85,8 @@ void rccl_load() {
   PPO_SYM(async_error, "ncclCommGetAsyncError")
   PPO_SYM(error_string, "ncclGetErrorString")
   PPO_SYM(get_version, "ncclGetVersion")
+  PPO_SYM(comm_count, "ncclCommCount")
+  PPO_SYM(comm_user_rank, "ncclCommUserRank")
 #undef PPO_SYM
 }
 
@@ -180,6 +184,20 @@ extern "C" int ppo_comm_check(ppo_comm *c) {
     ppo::set_error("RCCL asynchronous error: %s", api->error_string(async));
     return PPO_EHIP;
   }
+  return 0;
+}
+
+// The communicator's own view (not the arguments it was created with): RCCL's rank count and
+// this rank, plus the device -- what the bench line reports as "comm".
+extern "C" int ppo_comm_query(ppo_comm *c, int *nranks_out, int *rank_out, int *device_out) {
+  PPO_REQUIRE(c != nullptr, "ppo_comm_query: null comm");
+  PPO_RCCL_API(api);
+  int n = 0, r = -1;
+  PPO_NCCL_TRY(api, api->comm_count(c->comm, &n));
+  PPO_NCCL_TRY(api, api->comm_user_rank(c->comm, &r));
+  if (nranks_out) *nranks_out = n;
+  if (rank_out) *rank_out = r;
+  if (device_out) *device_out = c->device;
   return 0;
 }
 

@@ -780,7 +780,11 @@ static int fused_prep(const ppo_ctx *ctx, const FusedArgs &q, hipStream_t st) {
 
 // The gathered-copy record (ctx.h fg_rows): a caller's PPO_STAGED_ROWS_GATHERED is a promise
 // about stream order that nothing on the device checks, so the host keeps which rows the last
-// staged gather wrote and gathers again when the promise names other rows.
+// staged gather wrote and gathers again when the promise names other rows.  The check is POINTER
+// identity (the index buffer's address and count), not content: a caller that rewrites the same
+// index buffer in place (e.g. a fresh permutation into one buffer) must not pass
+// PPO_STAGED_ROWS_GATHERED for it.  A gather is recorded only once its launch was issued
+// successfully; a failed entry point clears the record.
 static bool gathered_holds(const ppo_ctx *ctx, const int32_t *rows_d, int b) {
   return rows_d != nullptr && ctx->fg_rows == rows_d && ctx->fg_b == b;
 }
@@ -1351,14 +1355,18 @@ extern "C" int ppo_adam_pack_gather(ppo_ctx *ctx, const float *g_d, float *m_d, 
                                                0.f, true, false).direct;
   t.b = direct ? 0 : next_b;
   t.reduce = false;
-  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
   ReduceArgs r{};
   r.total = ctx->total_params;
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_ADAM, "step_tail_kernel", 0.0,
                    28.0 * P + 2.0 * 2.0 * H * (t.a.din + 2.0 * H) +
                        static_cast<double>(t.b) * (4.0 + 2.0 * kRecordBytes)};
-  return step_tail_launch(r, t, rec, as_stream(stream));
+  if (int rc = step_tail_launch(r, t, rec, as_stream(stream))) {
+    note_gathered(ctx, nullptr, 0);
+    return rc;
+  }
+  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
+  return 0;
 }
 
 extern "C" int ppo_gather_staged_rows(ppo_ctx *ctx, const int32_t *rows_d, int b, void *stream) {
@@ -1434,13 +1442,20 @@ extern "C" int ppo_update_step_staged(ppo_ctx *ctx, const int32_t *rows_d, int b
   t.srow = ctx->fsrow;
   t.b = q.direct ? 0 : next_b;  // direct: the next fused launch reads its rows itself
   t.reduce = true;
-  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
-  if (int rc = fused_forward_backward(ctx, q, st)) return rc;
+  if (int rc = fused_forward_backward(ctx, q, st)) {
+    note_gathered(ctx, nullptr, 0);
+    return rc;
+  }
   const double P = static_cast<double>(ctx->total_params), H = ctx->fused_hidden;
   const TimRec rec{KC_REDUCE, "step_tail_kernel", static_cast<double>(q.G) * P,
                    4.0 * (q.G + 1.0) * P + 24.0 * P + 2.0 * 2.0 * H * (q.din + 2.0 * H) +
                        static_cast<double>(t.b) * (4.0 + 2.0 * kRecordBytes)};
-  return step_tail_launch(r, t, rec, st);
+  if (int rc = step_tail_launch(r, t, rec, st)) {
+    note_gathered(ctx, nullptr, 0);
+    return rc;
+  }
+  if (t.b > 0) note_gathered(ctx, next_rows_d, t.b);
+  return 0;
 }
 
 extern "C" int ppo_observe_act(ppo_ctx *ctx, double *window_d, const double *obs_d,

@@ -39,36 +39,55 @@ def shard_range(n_global: int, world: int, rank: int) -> Tuple[int, int]:
     return rank * n, (rank + 1) * n
 
 
-class NativeComm:
-    """One ``ppo_comm`` (csrc/comm.hip): an RCCL communicator over the ranks of ``process_group``
-    on ``device``.  ``allreduce`` sums an f32 tensor in place on the current stream (capturable)."""
+class NativeCommUnavailable(RuntimeError):
+    """Raised on EVERY rank when any rank cannot take part in the native communicator (the ranks
+    agree on it before and after ncclCommInitRank, so no rank is left inside a collective the
+    others skipped)."""
 
-    def __init__(self, process_group, device: torch.device, world: int, rank: int):
+
+def _resolve_device(device) -> torch.device:
+    """An indexed CUDA device: ``cuda`` without an index means the current device (an
+    unindexed device used to put every rank's communicator on GPU 0)."""
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+class NativeComm:
+    """One ``ppo_comm`` (csrc/comm.hip): an RCCL communicator over ``world`` ranks on ``device``,
+    built from a unique id every rank already holds.  ``allreduce`` sums an f32 tensor in place on
+    the current stream (capturable).  Use ``DataParallel.attach`` to build one: it agrees on the id
+    and on the outcome across ranks."""
+
+    def __init__(self, uid: bytes, device: torch.device, world: int, rank: int):
         import ctypes
         from . import _lib
         self.lib = _lib.load()
-        self.device = torch.device(device)
+        self.device = _resolve_device(device)
         self.world, self.rank = world, rank
-        uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
-            _lib.check(self.lib.ppo_comm_unique_id(buf))
-            uid.copy_(torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8))
-        if world > 1:  # the one use of the process group: the id from rank 0
-            on_dev = torch.distributed.get_backend(process_group) == "nccl"
-            t = uid.to(self.device) if on_dev else uid
-            torch.distributed.broadcast(t, src=0, group=process_group)
-            uid = t.cpu()
-        arr = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)(*uid.tolist())
+        self._retired = False
+        arr = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)(*uid)
         handle = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.ppo_comm_create(arr, world, rank, self.device.index or 0,
+            _lib.check(self.lib.ppo_comm_create(arr, world, rank, self.device.index,
                                                 ctypes.byref(handle)))
         self._comm = handle
 
     @property
     def handle(self):
         return self._comm
+
+    def info(self) -> dict:
+        """What the communicator itself reports (ppo_comm_query: ncclCommCount / ncclCommUserRank /
+        its device), for the bench line -- not what the caller asked for."""
+        import ctypes
+        from . import _lib
+        nranks, rank, device = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.ppo_comm_query(self._comm, ctypes.byref(nranks), ctypes.byref(rank),
+                                           ctypes.byref(device)))
+        return {"nranks": nranks.value, "rank": rank.value, "device": device.value,
+                "rccl_version": int(self.lib.ppo_comm_version())}
 
     def allreduce(self, t: torch.Tensor) -> None:
         from . import _lib
@@ -81,8 +100,14 @@ class NativeComm:
         from . import _lib
         _lib.check(self.lib.ppo_comm_check(self._comm))
 
+    def retire(self) -> None:
+        """Stop using this communicator WITHOUT ncclCommDestroy: after a failed graph capture its
+        state on some rank may hold a half-recorded collective, and a destroy that waits on it
+        would block; the handle is left to the process's exit."""
+        self._retired = True
+
     def close(self) -> None:
-        if getattr(self, "_comm", None) is not None and self._comm.value:
+        if getattr(self, "_comm", None) is not None and self._comm.value and not self._retired:
             self.lib.ppo_comm_destroy(self._comm)
         self._comm = None
 
@@ -91,6 +116,26 @@ class NativeComm:
             self.close()
         except Exception:  # interpreter shutdown
             pass
+
+
+def _native_unique_id() -> bytes:
+    """rank 0's RCCL unique id (ppo_comm_unique_id); raises the engine's error when RCCL is absent."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    _lib.check(lib.ppo_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def _native_loadable() -> bool:
+    """RCCL resolvable in this process (ppo_comm_version > 0), checked before any rank commits to
+    the collective ncclCommInitRank."""
+    from . import _lib
+    try:
+        return int(_lib.load().ppo_comm_version()) > 0
+    except Exception:  # noqa: BLE001 -- any failure to load means "not available here"
+        return False
 
 
 class DataParallel:
@@ -137,6 +182,69 @@ class DataParallel:
         exchange at all (one rank)."""
         return self.comm is not None or self.world == 1
 
+    def agree(self, ok: bool) -> bool:
+        """True only if ``ok`` holds on every rank: a MIN all-reduce of one flag over the process
+        group (its own collective, not the native communicator).  Every decision that changes
+        which collectives a rank issues goes through this, so all ranks take the same branch."""
+        if self.world <= 1 or not torch.distributed.is_initialized():
+            return bool(ok)
+        dev = (torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl"
+               else torch.device("cpu"))
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN, group=self.pg)
+        return bool(int(t.item()))
+
+    def _broadcast_id(self, ok: bool, uid: bytes) -> Tuple[bool, bytes]:
+        """rank 0's (ok, unique id) to every rank: one flag byte + the id, so a rank 0 that could
+        not draw an id sends a sentinel instead of leaving the others blocked in the broadcast."""
+        from . import _lib
+        n = _lib.COMM_ID_BYTES
+        t = torch.zeros(n + 1, dtype=torch.uint8)
+        if self.rank == 0:
+            t[0] = 1 if ok else 0
+            if ok:
+                t[1:] = torch.frombuffer(bytearray(uid), dtype=torch.uint8)
+        if self.world > 1:
+            on_dev = self.backend == "nccl"
+            w = t.to(torch.device("cuda", torch.cuda.current_device())) if on_dev else t
+            torch.distributed.broadcast(w, src=0, group=self.pg)
+            t = w.cpu()
+        return bool(t[0]), bytes(t[1:].tolist())
+
+    def build_comm(self, device, make_id=None, make_comm=None, loadable=None):
+        """The native communicator, built only if every rank can build it (NativeCommUnavailable on
+        every rank otherwise -- the same outcome everywhere):
+          1. every rank checks that RCCL resolves here; rank 0 draws the unique id;
+          2. rank 0 broadcasts (ok, id) -- a sentinel when it failed;
+          3. agree(all loadable and rank 0 ok), else every rank gives up before the collective init;
+          4. ncclCommInitRank on every rank; agree(all succeeded), else the ranks that did build one
+             retire it and every rank gives up.
+        ``make_id`` / ``make_comm`` / ``loadable`` are injectable for the CPU tests."""
+        make_id = make_id or _native_unique_id
+        make_comm = make_comm or (lambda uid, dev, w, r: NativeComm(uid, dev, w, r))
+        loadable = loadable or _native_loadable
+        local_ok = bool(loadable())
+        uid, id_ok, why = b"", True, ""
+        if self.rank == 0:
+            try:
+                uid = make_id()
+            except RuntimeError as err:
+                id_ok, why = False, f"rank 0 could not draw the RCCL unique id: {err}"
+        id_ok, uid = self._broadcast_id(id_ok, uid)
+        if not self.agree(local_ok and id_ok):
+            raise NativeCommUnavailable(why or ("RCCL is not resolvable on some rank" if id_ok else
+                                                "rank 0 could not draw the RCCL unique id"))
+        comm, err_msg = None, ""
+        try:
+            comm = make_comm(uid, device, self.world, self.rank)
+        except RuntimeError as err:
+            err_msg = str(err)
+        if not self.agree(comm is not None):
+            if comm is not None:
+                comm.retire()
+            raise NativeCommUnavailable(err_msg or "ncclCommInitRank failed on another rank")
+        return comm
+
     def attach(self, engine, device: torch.device) -> None:
         """Create the native communicator for an RCCL process group (or the rccl rehearsal) and
         hand it to the engine's ctx (``ppo_ctx_set_comm``).  The logged actor
@@ -147,13 +255,50 @@ class DataParallel:
         if self.comm is None and (self.backend == "nccl" and (self.world > 1 or self.rehearse_rccl)):
             if os.environ.get("PPO_DP_NATIVE", "1") == "1":
                 try:
-                    self.comm = NativeComm(self.pg, device, self.world, self.rank)
-                except RuntimeError as err:  # _lib.EngineError: no usable RCCL in this process
+                    self.comm = self.build_comm(_resolve_device(device))
+                except NativeCommUnavailable as err:  # the same on every rank (build_comm)
                     warnings.warn(f"native RCCL communicator unavailable ({err}); the gradient "
                                   f"all-reduce goes through torch.distributed, eagerly")
                     self.comm = None
         if self.comm is not None and hasattr(engine, "set_comm"):
             engine.set_comm(self.comm)
+
+    def drop_native(self, engine=None) -> None:
+        """Every rank leaves the native communicator together (after agree() said some rank
+        could not use it): the engine's ctx is detached, the communicator retired, and the
+        exchange falls back to torch.distributed."""
+        if engine is not None and hasattr(engine, "set_comm"):
+            engine.set_comm(None)
+        if self.comm is not None:
+            self.comm.retire()
+        self.comm = None
+
+    def capture_agreed(self, capture, engine=None) -> Optional[str]:
+        """Run ``capture()`` (recording an update loop that contains the native all-reduce into a
+        hipGraph).  None when it succeeded on EVERY rank.  When it failed on any rank, every rank
+        leaves the native communicator (drop_native) and the reason is returned, so all ranks
+        continue on the same eager torch.distributed path (the fallback used to be
+        decided per rank).  Without a native communicator a capture failure is a plain error."""
+        err = None
+        try:
+            capture()
+        except RuntimeError as e:
+            if self.comm is None:
+                raise
+            err = str(e) or type(e).__name__
+        if self.agree(err is None):
+            return None
+        self.drop_native(engine)
+        return err or "the capture failed on another rank"
+
+    def comm_info(self) -> dict:
+        """{backend, native, nranks, ...} of the exchange as it will run: read back from the native
+        communicator when there is one, else the process group's own size."""
+        out = {"backend": self.backend or "none", "native": self.comm is not None,
+               "nranks": self.world, "rank": self.rank}
+        if self.comm is not None and hasattr(self.comm, "info"):
+            out.update(self.comm.info())
+        return out
 
     def allreduce_grad(self, flat_grad: torch.Tensor) -> None:
         """SUM of the flat gradient over ranks, in place, ordered on the current stream (the native

@@ -33,17 +33,31 @@ from typing import List, Sequence
 import torch
 from torch import nn
 
-from .ppo_ref import ACTIVATIONS, MLPBlock, RefConfig, _BF16Linear, use_bf16_gemms as _mlp_bf16
+from .ppo_ref import ACTIVATIONS, MLPBlock, RefConfig, _BF16Linear, _bf, use_bf16_gemms as _mlp_bf16
+
+
+class _BF16GateLinear(_BF16Linear):
+    """_BF16Linear for the BiLSTM's gate products (X W_ih^T + b_ih, h W_hh^T + b_hh): the same
+    bf16-operand GEMMs, but the bias gradient is the sum of the bf16-ROUNDED gate gradient dG --
+    what csrc/bilstm.hip computes in bf16 mode, where the cell backward writes dG once as bf16 and
+    both the weight-gradient GEMMs and the b_ih / b_hh column sums (gemm_bf16_kernel's COLSUM,
+    wide_gemm.h's acol) read that one bf16 copy."""
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g = _bf(gy)
+        return g @ _bf(w), g.t() @ _bf(x), (g.sum(0) if ctx.has_b else None)
 
 
 def _linear(x, w, b, bf16: bool):
     """torch's F.linear, or the bf16-operand product of the engine's PPO_PREC_BF16 mode
-    (ppo_ref._BF16Linear: both operands rounded to bf16, accumulation in x's dtype, f32 bias and
-    bias gradient) -- not a reference behaviour."""
+    (_BF16GateLinear: both operands rounded to bf16, accumulation in x's dtype, f32 bias, the bias
+    gradient summed from bf16(dG)) -- not a reference behaviour."""
     if not bf16:
         return torch.nn.functional.linear(x, w, b)
     lead = x.shape[:-1]
-    return _BF16Linear.apply(x.reshape(-1, x.shape[-1]), w, b).reshape(*lead, w.shape[0])
+    return _BF16GateLinear.apply(x.reshape(-1, x.shape[-1]), w, b).reshape(*lead, w.shape[0])
 
 
 def lstm_direction(x: torch.Tensor, w_ih, w_hh, b_ih, b_hh, reverse: bool,
@@ -200,7 +214,8 @@ def use_bf16_gemms(agent: RefLSTMAgent) -> None:
     adds, the LSTM cells, activations, the distribution and the losses stay f32):
       * the BiLSTMs (lstm_actor.py:12-16, lstm_critic.py:19-23): the input projection X W_ih^T, the
         per-step recurrent projection h W_hh^T, and through autograd their backward products
-        (dG W_hh, dG W_ih, dG^T X, dG^T h_prev) on bf16(dG); bias gradients from the f32 dG;
+        (dG W_hh, dG W_ih, dG^T X, dG^T h_prev) on bf16(dG); the b_ih / b_hh gradients summed
+        from the same bf16(dG) (_BF16GateLinear), as the engine sums them;
       * the MLP heads (NetworkBlock, lstm_actor.py:17-38, lstm_critic.py:24-31): ppo_ref's
         _BF16Linear on every Linear.
     Run it on an agent cast to float64 (``agent.networks.double()`` with f64 inputs) for the

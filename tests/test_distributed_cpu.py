@@ -105,3 +105,80 @@ def test_exact_data_parallel_gradient_world2():
         assert p.exitcode == 0
     rel = q.get(timeout=5)
     assert rel < 1e-5, rel
+
+
+class _FakeComm:
+    def __init__(self):
+        self.retired = False
+
+    def retire(self):
+        self.retired = True
+
+
+def _agree_worker(rank, world, port, case, out):
+    """DataParallel.build_comm with injected pieces: whatever fails on ONE rank, every rank ends
+    with the same outcome and none is left blocked in a collective."""
+    from mujoco_reinforcement_learning_amd.distributed import NativeCommUnavailable
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    dp = DataParallel()
+    made = []
+
+    def make_id():
+        if case == "id_fails":
+            raise RuntimeError("no RCCL on rank 0")
+        return bytes(range(128))
+
+    def make_comm(uid, dev, w, r):
+        assert uid == bytes(range(128)), "every rank holds rank 0's id"
+        if case == "init_fails" and r == 1:
+            raise RuntimeError("ncclCommInitRank failed")
+        c = _FakeComm()
+        made.append(c)
+        return c
+
+    loadable = (lambda: rank != 1) if case == "not_loadable" else (lambda: True)
+    try:
+        comm = dp.build_comm(torch.device("cpu"), make_id=make_id, make_comm=make_comm,
+                             loadable=loadable)
+        res = "ok"
+        assert comm is made[0]
+    except NativeCommUnavailable:
+        res = "unavailable"
+    # the ranks still pair their collectives afterwards
+    g = torch.full((3,), float(rank + 1))
+    dp.allreduce_grad(g)
+    out.put((rank, res, [c.retired for c in made], float(g[0])))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,want", [("ok", "ok"), ("id_fails", "unavailable"),
+                                       ("init_fails", "unavailable"),
+                                       ("not_loadable", "unavailable")])
+def test_native_comm_build_agreed_across_ranks(case, want):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert [r[1] for r in res] == [want, want], res
+    assert all(r[3] == 3.0 for r in res), res  # the exchange after the decision pairs up
+    if case == "init_fails":
+        assert res[0][2] == [True], res  # rank 0 built one and retired it
+    if case == "ok":
+        assert res[0][2] == [False] and res[1][2] == [False]
+
+
+def test_capture_agreed_single_rank():
+    dp = DataParallel()
+    assert dp.capture_agreed(lambda: None) is None
+    with pytest.raises(RuntimeError):  # no native communicator: a capture error is an error
+        dp.capture_agreed(lambda: (_ for _ in ()).throw(RuntimeError("boom")))
+    c = dp.comm = _FakeComm()
+    assert dp.capture_agreed(lambda: (_ for _ in ()).throw(RuntimeError("boom"))) == "boom"
+    assert dp.comm is None and c.retired

@@ -324,14 +324,16 @@ def test_iteration_matches_bf16_emulation(gpu):
         values / actions / log-probs within 2e-3 of scale;
       * GAE of the engine's own rollout bit-exact;
       * step-wise (parity_util.bf16_stepwise) every optimizer step from the oracle's own state: the
-        gradient against the f64-accumulated emulation within 1e-1 of each tensor's max and 4e-2
-        relative L2, the update within 3e-2 relative L2 where the gradient's sign is determined,
-        every element within 2*lr.  The encoder's bf16 rounding cascade is wide: a conv output
+        gradient against the f64-accumulated emulation within 7.7e-2 of each tensor's max and
+        2.6e-2 relative L2, the update within 2.4e-2 relative L2 where the gradient's sign is
+        determined, every element within 2*lr -- bars at 1.3x the observed maxima (the kernels
+        are bitwise deterministic, so a regression shows as a move of the observed value).  The encoder's bf16 rounding cascade is wide: a conv output
         whose f32 sum (in the engine's order) lands on the other side of a bf16 rounding edge
         moves every product downstream by ~2^-8 of its term; the emulation's own f32-vs-f64
         spread reaches 3.4e-2 of max at 384 rows (test_minibatch_grad_matches_oracle), and the
         engine's summation order differs from torch's, which the same-order f32 / f64 pair does
-        not see (round 5 observed: 5.9e-2 of max, 2.0e-2 relative L2, update 1.9e-2)."""
+        not see (observed, rounds 5 and 6: 5.92e-2 of max, 2.01e-2 relative L2, update 1.86e-2,
+        beside the emulation's own spread of 2.76e-2 / 1.65e-2)."""
     import copy
     from mujoco_reinforcement_learning_amd.environments import make_synthetic_streams
     n, t, b, epochs = 32, 16, 256, 2
@@ -364,5 +366,5 @@ def test_iteration_matches_bf16_emulation(gpu):
     R.train(ref, ref_mem, 0)
     rows = replay_rows(99, n, t, b, epochs, cfg.act_dim)
     assert len(rows) == len(steps) == epochs * (n * t // b)
-    bf16_stepwise(agent, ref0, cfg, ref_mem, steps, rows, max_bar=1e-1, l2_bar=4e-2,
-                  update_bar=3e-2, label="cnn bf16", grad_fn=_cnn_f64_grad)
+    bf16_stepwise(agent, ref0, cfg, ref_mem, steps, rows, max_bar=7.7e-2, l2_bar=2.6e-2,
+                  update_bar=2.4e-2, label="cnn bf16", grad_fn=_cnn_f64_grad)

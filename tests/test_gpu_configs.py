@@ -168,11 +168,12 @@ def test_minibatch_grad_humanoid_bf16_paired_launches(gpu, monkeypatch):
     """At minibatch sizes above 4,096 rows the wide path runs each hidden layer's WGRAD and DGRAD
     as one wide_pair_kernel launch (DGRAD writing dZ to its own buffer): held to the
     f64-accumulated bf16 emulation at the bench's B_local = 8,192, and bitwise equal to the two
-    separate launches (PPO_WIDE_PAIR0=1) -- gradient and losses.  The emulation bar's max-element
-    part is 1.5e-2 here (1e-2 at 2,048 rows): four times the rows in every weight-gradient column
-    sum, four times the bf16 rounding flips of intermediates behind one element (observed
-    1.1e-2 on one critic element; the rel-L2 bar stays 5e-3, observed <= 1.9e-3)."""
-    _minibatch_case(gpu, HUMANOID, 16384, 8192, "bf16", bf16_bar=(1.5e-2, 5e-3))
+    separate launches (PPO_WIDE_PAIR0=1) -- gradient and losses.  The kernels are bitwise
+    deterministic, so the bar sits at <= 1.3x the observed value: observed
+    1.141e-2 of max on one critic element (four times the rows of the 2,048-row case in every
+    weight-gradient column sum, so more bf16 rounding flips of intermediates behind one element)
+    and 1.849e-3 relative L2 -> bars 1.45e-2 / 2.4e-3."""
+    _minibatch_case(gpu, HUMANOID, 16384, 8192, "bf16", bf16_bar=(1.45e-2, 2.4e-3))
     eng, _ = _agent_pair(gpu, 4, 16384, 8192, HUMANOID["obs"], HUMANOID["act"],
                          HUMANOID["hidden"], None, 1, precision="bf16")
     g = torch.Generator().manual_seed(11)

@@ -179,6 +179,57 @@ def test_minibatch_grad_deterministic_and_bf16_close(gpu):
         assert rel <= 6e-2, (i, rel)
 
 
+@pytest.mark.parametrize("latent,window,layers", [(8, 3, 1), (48, 2, 2)])
+def test_bf16_minibatch_grad_first_call_small_latent(gpu, latent, window, layers):
+    """bf16 minibatch gradient as the FIRST call on a fresh ctx at latents whose 4*latent is not
+    a multiple of 128, so the layer-0 input projection takes the layered GEMM instead of the wide
+    one (that fallback read the f32 row buffer, which bf16 mode never writes).  Held to
+    the f64-accumulated bf16 emulation: every tensor within 4x the emulation's own f32-vs-f64
+    spread plus 1e-5 (of its max, and in relative L2); losses within 1e-3.  Round 6 observed:
+    latent 8 2.3e-6 / 1.1e-6 (spread 9.0e-7 / 8.1e-7), latent 48 1.27e-4 / 3.6e-5 (spread the
+    same).  Before the fix the f32 row buffer held no data and the gradients were unrelated."""
+    import copy
+    obs, act, hidden, b = 17, 6, (32, 32), 256
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=3)
+    agent.engine.set_precision("bf16")
+    cfg = RefConfig(obs_dim=obs, act_dim=act, window=window, actor_hidden=hidden,
+                    critic_hidden=hidden, activation="relu")
+    torch.manual_seed(3)
+    ref = L.RefLSTMAgent(cfg, latent, layers)
+    assert torch.equal(agent.packed_params().cpu(), R.flat_params(ref))
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    with torch.no_grad():
+        mean, std = ref.networks["actor"](x)
+        lp = torch.distributions.Normal(mean, std).log_prob(actions).sum(1)
+    old_logp = lp + 0.15 * torch.randn(b, generator=gen)
+    g, loss = _grad(agent, x, actions, old_logp, adv, vt)
+    e32 = copy.deepcopy(ref)
+    L.use_bf16_gemms(e32)
+    e64 = copy.deepcopy(ref)
+    e64.networks.double()
+    L.use_bf16_gemms(e64)
+    g64, la, lc = L.minibatch_grads(e64, x.double(), actions.double(), old_logp.double(),
+                                    adv.double(), vt.double(), 0.1, 1e-4)
+    g32, _, _ = L.minibatch_grads(e32, x, actions, old_logp, adv, vt, 0.1, 1e-4)
+    assert abs(float(loss[0]) - la) <= 1e-3 * max(1.0, abs(la)), (float(loss[0]), la)
+    assert abs(float(loss[1]) - lc) <= 1e-3 * max(1.0, abs(lc)), (float(loss[1]), lc)
+    spread = {name: (e, l2) for name, e, l2 in grad_errors(g32, g64, ref)}
+    worst, worst_l2, bad = 0.0, 0.0, []
+    for name, err, l2 in grad_errors(g, g64, ref):
+        s_max, s_l2 = spread[name]
+        worst, worst_l2 = max(worst, err), max(worst_l2, l2)
+        if err > 4 * s_max + 1e-5 or l2 > 4 * s_l2 + 1e-5:
+            bad.append((name, err, l2, s_max, s_l2))
+    print(f"bf16 first call, latent {latent}: worst {worst:.3e} of max, rel L2 {worst_l2:.3e} "
+          f"(emulation f32 vs f64: {max(e for e, _ in spread.values()):.3e}, "
+          f"{max(v for _, v in spread.values()):.3e})")
+    assert not bad, bad
+
+
 MAIN_NET = dict(obs=348, window=5, act=17, latent=256, layers=1, hidden=(256, 256, 128, 128))
 
 
@@ -234,14 +285,16 @@ def test_bf16_forward_matches_f64_emulation(gpu):
 def test_bf16_minibatch_grad_matches_f64_emulation(gpu):
     """the bf16 BiLSTM minibatch gradient (ppo.py:108-135 with the LSTM agent)
     on the main.py network, B = 1024, against the f64-accumulated bf16 emulation at a FIXED bar per
-    tensor: max error <= 1.5e-1 of the tensor's max and relative L2 <= 5e-2.  Why that loose: a
-    bf16 rounding of an intermediate flipped by the f32 summation order changes it by 2^-8, which
-    moves the next layer's sums by about their own bf16 half-ulp, so flips cascade through the
-    LSTM and the 4 MLP layers -- the emulation's OWN f32-vs-f64 spread at this shape is 5e-2 of
-    max / 1.5e-2 L2 (critic hidden layers).  Over all tensors, the engine's worst error must also
-    stay within 2x the emulation's own worst (the spread of one tensor alone is a noisy sample:
-    round 5 saw 4.2e-2 against 1.2e-2 on critic.network.first_layers.6.weight while the worst
-    over all tensors was 5.0e-2 against 3.8e-2).  Losses within 1e-3 relative."""
+    tensor: max error <= 6.6e-2 of the tensor's max and relative L2 <= 2.25e-2 -- 1.3x the observed
+    worst (round 6: 5.03e-2 of max on actor.actor.first_layers.4.weight, 1.73e-2 L2 on the critic's reverse
+    bias; the kernels are bitwise deterministic, so a regression moves the observed value).  Why
+    that wide at all: a bf16 rounding of an intermediate flipped by the f32 summation order changes
+    it by 2^-8, which moves the next layer's sums by about their own bf16 half-ulp, so flips
+    cascade through the LSTM and the 4 MLP layers -- the emulation's OWN f32-vs-f64 spread at this
+    shape is 4.1e-2 of max / 1.1e-2 L2.  Over all tensors, the engine's worst error must also stay
+    within 2x the emulation's own worst.  The emulation sums the b_ih / b_hh gradients from the
+    bf16-rounded gate gradient, as the engine does (lstm_ref._BF16GateLinear).
+    Losses within 1e-3 relative."""
     agent, ref, e32, e64, (x, actions, old_logp, adv, vt) = _main_net_case(gpu, 1024)
     g, loss = _grad(agent, x, actions, old_logp, adv, vt)
     g64, la, lc = L.minibatch_grads(e64, x.double(), actions.double(), old_logp.double(),
@@ -256,7 +309,7 @@ def test_bf16_minibatch_grad_matches_f64_emulation(gpu):
         print(f"bf16 main.py grad {name}: err {err:.3e} of max, rel L2 {l2:.3e} "
               f"(emulation f32 vs f64: {s_max:.3e}, {s_l2:.3e})")
         worst, worst_l2 = max(worst, err), max(worst_l2, l2)
-        if err > 1.5e-1 or l2 > 5e-2:
+        if err > 6.6e-2 or l2 > 2.25e-2:
             bad.append((name, err, l2, s_max))
     s_worst = max(e for e, _ in spread.values())
     s_worst_l2 = max(l for _, l in spread.values())
@@ -269,11 +322,14 @@ def test_bf16_minibatch_grad_matches_f64_emulation(gpu):
 def test_lstm_bf16_iteration_matches_bf16_emulation(gpu):
     """One PPO iteration with the BiLSTM agent in bf16 mode (latent 64 so the forward steps run
     as lstm_step_fwd_kernel) against the bf16 emulation oracle on the same torch RNG streams:
-    rollout values / actions / log-probs within 2e-3 of scale; free-running update within 2e-2
+    rollout values / actions / log-probs within 2e-3 of scale; free-running update within 1e-4
     relative L2 per tensor; and step-wise (parity_util.bf16_stepwise) every optimizer step from
-    the oracle's own state: gradient within 1e-2 of each tensor's max / 5e-3 relative L2 of the
-    f64-accumulated emulation (its own f32 spread at these shapes: <= 1.9e-3 / 6.5e-4), update
-    within 1e-2 relative L2 where the gradient sign is determined."""
+    the oracle's own state: gradient within 2.5e-3 of each tensor's max / 8.5e-4 relative L2 of the
+    f64-accumulated emulation, update within 1e-4 relative L2 where the gradient sign is
+    determined.  Round 6 observed (with the emulation's bias gradients summed from bf16(dG), as
+    the engine sums them): step-wise 1.87e-3 / 6.47e-4 -- exactly the f32 emulation's own spread
+    from f64, i.e. the engine tracks the f32 emulation -- update 7.1e-5, free-running 4.7e-5
+    (round 5, before that oracle fix: 2.7e-3 / 1.8e-3 / 1.1e-3 and 1.5e-2).  Bars at 1.3x."""
     import copy
     n, t, b = 32, 16, 128
     algo, agent, ref, env, cfg = make_pair(gpu, n=n, t=t, b=b, epochs=2, p_term=0.05,
@@ -299,11 +355,11 @@ def test_lstm_bf16_iteration_matches_bf16_emulation(gpu):
             continue
         rel = float((du_e - du_r).norm() / du_r.norm())
         worst = max(worst, rel)
-        assert rel <= 2e-2, (name, rel)
+        assert rel <= 1e-4, (name, rel)
     print(f"lstm bf16 free-running update: worst rel L2 {worst:.3e}")
     rows = replay_rows(99, n, t, b, 2, cfg.act_dim)
-    bf16_stepwise(agent, ref0, cfg, ref_mem, steps, rows, max_bar=1e-2, l2_bar=5e-3,
-                  update_bar=1e-2, bf16_fn=L.use_bf16_gemms, label="lstm bf16")
+    bf16_stepwise(agent, ref0, cfg, ref_mem, steps, rows, max_bar=2.5e-3, l2_bar=8.5e-4,
+                  update_bar=1e-4, bf16_fn=L.use_bf16_gemms, label="lstm bf16")
 
 
 def test_fused_forward_step_bitwise_equals_layered(gpu):
