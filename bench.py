@@ -86,9 +86,9 @@ def parse():
                    help="launch the rollout and the update loop eagerly (no hipGraph replay)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "bench_traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
-    p.add_argument("--gae-sweep", default="16384,65536",
+    p.add_argument("--gae-sweep", default="4096,16384,65536",
                    help="env counts at which the headline line also times the standalone GAE scan "
-                        "(its bandwidth ceiling beyond 4096 envs; empty for none)")
+                        "(the headline's 4096 and its bandwidth ceiling beyond; empty for none)")
     p.add_argument("--legs", default="ant,humanoid,cnn,lstm",
                    help="BASELINE-config legs the default N=1 line carries (comma list of ant, "
                         "humanoid, cnn, lstm; empty for none)")
@@ -145,6 +145,21 @@ _ENV_NAMES = {(17, 6): "HalfCheetah-v4", (27, 8): "Ant-v4", (376, 17): "Humanoid
               (348, 17): "main.py humanoid (O=348)", (84 * 84 * 3, 6): "cheetah-run pixels"}
 
 
+def _traffic_of(traffic, name):
+    """PMC bytes per launch of ``name``; a fused-update name carries its phase schedule as the last
+    template argument (PPO_FUSED_SCHED: an LDS-level reordering, the same global loads and stores),
+    so a table measured under another schedule of the same instantiation is used for it."""
+    if name in traffic:
+        return traffic[name]
+    import re
+    base = re.sub(r", \d+>$", ">", name)
+    if name.startswith("fused_update_kernel<"):
+        for k, v in traffic.items():
+            if k == base or re.sub(r", \d+>$", ">", k) == base:
+                return v
+    return None
+
+
 def roofline(name, c, traffic, force_hbm=False):
     """Roofline of one kernel instantiation from its live event records.  The bound is the roof
     the kernel's own algorithmic work hits first: MFMA (FLOPs / dense peak of its dtype) or HBM
@@ -167,7 +182,8 @@ def roofline(name, c, traffic, force_hbm=False):
         achieved, peak, unit = c["bytes"] / launches / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
     return {"bound": "mfma" if mfma else "hbm", "kernel": name, "achieved": achieved,
             "peak": peak, "unit": unit, "frac": achieved / peak,
-            "traffic": traffic.get(name), "avg_launch_us": avg_s * 1e6, "launches": c["launches"],
+            "traffic": _traffic_of(traffic, name), "avg_launch_us": avg_s * 1e6,
+            "launches": c["launches"],
             "algorithmic_per_launch": (c["flops"] if mfma else c["bytes"]) / launches}
 
 

@@ -121,5 +121,8 @@ int fused_prep_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 int fused_update_launch(const FusedArgs &q, const TimRec &rec, hipStream_t st);
 // Supported hidden widths (compiled instantiations).
 bool fused_width_ok(int hidden);
+// The phase schedule the fused kernel runs for activation `act` (its SCHED template argument:
+// part of the launched instantiation's name, e.g. for the rocprof agreement check).
+int fused_sched(int act);
 
 }  // namespace ppo

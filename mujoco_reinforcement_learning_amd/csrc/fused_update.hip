@@ -387,7 +387,10 @@ struct Lds {
   // ReLU: W_h^T as a bf16 [H][16] image (32-B rows): the d2 product's A fragment is one 16-B read
   // (head_t_frag gathers it from the head image with 8 two-byte reads otherwise)
   static constexpr int WHT = W0 + (F32A2 ? 0 : H * 64);
-  static constexpr int TOTAL = WHT + (F32A2 ? 0 : H * 32);
+  // ReLU, deferred dW0 (SCHED bit 0): the previous chunk's X image stays resident while the next
+  // one is staged (the two buffers alternate chunk by chunk)
+  static constexpr int X2 = WHT + (F32A2 ? 0 : H * 32);
+  static constexpr int TOTAL = X2 + (F32A2 ? 0 : R * 64);
   static_assert(TOTAL <= 163840, "LDS budget");
   static_assert(R * PITCH <= A2BYTES, "D1 image must fit in the a2 region");
 };
@@ -414,14 +417,32 @@ __device__ __forceinline__ void mfma16_drain(f32x4 &acc) { asm volatile("s_nop 1
 // Phase barriers are LDS-only (lds_sync): waves hand each other data through LDS only, so the
 // record prefetch and the weight-ring primes stay in flight across them (__syncthreads drained
 // them at every phase; measured 10.40-10.47 -> 10.29-10.33 ms per iteration, profiles/r04_lds_barrier/)
-template <int H, int ACT, int NH, bool ACTOR, bool STAMP>
+//
+// SCHED (ReLU instantiations; tanh / ELU always run 0): wave-local work moved out of its own
+// barrier-bounded phase into an MFMA pass of the same wave, where its LDS reads and MFMAs overlap
+// the pass instead of serialising behind a barrier:
+//   bit 0  dW0 += D1^T X of chunk c runs at the start of chunk c+1's L1 pass (phase 2): D1 sits in
+//          the wave's OWN columns of the a2 region until the wave itself overwrites them in phase
+//          3, and X(c) stays in the second X buffer; phase 7 and the chunk's closing barrier go
+//          away (the last chunk's dW0 runs after the loop).  Same MFMA chain into gw0 in the same
+//          order: bitwise the same gradient.
+//   bit 2  (SCHED 5) the deferred dW0 is issued right AFTER the L1 pass instead of before it, so
+//          its MFMAs overlap the wave's own phase-3 epilogue (bias + act + the a2 stores, VALU /
+//          LDS) rather than the pass's ring loads.
+// Measured and dropped (round 6): the head dW inside phase 6a (a tie) and the next
+// chunk's layer 0 hoisted behind the dgrad pass with phases 0 and 1 removed (16 spilled VGPRs,
+// 10-17 % slower).
+template <int H, int ACT, int NH, bool ACTOR, bool STAMP, int SCHED>
 __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N, char *lds,
                                            uint64_t *stamps) {
   static_assert(H == 32 * NW, "wave w owns feature tile w");
   constexpr bool F32A2 = ACT != PPO_ACT_RELU;
+  constexpr bool DEFER_DW0 = (SCHED & 1) && !F32A2;
+  constexpr bool DW0_AFTER = DEFER_DW0 && (SCHED & 4);
   using L = Lds<H, F32A2>;
   constexpr int z = ACTOR ? 0 : 1;
-  char *const ximg = lds + L::X;
+  char *ximg = lds + L::X;        // this chunk's X image
+  char *xprev = lds + L::X2;      // DEFER_DW0: the previous chunk's (its dW0 runs in phase 2)
   char *const a1img = lds + L::A1;
   char *const d2img = lds + L::D2;
   char *const a2img = lds + L::A2;
@@ -518,6 +539,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
   uint64_t xpre = load_half(blockIdx.x, i_first, tid0, false);
   bool xok = row_ok(blockIdx.x, i_first, tid0);
+  if constexpr (DEFER_DW0) {  // the first deferred dW0 reads these: exact zeros (see phase 2)
+    for (int i = tid; i < R * (2 * H) / 16; i += NT)
+      *reinterpret_cast<uint4 *>(lds + L::A2 + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < R * 64 / 16; i += NT)
+      *reinterpret_cast<uint4 *>(lds + L::X2 + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+  }
   lds_sync();
 
   // ---- persistent accumulators ----
@@ -555,15 +582,24 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   }
 
   bf16x8 ring[PD + 1];
+  // the current chunk's row scalars / validity and the next chunk's row index (loop-carried)
+  uint64_t srow_c = 0;
+  bool sok_c = false;
+  int inext = 0;
   for (; chunk < nchunks; chunk += G) {
     // ---- phase 0: the chunk's rows (loaded during the previous chunk) -> X image and the row
     //      scalars (actions, old log-prob, advantage, value target: 64 x 64 B); W0 fragments;
     //      the next chunk's row indices ----
+    if constexpr (DEFER_DW0) {  // X(c) into the buffer X(c-2) used; X(c-1) stays for its dW0
+      char *const t = ximg;
+      ximg = xprev;
+      xprev = t;
+    }
     OPAQUE_LANE();
     *reinterpret_cast<uint64_t *>(ximg + x_off(tid >> 3, (tid & 7) >> 1) + 8 * (tid & 1)) = xok ? xpre : 0;
-    const bool sok = xok;
-    const uint64_t srow_v = load_half(chunk, icur, tid, true);
-    const int inext = row_index(chunk + G);  // lands by phase 6a
+    sok_c = xok;
+    srow_c = load_half(chunk, icur, tid, true);
+    inext = row_index(chunk + G);  // lands by phase 6a
     bf16x8 w0f[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -609,13 +645,29 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
 
     // ---- phase 2: a2 = W1 a1 (f32 accumulators) ----
     OPAQUE_LANE();
+    // the previous chunk's dW0 += D1^T X (phase 7 of the undeferred schedule): the wave's own D1
+    // columns (untouched until its phase 3 below) and X(c-1); every transposed read first, then
+    // the four chained MFMAs.  Unconditional: before the first chunk the prologue zeroed the
+    // wave's D1 columns and the second X image, so the first chunk adds an exact +0 (no branch,
+    // no register merge).
+#define DEFERRED_DW0()                                                     \
+  {                                                                        \
+    bf16x8 fd[R / 16], fx[R / 16];                                         \
+    _Pragma("unroll") for (int ks = 0; ks < R / 16; ++ks) {                \
+      fd[ks] = tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane);            \
+      fx[ks] = tr_frag_x(xprev, 16 * ks, lane);                            \
+    }                                                                      \
+    _Pragma("unroll") for (int ks = 0; ks < R / 16; ++ks) gw0 = mfma(fd[ks], fx[ks], gw0); \
+  }
+    if constexpr (DEFER_DW0 && !DW0_AFTER) DEFERRED_DW0()
     f32x16 a2[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
-    *reinterpret_cast<uint64_t *>(lds + L::SROW + tid0 * 8) = sok ? srow_v : 0;  // landed during phases 1-2
+    if constexpr (DW0_AFTER) DEFERRED_DW0()
+    *reinterpret_cast<uint64_t *>(lds + L::SROW + tid0 * 8) = sok_c ? srow_c : 0;  // landed during phases 1-2
     STAMP_AT(2);
 
     // ---- phase 3: bias + act -> a2 region ----
@@ -812,24 +864,23 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
       gb1 += rs16(bsum, lane);
     }
     // head dW += dz^T a2 over the chunk's 64 rows: wave w's two 16-feature tiles
-#pragma unroll
-    for (int ks = 0; ks < R / 32; ++ks) {
-      const bf16x8 af = lds_b128(dztimg + (lane & 15) * kDzTPitch + 2 * (32 * ks + 8 * (lane >> 4)));
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        bf16x8 bv;
-        if constexpr (F32A2) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = a2f[(32 * ks + 8 * (lane >> 4) + j) * (L::A2P / 4) + 32 * w + 16 * u + (lane & 15)];
-          bv = pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
-        } else {
-          bv = tr_frag16(a2img, L::PITCH, 32 * ks, 32 * w + 16 * u, lane);
-        }
-        ghw[u] = mfma16(af, bv, ghw[u]);
-      }
-    }
+#define HEAD_DW()                                                                                 \
+  _Pragma("unroll") for (int ks = 0; ks < R / 32; ++ks) {                                         \
+    const bf16x8 af = lds_b128(dztimg + (lane & 15) * kDzTPitch + 2 * (32 * ks + 8 * (lane >> 4))); \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                               \
+      bf16x8 bv;                                                                                  \
+      if constexpr (F32A2) {                                                                      \
+        float v[8];                                                                               \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] =                                      \
+            a2f[(32 * ks + 8 * (lane >> 4) + j) * (L::A2P / 4) + 32 * w + 16 * u + (lane & 15)]; \
+        bv = pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));     \
+      } else {                                                                                    \
+        bv = tr_frag16(a2img, L::PITCH, 32 * ks, 32 * w + 16 * u, lane);                          \
+      }                                                                                           \
+      ghw[u] = mfma16(af, bv, ghw[u]);                                                            \
+    }                                                                                             \
+  }
+    HEAD_DW()
     lds_sync();
     STAMP_AT(5);
 
@@ -916,26 +967,47 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     STAMP_AT(8);
 
     // ---- phase 7: dW0 += D1^T X (the wave's own D1 columns, written by this wave above: no
-    //      barrier before it; the chunk's closing barrier follows) ----
-    OPAQUE_LANE();
-    {
-      // every transposed fragment read issued first (16 ds_read_b64_tr_b16, 32 registers: the
-      // dgrad accumulators are dead here), then the four chained MFMAs -- one LDS round trip for
-      // the phase instead of one per k-step
+    //      barrier before it; the chunk's closing barrier follows).  DEFER_DW0: in the next
+    //      chunk's phase 2 (or after the loop), and no closing barrier: the next chunk's X goes to
+    //      the other buffer, and every other region it writes before its phase-0 barrier is
+    //      read by no wave after this chunk's phase-5 barrier ----
+    if constexpr (!DEFER_DW0) {
+      OPAQUE_LANE();
+      {
+        // every transposed fragment read issued first (16 ds_read_b64_tr_b16, 32 registers: the
+        // dgrad accumulators are dead here), then the four chained MFMAs -- one LDS round trip
+        // for the phase instead of one per k-step
+        bf16x8 fd[R / 16], fx[R / 16];
+#pragma unroll
+        for (int ks = 0; ks < R / 16; ++ks) {
+          fd[ks] = tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane);
+          fx[ks] = tr_frag_x(ximg, 16 * ks, lane);
+        }
+#pragma unroll
+        for (int ks = 0; ks < R / 16; ++ks) gw0 = mfma(fd[ks], fx[ks], gw0);
+      }
+      lds_sync();
+    }
+    STAMP_AT(9);
+  }
+  if constexpr (DEFER_DW0) {  // the last chunk's dW0 (wave-local: D1 own columns, its X image)
+    {  // (a workgroup without chunks adds the prologue's zeros)
+      OPAQUE_LANE();
+      char *const xlast = ximg;
       bf16x8 fd[R / 16], fx[R / 16];
 #pragma unroll
       for (int ks = 0; ks < R / 16; ++ks) {
         fd[ks] = tr_frag(d1img, L::PITCH, 16 * ks, 32 * w, lane);
-        fx[ks] = tr_frag_x(ximg, 16 * ks, lane);
+        fx[ks] = tr_frag_x(xlast, 16 * ks, lane);
       }
 #pragma unroll
       for (int ks = 0; ks < R / 16; ++ks) gw0 = mfma(fd[ks], fx[ks], gw0);
     }
-    lds_sync();
-    STAMP_AT(9);
   }
 #undef STAMP_AT
 #undef OPAQUE_LANE
+#undef HEAD_DW
+#undef DEFERRED_DW0
 
   // ================= epilogue: one partial-gradient slab per workgroup =================
   tid = tid0;
@@ -1024,11 +1096,11 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   }
 }
 
-template <int H, int ACT, int NA, bool STAMP>
+template <int H, int ACT, int NA, bool STAMP, int SCHED = 0>
 __global__ __launch_bounds__(NT, 1) void fused_update_kernel(FusedArgs q, uint64_t *stamps) {
   __shared__ __attribute__((aligned(16))) char lds[Lds<H, ACT != PPO_ACT_RELU>::TOTAL];
-  if (blockIdx.y == 0) fused_body<H, ACT, NA, true, STAMP>(q, q.net[0], lds, stamps);
-  else fused_body<H, ACT, 1, false, STAMP>(q, q.net[1], lds, stamps);
+  if (blockIdx.y == 0) fused_body<H, ACT, NA, true, STAMP, SCHED>(q, q.net[0], lds, stamps);
+  else fused_body<H, ACT, 1, false, STAMP, SCHED>(q, q.net[1], lds, stamps);
 }
 
 bool fused_width_ok(int hidden) { return hidden == 256; }
@@ -1122,13 +1194,35 @@ int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, 
   return 0;
 }
 
-template <int ACT, int NA>
-static void launch_na(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+// PPO_FUSED_SCHED=0|1|5: the ReLU kernel's phase schedule (fused_body SCHED; A/B knob, bitwise the
+// same gradient for every value), read at every launch so one process can compare them
+static int env_fused_sched() {
+  const char *v = getenv("PPO_FUSED_SCHED");
+  return v ? atoi(v) : 0;
+}
+
+int fused_sched(int act) {
+  const int s = env_fused_sched();
+  return act == PPO_ACT_RELU && (s == 1 || s == 5) ? s : 0;
+}
+
+template <int ACT, int NA, int SCHED>
+static void launch_sched(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   uint64_t *nul = nullptr;
   if (ACT == PPO_ACT_RELU && q.stamps)
-    launch_k(rec, fused_update_kernel<256, ACT, NA, true>, dim3(q.G, 2), dim3(NT), 0, st, q, q.stamps);
+    launch_k(rec, fused_update_kernel<256, ACT, NA, true, SCHED>, dim3(q.G, 2), dim3(NT), 0, st, q, q.stamps);
   else
-    launch_k(rec, fused_update_kernel<256, ACT, NA, false>, dim3(q.G, 2), dim3(NT), 0, st, q, nul);
+    launch_k(rec, fused_update_kernel<256, ACT, NA, false, SCHED>, dim3(q.G, 2), dim3(NT), 0, st, q, nul);
+}
+
+template <int ACT, int NA>
+static void launch_na(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
+  if constexpr (ACT == PPO_ACT_RELU) {
+    const int sched = fused_sched(ACT);
+    if (sched == 1) return launch_sched<ACT, NA, 1>(q, rec, st);
+    if (sched == 5) return launch_sched<ACT, NA, 5>(q, rec, st);
+  }
+  launch_sched<ACT, NA, 0>(q, rec, st);
 }
 
 template <int ACT>

@@ -810,7 +810,8 @@ static int fused_forward_backward(ppo_ctx *ctx, const FusedArgs &q, hipStream_t 
                     4.0 * q.G * static_cast<double>(P) + 2.0 * 2.0 * H * (kFusedKX + 2.0 * H);
   const int na = A <= 2 ? 2 : A <= 4 ? 4 : A <= 6 ? 6 : 8;
   const TimRec rec{KC_FUSED,
-                   tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false>", H, q.act, na)
+                   tim_active() ? intern_name("fused_update_kernel<%d, %d, %d, false, %d>", H, q.act, na,
+                                              fused_sched(q.act))
                                 : nullptr,
                    fl, by};
   return fused_update_launch(q, rec, st);

@@ -829,3 +829,48 @@ def test_fused_direct_records_match_gathered_copy(gpu, with_count):
     e.fused_direct(True)
     for i, (x, y) in enumerate(zip(outs[True], outs[False])):
         assert torch.equal(x, y), (i, int((x != y).sum()))
+
+
+@pytest.mark.parametrize("sched", [1, 5])
+@pytest.mark.parametrize("n,t,b", [(512, 16, 2000), (4096, 32, 65536)])
+def test_fused_schedules_bitwise(gpu, monkeypatch, sched, n, t, b):
+    """PPO_FUSED_SCHED (fused_body SCHED, round 6): the ReLU kernel with dW0 deferred into the next
+    chunk's L1 pass (1) and also the head dW inside the dW1 pass (3) moves wave-local work between
+    phases only -- gradient, losses and the Adam step are bitwise those of schedule 0, from one
+    chunk per workgroup (b = 2000, a partial last chunk) to the headline's eight (b = 65,536)."""
+    run, eng, ref, cfg = _agents(gpu, 15, num_envs=n, hidden=(256, 256), batch_size=b,
+                                 precision="bf16")
+    e = eng.engine
+    assert e.fused
+    g = torch.Generator().manual_seed(9)
+    states = torch.randn(t + 1, n, 17, generator=g).to(gpu)
+    actions = torch.randn(t, n, 6, generator=g).to(gpu)
+    old_lp = torch.randn(t, n, generator=g).to(gpu) - 5
+    adv = torch.randn(t, n, generator=g).to(gpu)
+    vt = torch.randn(t, n, generator=g).to(gpu)
+    rows = [torch.randperm(n * t, generator=g)[:b].to(torch.int32).to(gpu) for _ in range(2)]
+    args = (0.9, 1.1, 1e-4, 1.0 / b, 1.0 / (b * 6))
+    hyper = dict(one_minus_beta1=0.1, beta2=0.999, one_minus_beta2=0.001, eps=1e-8)
+    p0 = eng.flat_params.clone()
+    m0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-3
+    v0 = torch.rand(e.n_params, generator=g).to(gpu) * 1e-6
+    e.stage_records(states, actions, old_lp, adv, vt)
+    outs = {}
+    for s in (0, sched):
+        monkeypatch.setenv("PPO_FUSED_SCHED", str(s))
+        eng.flat_params.copy_(p0)
+        m, v = m0.clone(), v0.clone()
+        e.pack_weights()
+        res = []
+        for k in range(2):
+            grad, loss = torch.empty(e.n_params, device=gpu), torch.empty(2, device=gpu)
+            e.update_step_staged(rows[k], b, grad, loss, m, v, *args, neg_step_actor=-1e-3,
+                                 neg_step_critic=-2e-3, bc2_sqrt=0.3,
+                                 next_rows=rows[1] if k == 0 else None,
+                                 weights_current=k > 0, rows_gathered=k > 0, **hyper)
+            res += [grad.clone(), loss.clone()]
+        torch.cuda.synchronize()
+        outs[s] = res + [eng.flat_params.clone(), m, v]
+    assert bool(torch.isfinite(outs[0][0]).all()) and float(outs[0][0].abs().max()) > 0
+    for i, (x, y) in enumerate(zip(outs[0], outs[sched])):
+        assert torch.equal(x, y), (sched, i, int((x != y).sum()))

@@ -3,6 +3,7 @@
 # stops at the first failing step).  Every GPU step has its own time limit.
 #   tests     pytest -m gpu (K="expr" narrows it with -k)
 #   smoke     __graft_entry__.smoke()
+#   floor     tools/launch_floor: empty / one-load kernels and the GAE scan's bytes at its grid
 #   bench     the default bench line (bf16) -> gpurun_out/bench_$TAG.json (BENCH_ARGS appended)
 #   f32       bench --precision f32 -> gpurun_out/bench_${TAG}_f32.json
 #   host      bench --env host (PCIe-inclusive) -> gpurun_out/bench_${TAG}_host.json
@@ -47,6 +48,14 @@ for S in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 \
         || fail smoke gpurun_out/smoke_${TAG}.log
       tail -2 gpurun_out/smoke_${TAG}.log ;;
+    floor)
+      # the launch / memory floor under the GAE scan (tools/launch_floor.hip): events and rocprofv3
+      timeout -k 10 120 ./tools/launch_floor 400 > gpurun_out/floor_${TAG}.json 2> gpurun_out/floor_${TAG}.err \
+        || fail floor gpurun_out/floor_${TAG}.err
+      cat gpurun_out/floor_${TAG}.json
+      timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_${TAG}_floor -o floor --output-format csv \
+        -- ./tools/launch_floor 400 > gpurun_out/rp_${TAG}_floor.log 2>&1 || fail floortrace gpurun_out/rp_${TAG}_floor.log
+      cat $(find gpurun_out/rp_${TAG}_floor -name "*kernel_stats.csv") ;;
     bench)
       timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
         || fail bench gpurun_out/bench_${TAG}.err
