@@ -426,19 +426,17 @@ __device__ __forceinline__ void mfma16_drain(f32x4 &acc) { asm volatile("s_nop 1
 //          3, and X(c) stays in the second X buffer; phase 7 and the chunk's closing barrier go
 //          away (the last chunk's dW0 runs after the loop).  Same MFMA chain into gw0 in the same
 //          order: bitwise the same gradient.
-//   bit 2  (SCHED 5) the deferred dW0 is issued right AFTER the L1 pass instead of before it, so
-//          its MFMAs overlap the wave's own phase-3 epilogue (bias + act + the a2 stores, VALU /
-//          LDS) rather than the pass's ring loads.
-// Measured and dropped (round 6): the head dW inside phase 6a (a tie) and the next
+// Measured and dropped (round 6): the head dW inside phase 6a (a tie); the next
 // chunk's layer 0 hoisted behind the dgrad pass with phases 0 and 1 removed (16 spilled VGPRs,
-// 10-17 % slower).
+// 10-17 % slower); the deferred dW0 issued after the L1 pass (3 % slower) or without the
+// first-chunk branch (a tie).
 template <int H, int ACT, int NH, bool ACTOR, bool STAMP, int SCHED>
 __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N, char *lds,
                                            uint64_t *stamps) {
   static_assert(H == 32 * NW, "wave w owns feature tile w");
   constexpr bool F32A2 = ACT != PPO_ACT_RELU;
   constexpr bool DEFER_DW0 = (SCHED & 1) && !F32A2;
-  constexpr bool DW0_AFTER = DEFER_DW0 && (SCHED & 4);
+  bool have_prev = false;  // DEFER_DW0: a previous chunk's dW0 is pending
   using L = Lds<H, F32A2>;
   constexpr int z = ACTOR ? 0 : 1;
   char *ximg = lds + L::X;        // this chunk's X image
@@ -539,11 +537,13 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
   const float *const hbias = reinterpret_cast<const float *>(lds + L::HS);
   uint64_t xpre = load_half(blockIdx.x, i_first, tid0, false);
   bool xok = row_ok(blockIdx.x, i_first, tid0);
-  if constexpr (DEFER_DW0) {  // the first deferred dW0 reads these: exact zeros (see phase 2)
+  if constexpr (DEFER_DW0) {
+    // a workgroup without chunks runs the after-loop dW0 on these: exact zeros (the D1 region
+    // and L::X, its `ximg`), so it adds +0 instead of stale LDS contents
     for (int i = tid; i < R * (2 * H) / 16; i += NT)
       *reinterpret_cast<uint4 *>(lds + L::A2 + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
     for (int i = tid; i < R * 64 / 16; i += NT)
-      *reinterpret_cast<uint4 *>(lds + L::X2 + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4 *>(lds + L::X + 16 * i) = make_uint4(0u, 0u, 0u, 0u);
   }
   lds_sync();
 
@@ -647,9 +647,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     OPAQUE_LANE();
     // the previous chunk's dW0 += D1^T X (phase 7 of the undeferred schedule): the wave's own D1
     // columns (untouched until its phase 3 below) and X(c-1); every transposed read first, then
-    // the four chained MFMAs.  Unconditional: before the first chunk the prologue zeroed the
-    // wave's D1 columns and the second X image, so the first chunk adds an exact +0 (no branch,
-    // no register merge).
+    // the four chained MFMAs.
 #define DEFERRED_DW0()                                                     \
   {                                                                        \
     bf16x8 fd[R / 16], fx[R / 16];                                         \
@@ -659,14 +657,16 @@ __device__ __forceinline__ void fused_body(const FusedArgs &q, const FusedNet &N
     }                                                                      \
     _Pragma("unroll") for (int ks = 0; ks < R / 16; ++ks) gw0 = mfma(fd[ks], fx[ks], gw0); \
   }
-    if constexpr (DEFER_DW0 && !DW0_AFTER) DEFERRED_DW0()
+    if constexpr (DEFER_DW0) {
+      if (have_prev) DEFERRED_DW0()  // (a uniform branch: none before the first chunk)
+      have_prev = true;
+    }
     f32x16 a2[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) a2[t][e] = 0.f;
     mlp_pass<H>(w_frag_base<H>(N.w1b, w, lane), a1img, r, h, ring, a2);
-    if constexpr (DW0_AFTER) DEFERRED_DW0()
     *reinterpret_cast<uint64_t *>(lds + L::SROW + tid0 * 8) = sok_c ? srow_c : 0;  // landed during phases 1-2
     STAMP_AT(2);
 
@@ -1194,16 +1194,16 @@ int step_tail_launch(const ReduceArgs &r, const TailArgs &t, const TimRec &rec, 
   return 0;
 }
 
-// PPO_FUSED_SCHED=0|1|5: the ReLU kernel's phase schedule (fused_body SCHED; A/B knob, bitwise the
+// PPO_FUSED_SCHED=0|1: the ReLU kernel's phase schedule (fused_body SCHED; A/B knob, bitwise the
 // same gradient for every value), read at every launch so one process can compare them
 static int env_fused_sched() {
   const char *v = getenv("PPO_FUSED_SCHED");
-  return v ? atoi(v) : 0;
+  return v ? atoi(v) : 1;  // default: dW0 deferred (round 6: 1-4 % faster per launch, bitwise equal)
 }
 
 int fused_sched(int act) {
   const int s = env_fused_sched();
-  return act == PPO_ACT_RELU && (s == 1 || s == 5) ? s : 0;
+  return act == PPO_ACT_RELU && s == 1 ? 1 : 0;
 }
 
 template <int ACT, int NA, int SCHED>
@@ -1220,7 +1220,6 @@ static void launch_na(const FusedArgs &q, const TimRec &rec, hipStream_t st) {
   if constexpr (ACT == PPO_ACT_RELU) {
     const int sched = fused_sched(ACT);
     if (sched == 1) return launch_sched<ACT, NA, 1>(q, rec, st);
-    if (sched == 5) return launch_sched<ACT, NA, 5>(q, rec, st);
   }
   launch_sched<ACT, NA, 0>(q, rec, st);
 }

@@ -831,7 +831,7 @@ def test_fused_direct_records_match_gathered_copy(gpu, with_count):
         assert torch.equal(x, y), (i, int((x != y).sum()))
 
 
-@pytest.mark.parametrize("sched", [1, 5])
+@pytest.mark.parametrize("sched", [1])
 @pytest.mark.parametrize("n,t,b", [(512, 16, 2000), (4096, 32, 65536)])
 def test_fused_schedules_bitwise(gpu, monkeypatch, sched, n, t, b):
     """PPO_FUSED_SCHED (fused_body SCHED, round 6): the ReLU kernel with dW0 deferred into the next
