@@ -200,6 +200,21 @@ __global__ __launch_bounds__(EB * 16) void gae_pipe_kernel(const float *__restri
                               lg_f, adv, vtarget, em);
 }
 
+// Producer / consumer variant (gae_pipe.h gae_chain_body): EB*16 producer threads + one chain wave.
+template <typename RT, int EB, int KMAX>
+__global__ __launch_bounds__(EB * 16 + 64) void gae_chain_kernel(const float *__restrict__ value,
+                                                                 const float *__restrict__ next_value,
+                                                                 const RT *__restrict__ reward,
+                                                                 const uint8_t *__restrict__ done,
+                                                                 const uint8_t *__restrict__ term,
+                                                                 int force_last, int n, int t_len,
+                                                                 float gamma_f, float lg_f,
+                                                                 float *__restrict__ adv,
+                                                                 float *__restrict__ vtarget) {
+  gae_chain_body<RT, EB, KMAX>(value, next_value, reward, done, term, force_last, n, t_len, gamma_f,
+                               lg_f, adv, vtarget);
+}
+
 // ============================================================================================
 // Per-env standardisation over T (ppo.py:66-69 rewards f64, :81-88 advantage / value target f32)
 // x <- ((x - mean_T) / std_T) * scale, unbiased std.  torch computes mean in the tensor dtype and
@@ -575,10 +590,42 @@ extern "C" int ppo_gae(const float *value_d, const float *next_value_d, const vo
   while (eb > 1 && (static_cast<size_t>(t) * eb * per_elem > 131072 || t * eb > 16 * 256))
     eb >>= 1;
   const size_t shm = static_cast<size_t>(t) * eb * per_elem + 16;
-  static const int kind = [] {  // PPO_GAE_KERNEL=reg / lds forces the register-chunked / the
-    const char *v = getenv("PPO_GAE_KERNEL");  // whole-tile LDS scan (experiments)
-    return (v && v[0] == 'r') ? 1 : ((v && v[0] == 'l') ? 2 : ((v && v[0] == 'p') ? 3 : 0));
-  }();
+  // PPO_GAE_KERNEL=reg / lds / pipe / chain forces the register-chunked, the whole-tile LDS, the
+  // pipelined or the producer/consumer scan (experiments; read per call)
+  const char *kv = getenv("PPO_GAE_KERNEL");
+  const int kind = (kv && kv[0] == 'r') ? 1 : (kv && kv[0] == 'l') ? 2 : (kv && kv[0] == 'p') ? 3
+                 : (kv && kv[0] == 'c') ? 4 : 0;
+  // the producer / consumer scan is opt-in (PPO_GAE_KERNEL=chain): at N = 4096, T = 128 it ties the
+  // pipelined scan by the engine's events (5.77 vs 5.80 us; rocprofv3 5.44 vs 5.72) and is slower
+  // from 16384 envs (15.3 vs 12.8 us) -- tools/gae_sizes.py, profiles/r06
+  if (kind == 4 && t <= 16 * 16) {
+    // producer / consumer scan: 16 envs per block (32 from N = 16384 at T <= 128: every chunk's
+    // delta / discount stays LDS-resident), + one chain wave
+    const int peb = (n >= 16384 && t <= 16 * 8) ? 32 : 16;
+    hipStream_t st = as_stream(stream);
+    FreeTimingScope timing_scope;
+    auto go = [&](auto rt_tag, auto eb_tag, auto k_tag) {
+      using RT = decltype(rt_tag);
+      constexpr int EB = decltype(eb_tag)::value, KM = decltype(k_tag)::value;
+      const TimRec rec{KC_GAE,
+                       tim_active() ? intern_name("gae_chain_kernel<%s, %d, %d>",
+                                                  sizeof(RT) == 8 ? "double" : "float", EB, KM)
+                                    : nullptr,
+                       0.0, gae_bytes(sizeof(RT), done_d != nullptr, n, t)};
+      launch_k(rec, gae_chain_kernel<RT, EB, KM>, dim3(ceil_div(n, EB)), dim3(EB * 16 + 64), 0, st,
+               value_d, next_value_d, static_cast<const RT *>(reward_d), done_d, terminated_d,
+               force_last_done, n, t, gamma_f, lg_f, adv_d, vtarget_d);
+    };
+    auto by_eb = [&](auto rt_tag) {
+      if (t > 16 * 8) go(rt_tag, std::integral_constant<int, 16>{}, std::integral_constant<int, 16>{});
+      else if (peb == 16) go(rt_tag, std::integral_constant<int, 16>{}, std::integral_constant<int, 8>{});
+      else go(rt_tag, std::integral_constant<int, 32>{}, std::integral_constant<int, 8>{});
+    };
+    if (reward_is_f64) by_eb(double{});
+    else by_eb(float{});
+    PPO_LAUNCHED();
+    return 0;
+  }
   if ((kind == 0 || kind == 3) && t <= 16 * 16) {
     // pipelined scan: 16 envs per block (>= 256 blocks at N = 4096), 32 from N = 16384.
     // Measured (tools/gae_sweep.py, per-dispatch events, T = 128): N = 4096 6.2 us (LDS-staged

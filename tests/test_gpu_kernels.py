@@ -20,10 +20,15 @@ def _E():
 
 
 # ---------------------------------------------------------------------------------- GAE (A7/A8)
+@pytest.mark.parametrize("kernel", ["pipe", "chain"])
 @pytest.mark.parametrize("n,t,p_term,reward_f64", [(8, 16, 0.1, True), (257, 33, 0.05, True),
                                                    (4096, 128, 0.0, True), (1000, 64, 0.2, False),
-                                                   (3, 1, 0.5, True)])
-def test_gae_bit_exact(gpu, n, t, p_term, reward_f64):
+                                                   (3, 1, 0.5, True), (16384, 128, 0.01, True),
+                                                   (100, 200, 0.02, True)])
+def test_gae_bit_exact(gpu, monkeypatch, n, t, p_term, reward_f64, kernel):
+    """kernel: the pipelined scan (gae_pipe_kernel, the default) or the producer / consumer one
+    (gae_chain_kernel, opt-in) -- both bit-exact against the oracle's f64 recurrence."""
+    monkeypatch.setenv("PPO_GAE_KERNEL", kernel)
     E = _E()
     g = torch.Generator().manual_seed(n * 7 + t)
     v = torch.randn(n, t, 1, generator=g)
@@ -42,7 +47,9 @@ def test_gae_bit_exact(gpu, n, t, p_term, reward_f64):
     assert torch.equal(vt.t().cpu(), vt_ref[..., 0]), "GAE value target not bit-exact"
 
 
-def test_gae_explicit_done_and_nan_propagation(gpu):
+@pytest.mark.parametrize("kernel", ["pipe", "chain"])
+def test_gae_explicit_done_and_nan_propagation(gpu, monkeypatch, kernel):
+    monkeypatch.setenv("PPO_GAE_KERNEL", kernel)
     E = _E()
     n, t = 64, 20
     g = torch.Generator().manual_seed(1)

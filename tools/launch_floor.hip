@@ -66,6 +66,26 @@ __global__ __launch_bounds__(EB * 16) void scanbytes_kernel(const float *__restr
   }
 }
 
+// the GAE recurrence's dependent chain alone: STEPS x (v_mul_f64, v_add_f64) on registers, one
+// wave per block, 16 active lanes -- its duration minus the empty kernel's is the chain latency
+template <int STEPS>
+__global__ __launch_bounds__(64) void chain_kernel(const double *__restrict__ dq, double *__restrict__ out) {
+  const int lane = threadIdx.x;
+  if (lane >= 16) return;
+  double d[16], q[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    d[j] = dq[2 * j];
+    q[j] = dq[2 * j + 1];
+  }
+  double prev = 0.0;
+  for (int s = 0; s < STEPS / 16; ++s) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) prev = d[j] + prev * q[j];
+  }
+  out[blockIdx.x * 16 + lane] = prev;
+}
+
 struct Bufs {
   float *v, *vn, *adv, *vt, *in, *out;
   double *r;
@@ -124,6 +144,17 @@ int main(int argc, char **argv) {
            bytes > 0 ? bytes / us * 1e-3 / 8000.0 : 0.0);
     first = false;
   };
+  {
+    double *dq, *o;
+    CK(hipMalloc(&dq, 64 * 8));
+    CK(hipMalloc(&o, 1 << 20));
+    std::vector<double> h(64);
+    for (int i = 0; i < 64; ++i) h[i] = (i & 1) ? 0.97 : 0.01 * i;
+    CK(hipMemcpy(dq, h.data(), 64 * 8, hipMemcpyHostToDevice));
+    emit("chain_kernel<128>", 0, 256, 64, time_us(chain_kernel<128>, 256, 64, reps, (const double *)dq, o), 0.0);
+    emit("chain_kernel<1024>", 0, 256, 64, time_us(chain_kernel<1024>, 256, 64, reps, (const double *)dq, o), 0.0);
+    emit("chain_kernel<8192>", 0, 256, 64, time_us(chain_kernel<8192>, 256, 64, reps, (const double *)dq, o), 0.0);
+  }
   for (int n : {4096, 16384, 65536}) {
     const int grid = n / 16;
     const double bytes = 25.0 * n * T;
