@@ -29,7 +29,10 @@
 // In bf16 mode the producers of the operands only GEMMs read -- the gathered states, h_prev and
 // dG -- write them as bf16 (the RNE rounding the GEMM would apply while staging), so the
 // weight-gradient, recurrent-gradient and input-gradient GEMMs move half the bytes; the bias
-// gradients (column sums of dG) are then sums of those bf16 values.
+// gradients (column sums of dG) are then sums of those bf16 values.  The gate activations stay
+// f32: stored as bf16 (measured, round 6) the sigmoid derivative y (1 - y) of a saturated gate
+// loses its digits (bf16's spacing below 1 is 2^-8), which moved the BiLSTM weight gradients by
+// 0.02-6.5 % (relative L2; latent 64, W = 3) in the bf16 emulation.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -156,26 +159,46 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
 // needs no exchange).  Bitwise the layered result: the operands rounded to bf16 (RNE) as staged,
 // the K order of gemm_bf16_kernel (k-steps of 16 in order into one v_mfma_f32_32x32x16_bf16
 // accumulator), gh = acc + b_hh, then pre = gh + Gx and the same cell arithmetic.
-constexpr int kStepRows = 64, kStepUnits = 64, kStepBK = 32;
+constexpr int kStepUnits = 64, kStepBK = 32;
+constexpr int kStepRowsMb = 128;  // rows per workgroup of the minibatch step launches
 struct StepArgs {
   CellArgs cell;
   const float *whh[2];  // W_hh per direction, [4H][H] f32 (torch layout)
   const __bf16 *whh16[2];  // W16 instantiation: the same rows as bf16 (the ctx's weight copy)
+  // FX instantiation (layer 0): the input projection Gx = x_t W_ih^T + b_ih in the same launch,
+  // from the bf16 window rows ([B*W][ldx], row b*W + t) and the W_ih images ([4H][ldx])
+  const __bf16 *x16;
+  const __bf16 *wih16[2];
+  const float *b_ih[2];
+  int ldx;
 };
 
 typedef __bf16 lstm_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
 
-template <bool W16>
+// FX (W16 only): the step also computes its own input projection -- Gx of row t never goes to
+// HBM.  Phase X accumulates x_t W_ih^T over the ldx k-columns (k-steps of 16 in order, one
+// v_mfma_f32_32x32x16_bf16 accumulator per gate: wide_gemm.h's WK_F32 order over the same bf16
+// operands), adds b_ih (its epilogue's f32 add) and keeps the result in registers; phase H is the
+// recurrent projection as above (skipped at s = 0, where h_prev = c_prev = 0).  Bitwise the
+// projection GEMM + step pair.
+//
+// ROWS rows x 64 units per workgroup, ROWS / 32 x 2 waves (a wave: 32 rows x 32 units x 4 gates).
+// Every workgroup streams the whole 256 x K weight panel of its 64 units, so the panel traffic
+// per launch is (b / ROWS) x 2 x 4H x K x 2 B: 128-row workgroups halve it against 64.
+template <bool W16, bool FX, int ROWS, bool PF2>
 __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
+  static_assert(ROWS == 64 || ROWS == 128, "step rows");
+  constexpr int NT = 4 * ROWS, RT = ROWS / 32;    // threads, row tiles
+  constexpr int NB = 2048 / NT;                   // B staging items per thread
   constexpr int AP = kStepBK + 8;                 // bf16 image row pitch (16 B of padding)
-  constexpr int AIMG = kStepRows * AP, BIMG = 4 * kStepUnits * AP;
+  constexpr int AIMG = ROWS * AP, BIMG = 4 * kStepUnits * AP;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * (AIMG + BIMG)];
   const CellArgs &c = q.cell;
   const int H = c.h, W = c.w;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int mt = wv & 1, ug = wv >> 1;
-  const int r0 = blockIdx.x * kStepRows, j0 = blockIdx.y * kStepUnits, d = blockIdx.z;
+  const int mt = wv % RT, ug = wv / RT;
+  const int r0 = blockIdx.x * ROWS, j0 = blockIdx.y * kStepUnits, d = blockIdx.z;
   const int t = d == 0 ? c.s : W - 1 - c.s;
   const int tp = d == 0 ? t - 1 : t + 1;
   const float *arow = c.y + static_cast<int64_t>(tp) * 2 * H + d * H;  // + row * W * 2H + k
@@ -184,40 +207,46 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   const __bf16 *arow16 = W16 ? c.hp16 + static_cast<int64_t>(t) * 2 * H + d * H : nullptr;
   const int64_t lda = static_cast<int64_t>(W) * 2 * H;
   const float *wb = q.whh[d];
+  const bool first = c.s == 0;
 
-  // staging: A 64 rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63) x
-  // 32 k (8 float4 per thread); rows past b load row b-1 (clamped, results discarded)
-  float4 va[2], vb[8];
-  uint2 va16[2], vb16[8];
+  // staging: A ROWS rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63)
+  // x 32 k (NB float4 per thread); rows past b load row b-1 (clamped, results discarded).  W16:
+  // the phase's bf16 operands (A rows at pa + row * pla, B rows at pb + n * plb)
+  float4 va[2], vb[NB];
+  uint2 va16[2], vb16[NB];
   const __bf16 *wb16 = W16 ? q.whh16[d] : nullptr;
+  const __bf16 *pa = arow16, *pb = wb16;
+  int64_t pla = lda, plb = H;
   auto gload = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
       const int row = min(r0 + rr, c.b - 1);
-      if constexpr (W16) va16[u] = *reinterpret_cast<const uint2 *>(arow16 + row * lda + k0 + kk);
+      if constexpr (W16) va16[u] = *reinterpret_cast<const uint2 *>(pa + row * pla + k0 + kk);
       else va[u] = *reinterpret_cast<const float4 *>(arow + row * lda + k0 + kk);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
       const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
-      const int64_t off = static_cast<int64_t>(gate * H + j0 + jj) * H + k0 + kk;
-      if constexpr (W16) vb16[u] = *reinterpret_cast<const uint2 *>(wb16 + off);
-      else vb[u] = *reinterpret_cast<const float4 *>(wb + off);
+      if constexpr (W16) {
+        vb16[u] = *reinterpret_cast<const uint2 *>(pb + static_cast<int64_t>(gate * H + j0 + jj) * plb + k0 + kk);
+      } else {
+        vb[u] = *reinterpret_cast<const float4 *>(wb + static_cast<int64_t>(gate * H + j0 + jj) * H + k0 + kk);
+      }
     }
   };
   auto lstore = [&](int buf) {
     __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int e = tid + 256 * u, rr = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
       *reinterpret_cast<uint2 *>(ai + rr * AP + kk) =
           W16 ? va16[u] : make_uint2(pack_bf16x2(va[u].x, va[u].y), pack_bf16x2(va[u].z, va[u].w));
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, nn = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
       *reinterpret_cast<uint2 *>(bi + nn * AP + kk) =
           W16 ? vb16[u] : make_uint2(pack_bf16x2(vb[u].x, vb[u].y), pack_bf16x2(vb[u].z, vb[u].w));
     }
@@ -228,13 +257,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[g][e] = 0.f;
-  const int nk = H / kStepBK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * kStepBK);
+  auto mfma_tile = [&](int cur) {
     const __bf16 *ai = lds + cur * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
     for (int ks = 0; ks < kStepBK / 16; ++ks) {
@@ -247,15 +270,103 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
+  };
+  // W16: two register sets, tile i's loads in set i % 2 issued two tiles ahead of its LDS store
+  // (one tile's MFMA + barrier more to land than a single set gives: the loop is load-latency
+  // bound at two waves per SIMD); the same tiles in the same order
+  uint2 sa0[2], sb0[NB], sa1[2], sb1[NB];
+  auto gl16 = [&](int k0, uint2(&ra)[2], uint2(&rb)[NB]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+      const int row = min(r0 + rr, c.b - 1);
+      ra[u] = *reinterpret_cast<const uint2 *>(pa + row * pla + k0 + kk);
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
+      rb[u] = *reinterpret_cast<const uint2 *>(pb + static_cast<int64_t>(gate * H + j0 + jj) * plb + k0 + kk);
+    }
+  };
+  auto ls16 = [&](int buf, const uint2(&ra)[2], const uint2(&rb)[NB]) {
+    __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+      *reinterpret_cast<uint2 *>(ai + rr * AP + kk) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      *reinterpret_cast<uint2 *>(bi + nn * AP + kk) = rb[u];
+    }
+  };
+  auto kloop = [&](int nk) {
+    if constexpr (W16 && PF2) {
+      gl16(0, sa0, sb0);
+      if (nk > 1) gl16(kStepBK, sa1, sb1);
+      ls16(0, sa0, sb0);
+      if (nk > 2) gl16(2 * kStepBK, sa0, sb0);
+      __syncthreads();
+      for (int kt = 0; kt < nk; kt += 2) {
+        mfma_tile(0);  // tile kt
+        if (kt + 1 < nk) {
+          ls16(1, sa1, sb1);
+          if (kt + 3 < nk) gl16((kt + 3) * kStepBK, sa1, sb1);
+        }
+        __syncthreads();
+        if (kt + 1 >= nk) break;
+        mfma_tile(1);  // tile kt + 1
+        if (kt + 2 < nk) {
+          ls16(0, sa0, sb0);
+          if (kt + 4 < nk) gl16((kt + 4) * kStepBK, sa0, sb0);
+        }
+        __syncthreads();
+      }
+    } else {
+      gload(0);
+      lstore(0);
+      __syncthreads();
+      int cur = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) gload((kt + 1) * kStepBK);
+        mfma_tile(cur);
+        if (kt + 1 < nk) lstore(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+      }
+    }
+  };
+
+  const int j = j0 + 32 * ug + (lane & 31);
+  // FX phase X: Gx of the lane's (row, unit) for all four gates, + b_ih, held in gxr
+  lstm_f32x16 gxr[4];
+  if constexpr (FX) {
+    pa = q.x16 + static_cast<int64_t>(t) * q.ldx;
+    pla = static_cast<int64_t>(W) * q.ldx;
+    pb = q.wih16[d];
+    plb = q.ldx;
+    kloop(q.ldx / kStepBK);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float bi = q.b_ih[d][g * H + j];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        gxr[g][e] = acc[g][e] + bi;
+        acc[g][e] = 0.f;
+      }
+    }
+    pa = arow16;
+    pla = lda;
+    pb = wb16;
+    plb = H;
   }
+  if (!FX || !first) kloop(H / kStepBK);
 
   // epilogue: C row (r&3) + 8 (r>>2) + 4 (lane>>5) of the wave's 32 rows, unit j = lane & 31.
   // Eight rows at a time, every load first and unconditional (rows past b read row b-1): a load
   // behind the row test made each row wait a memory round trip of its own.
-  const int j = j0 + 32 * ug + (lane & 31);
   float bh[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bh[g] = c.b_hh[d][g * H + j];
@@ -267,11 +378,16 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       const int e = e0 + u;
       const int64_t bb = r0 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
       const int64_t bc = bb < c.b ? bb : c.b - 1;
-      const float *g = c.g + (bc * W + t) * (8 * H) + d * (4 * H);
+      if constexpr (FX) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gx[u][k] = g[k * H + j];
-      const int64_t op = (bc * W + tp) * (2 * H) + d * H + j;
-      cpv[u] = c.c[op];
+        for (int k = 0; k < 4; ++k) gx[u][k] = gxr[k][e];
+      } else {
+        const float *g = c.g + (bc * W + t) * (8 * H) + d * (4 * H);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gx[u][k] = g[k * H + j];
+      }
+      const int64_t op = (bc * W + (first ? t : tp)) * (2 * H) + d * H + j;
+      cpv[u] = first ? 0.f : c.c[op];
       if constexpr (!W16) hpv[u] = c.y[op];
     }
 #pragma unroll
@@ -281,8 +397,13 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       if (bb >= c.b) continue;
       float *g = c.g + (bb * W + t) * (8 * H) + d * (4 * H);
       float pre[4];
+      if (FX && first) {  // lstm_cell_fwd_kernel's first step: b_hh + Gx
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pre[k] = (acc[k][e] + bh[k]) + gx[u][k];  // gh.add_(igates)
+        for (int k = 0; k < 4; ++k) pre[k] = bh[k] + gx[u][k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pre[k] = (acc[k][e] + bh[k]) + gx[u][k];  // gh.add_(igates)
+      }
       const int64_t o = (bb * W + t) * (2 * H) + d * H + j;
       const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), gg = tanhf(pre[2]),
                   og = sigmoidf_(pre[3]);
@@ -295,7 +416,8 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       c.c[o] = cn;
       c.y[o] = h;
       if constexpr (W16) {
-        // row t's h_prev is already there; h goes to the next step's row
+        // row t's h_prev is already there (FX, first step: zeros); h goes to the next step's row
+        if (FX && first) c.hp16[o] = static_cast<__bf16>(0.f);
         if (c.s + 1 < W) {
           const int tn = d == 0 ? t + 1 : t - 1;
           c.hp16[(bb * W + tn) * (2 * H) + d * H + j] = static_cast<__bf16>(h);
@@ -312,13 +434,18 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
 }
 
 template <bool W16>
-__global__ __launch_bounds__(256) void lstm_step_fwd_kernel(StepArgs q) {
-  lstm_step_fwd_body<W16>(q);
+__global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwd_kernel(StepArgs q) {
+  lstm_step_fwd_body<W16, false, kStepRowsMb, W16>(q);
 }
-// the rollout's launches (1,024-row windows): the same body under its own name, so the traffic /
-// roofline rows of the minibatch kernel stay per-launch comparable
+// the rollout's launches (1,024-row windows, 64-row workgroups: 8 x more of them than rows / 128
+// would give): the same body under its own name, so the traffic / roofline rows of the minibatch
+// kernel stay per-launch comparable
 __global__ __launch_bounds__(256) void lstm_step_fwd_rollout_kernel(StepArgs q) {
-  lstm_step_fwd_body<true>(q);
+  lstm_step_fwd_body<true, false, 64, false>(q);
+}
+// layer 0 with the input projection in the step (FX), minibatch launches
+__global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwdx_kernel(StepArgs q) {
+  lstm_step_fwd_body<true, true, kStepRowsMb, true>(q);
 }
 
 struct CellBwdArgs {
@@ -726,6 +853,13 @@ const int g_lstm_splits = [] {
   return (n == 8 || n == 16) ? n : 32;
 }();
 
+// PPO_LSTM_FUSEX=0: layer 0's input projection as its own GEMM (read per call: the bitwise test
+// flips it)
+bool lstm_fusex_env() {
+  const char *v = getenv("PPO_LSTM_FUSEX");
+  return !(v && atoi(v) == 0);
+}
+
 struct TimingScope {
   explicit TimingScope(ppo_lstm_ctx *x) { g_tim = x->tim.on ? &x->tim : nullptr; }
   ~TimingScope() { g_tim = nullptr; }
@@ -844,7 +978,17 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
       p[d].m = b * W;
       p[d].n = 4 * H;
     }
-    if (l == 0 && xin16 && x->w16 && (4 * H) % 128 == 0) {
+    const bool fused_step = x->prec == PPO_PREC_BF16 && x->fused_step && H % kStepUnits == 0;
+    // layer 0 of a bf16 step with the padded bf16 rows: the input projection inside each step's
+    // launch (lstm_step_fwdx_kernel) instead of one Gx GEMM whose f32 output ([B*W][8H]) every
+    // step reads back; PPO_LSTM_FUSEX=0 keeps the GEMM
+    // step launch (the rollout's 1,024-row windows keep the GEMM: 5x the rows per launch fill the
+    // GPU where one step's 1,024 rows do not)
+    const bool fusex = fused_step && l == 0 && xin16 && x->w16 && !x->rollout &&
+                       (4 * H) % 128 == 0 && x->ldx16 % kStepBK == 0 && lstm_fusex_env();
+    if (fusex) {
+      // no separate projection: lstm_step_fwdx_kernel below
+    } else if (l == 0 && xin16 && x->w16 && (4 * H) % 128 == 0) {
       // the bf16 minibatch rows (padded to 64-deep k-tiles) through the wide path's LDS-DMA GEMM
       // into f32 Gx + b_ih: the same k-steps in the same order over the same bf16 operands (zeros
       // past O), the bias added as the layered epilogue adds it -- bitwise gemm_bf16_kernel's Gx
@@ -866,9 +1010,8 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
     } else if (int rc = gemm_fwd(x, p, 2, L.in, b * W, 4 * H, PPO_ACT_IDENTITY, false, st)) {
       return rc;
     }
-    const bool fused_step = x->prec == PPO_PREC_BF16 && x->fused_step && H % kStepUnits == 0;
     for (int s = 0; s < W; ++s) {
-      if (s > 0 && fused_step) {
+      if ((s > 0 || fusex) && fused_step) {
         StepArgs a{};
         a.cell.g = x->g[z][l];
         a.cell.b_hh[0] = P + L.b_hh[0];
@@ -887,6 +1030,30 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         a.cell.s = s;
         a.whh[0] = P + L.w_hh[0];
         a.whh[1] = P + L.w_hh[1];
+        const dim3 grid(ceil_div(b, kStepRowsMb), H / kStepUnits, 2), block(4 * kStepRowsMb);
+        const dim3 grid_r(ceil_div(b, 64), H / kStepUnits, 2);  // the rollout kernel's 64 rows
+        if (fusex) {
+          const int ldx = x->ldx16;
+          for (int d = 0; d < 2; ++d) {
+            a.whh16[d] = x->w16 + L.w_hh[d];
+            a.wih16[d] = x->wih16[z][d];
+            a.b_ih[d] = ih_bias(x, L, d);
+          }
+          a.x16 = xin16;
+          a.ldx = ldx;
+          TimRec rec{KC_LSTM, "lstm_step_fwdx_kernel", 0.0, 0.0};
+          if (tim_active()) {
+            const double kk = ldx + (s > 0 ? H : 0);
+            rec.flops = 2.0 * 2 * b * 4.0 * H * kk;
+            // W_ih (and W_hh) images and the bf16 rows in; gates / c / h out (f32) and the next
+            // row's bf16 h_prev; s > 0: the staged bf16 h_prev and c_prev in
+            rec.bytes = 2.0 * 4 * H * ldx * 2 + 2.0 * b * ldx * 2 + 2.0 * b * H * (4.0 * 6 + 2.0) +
+                        (s > 0 ? 2.0 * 4 * H * H * 2 + 2.0 * b * H * (2.0 + 4.0) : 0.0);
+          }
+          launch_k(rec, lstm_step_fwdx_kernel, grid, block, 0, st, a);
+          PPO_LAUNCHED();
+          continue;
+        }
         // the launched instantiation's name (rocprof's, for the traffic table)
         TimRec rec{KC_LSTM,
                    x->w16 ? (x->rollout ? "lstm_step_fwd_rollout_kernel" : "lstm_step_fwd_kernel<true>")
@@ -900,14 +1067,13 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
                              : 4.0 * 2 * 4.0 * H * H +
                                    2.0 * b * H * (4.0 * (1 + 4 + 2 + 4 + 2) + (b16 ? 2.0 : 4.0));
         }
-        const dim3 grid(ceil_div(b, kStepRows), H / kStepUnits, 2);
         if (x->w16) {
           a.whh16[0] = x->w16 + L.w_hh[0];
           a.whh16[1] = x->w16 + L.w_hh[1];
-          if (x->rollout) launch_k(rec, lstm_step_fwd_rollout_kernel, grid, dim3(256), 0, st, a);
-          else launch_k(rec, lstm_step_fwd_kernel<true>, grid, dim3(256), 0, st, a);
+          if (x->rollout) launch_k(rec, lstm_step_fwd_rollout_kernel, grid_r, dim3(256), 0, st, a);
+          else launch_k(rec, lstm_step_fwd_kernel<true>, grid, block, 0, st, a);
         } else {
-          launch_k(rec, lstm_step_fwd_kernel<false>, grid, dim3(256), 0, st, a);
+          launch_k(rec, lstm_step_fwd_kernel<false>, grid, block, 0, st, a);
         }
         PPO_LAUNCHED();
         continue;

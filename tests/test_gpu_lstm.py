@@ -362,11 +362,15 @@ def test_lstm_bf16_iteration_matches_bf16_emulation(gpu):
                   update_bar=1e-4, bf16_fn=L.use_bf16_gemms, label="lstm bf16")
 
 
-def test_fused_forward_step_bitwise_equals_layered(gpu):
+@pytest.mark.parametrize("fusex", ["1", "0"])
+def test_fused_forward_step_bitwise_equals_layered(gpu, monkeypatch, fusex):
     """bf16 mode: the forward steps s > 0 as one lstm_step_fwd_kernel launch (recurrent projection
     on MFMA, the cell in its epilogue) reproduce the layered projection GEMM + cell kernel bitwise
     -- forward outputs and the whole minibatch gradient -- on the main.py network (latent 256,
-    W = 5); 200 rows, so the last 64-row block is partial."""
+    W = 5); 200 rows, so the last 64-row block is partial.  fusex 1 (the default): layer 0's input
+    projection inside every step's launch (lstm_step_fwdx_kernel, s = 0 included); 0: its own
+    GEMM."""
+    monkeypatch.setenv("PPO_LSTM_FUSEX", fusex)
     obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
     b = 200
     agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=24)
