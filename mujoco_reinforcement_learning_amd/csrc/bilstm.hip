@@ -86,6 +86,8 @@ struct CellArgs {
   float *hp;           // [B*W][2H] h_prev (zeros at each direction's first step)
   __bf16 *hp16;        // bf16 mode: h_prev as bf16 instead (the dW_hh GEMM's only operand use)
   float *feat;         // optional act(h): mode 1 -> [B*W][2H] (actor), mode 2 -> [B][2H] at t=W-1
+  __bf16 *feat16;      // mode 1, nullable: act(h) as bf16 here instead of feat (bf16 ReLU nets:
+                       // the actor MLPs' GEMMs read the features only as RNE bf16)
   int feat_mode, act;
   int b, w, h, s;
 };
@@ -144,7 +146,11 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
     }
   } else
     *reinterpret_cast<float4 *>(q.hp + o) = hp4;
-  if (q.feat_mode == 1 || (q.feat_mode == 2 && t == W - 1)) {
+  if (q.feat_mode == 1 && q.feat16) {
+    *reinterpret_cast<uint2 *>(q.feat16 + o) =
+        make_uint2(pack_bf16x2(act_forward(h[0], q.act), act_forward(h[1], q.act)),
+                   pack_bf16x2(act_forward(h[2], q.act), act_forward(h[3], q.act)));
+  } else if (q.feat_mode == 1 || (q.feat_mode == 2 && t == W - 1)) {
     float *f = q.feat_mode == 1 ? q.feat + o : q.feat + b * (2 * H) + d * H + j;
     *reinterpret_cast<float4 *>(f) = make_float4(act_forward(h[0], q.act), act_forward(h[1], q.act),
                                                  act_forward(h[2], q.act), act_forward(h[3], q.act));
@@ -190,8 +196,12 @@ template <bool W16, bool FX, int ROWS, bool PF2>
 __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   static_assert(ROWS == 64 || ROWS == 128, "step rows");
   constexpr int NT = 4 * ROWS, RT = ROWS / 32;    // threads, row tiles
-  constexpr int NB = 2048 / NT;                   // B staging items per thread
-  constexpr int AP = kStepBK + 8;                 // bf16 image row pitch (16 B of padding)
+  // k-tile depth (64 for the prefetching loop measured: its two staging sets then need 123 VGPRs
+  // of spill in lstm_step_fwdx_kernel)
+  constexpr int BK = kStepBK;
+  constexpr int IPR = BK / 4;                     // 4-element staging items per operand row
+  constexpr int NA = IPR * ROWS / NT, NB = 256 * IPR / NT;  // A / B staging items per thread
+  constexpr int AP = BK + 8;                      // bf16 image row pitch (16 B of padding)
   constexpr int AIMG = ROWS * AP, BIMG = 4 * kStepUnits * AP;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * (AIMG + BIMG)];
   const CellArgs &c = q.cell;
@@ -212,22 +222,22 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   // staging: A ROWS rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63)
   // x 32 k (NB float4 per thread); rows past b load row b-1 (clamped, results discarded).  W16:
   // the phase's bf16 operands (A rows at pa + row * pla, B rows at pb + n * plb)
-  float4 va[2], vb[NB];
-  uint2 va16[2], vb16[NB];
+  float4 va[NA], vb[NB];
+  uint2 va16[NA], vb16[NB];
   const __bf16 *wb16 = W16 ? q.whh16[d] : nullptr;
   const __bf16 *pa = arow16, *pb = wb16;
   int64_t pla = lda, plb = H;
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + NT * u, rr = e / IPR, kk = (e % IPR) * 4;
       const int row = min(r0 + rr, c.b - 1);
       if constexpr (W16) va16[u] = *reinterpret_cast<const uint2 *>(pa + row * pla + k0 + kk);
       else va[u] = *reinterpret_cast<const float4 *>(arow + row * lda + k0 + kk);
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, nn = e / IPR, kk = (e % IPR) * 4;
       const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
       if constexpr (W16) {
         vb16[u] = *reinterpret_cast<const uint2 *>(pb + static_cast<int64_t>(gate * H + j0 + jj) * plb + k0 + kk);
@@ -239,14 +249,14 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   auto lstore = [&](int buf) {
     __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + NT * u, rr = e / IPR, kk = (e % IPR) * 4;
       *reinterpret_cast<uint2 *>(ai + rr * AP + kk) =
           W16 ? va16[u] : make_uint2(pack_bf16x2(va[u].x, va[u].y), pack_bf16x2(va[u].z, va[u].w));
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, nn = e / IPR, kk = (e % IPR) * 4;
       *reinterpret_cast<uint2 *>(bi + nn * AP + kk) =
           W16 ? vb16[u] : make_uint2(pack_bf16x2(vb[u].x, vb[u].y), pack_bf16x2(vb[u].z, vb[u].w));
     }
@@ -260,7 +270,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   auto mfma_tile = [&](int cur) {
     const __bf16 *ai = lds + cur * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
-    for (int ks = 0; ks < kStepBK / 16; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       const lstm_bf16x8 a = *reinterpret_cast<const lstm_bf16x8 *>(
           ai + (32 * mt + (lane & 31)) * AP + 16 * ks + 8 * (lane >> 5));
 #pragma unroll
@@ -274,53 +284,53 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   // W16: two register sets, tile i's loads in set i % 2 issued two tiles ahead of its LDS store
   // (one tile's MFMA + barrier more to land than a single set gives: the loop is load-latency
   // bound at two waves per SIMD); the same tiles in the same order
-  uint2 sa0[2], sb0[NB], sa1[2], sb1[NB];
-  auto gl16 = [&](int k0, uint2(&ra)[2], uint2(&rb)[NB]) {
+  uint2 sa0[NA], sb0[NB], sa1[NA], sb1[NB];
+  auto gl16 = [&](int k0, uint2(&ra)[NA], uint2(&rb)[NB]) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + NT * u, rr = e / IPR, kk = (e % IPR) * 4;
       const int row = min(r0 + rr, c.b - 1);
       ra[u] = *reinterpret_cast<const uint2 *>(pa + row * pla + k0 + kk);
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, nn = e / IPR, kk = (e % IPR) * 4;
       const int gate = nn / kStepUnits, jj = nn - gate * kStepUnits;
       rb[u] = *reinterpret_cast<const uint2 *>(pb + static_cast<int64_t>(gate * H + j0 + jj) * plb + k0 + kk);
     }
   };
-  auto ls16 = [&](int buf, const uint2(&ra)[2], const uint2(&rb)[NB]) {
+  auto ls16 = [&](int buf, const uint2(&ra)[NA], const uint2(&rb)[NB]) {
     __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + NT * u, rr = e >> 3, kk = (e & 7) * 4;
+    for (int u = 0; u < NA; ++u) {
+      const int e = tid + NT * u, rr = e / IPR, kk = (e % IPR) * 4;
       *reinterpret_cast<uint2 *>(ai + rr * AP + kk) = ra[u];
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int e = tid + NT * u, nn = e >> 3, kk = (e & 7) * 4;
+      const int e = tid + NT * u, nn = e / IPR, kk = (e % IPR) * 4;
       *reinterpret_cast<uint2 *>(bi + nn * AP + kk) = rb[u];
     }
   };
   auto kloop = [&](int nk) {
     if constexpr (W16 && PF2) {
       gl16(0, sa0, sb0);
-      if (nk > 1) gl16(kStepBK, sa1, sb1);
+      if (nk > 1) gl16(BK, sa1, sb1);
       ls16(0, sa0, sb0);
-      if (nk > 2) gl16(2 * kStepBK, sa0, sb0);
+      if (nk > 2) gl16(2 * BK, sa0, sb0);
       __syncthreads();
       for (int kt = 0; kt < nk; kt += 2) {
         mfma_tile(0);  // tile kt
         if (kt + 1 < nk) {
           ls16(1, sa1, sb1);
-          if (kt + 3 < nk) gl16((kt + 3) * kStepBK, sa1, sb1);
+          if (kt + 3 < nk) gl16((kt + 3) * BK, sa1, sb1);
         }
         __syncthreads();
         if (kt + 1 >= nk) break;
         mfma_tile(1);  // tile kt + 1
         if (kt + 2 < nk) {
           ls16(0, sa0, sb0);
-          if (kt + 4 < nk) gl16((kt + 4) * kStepBK, sa0, sb0);
+          if (kt + 4 < nk) gl16((kt + 4) * BK, sa0, sb0);
         }
         __syncthreads();
       }
@@ -330,7 +340,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       __syncthreads();
       int cur = 0;
       for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) gload((kt + 1) * kStepBK);
+        if (kt + 1 < nk) gload((kt + 1) * BK);
         mfma_tile(cur);
         if (kt + 1 < nk) lstore(cur ^ 1);
         __syncthreads();
@@ -347,7 +357,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
     pla = static_cast<int64_t>(W) * q.ldx;
     pb = q.wih16[d];
     plb = q.ldx;
-    kloop(q.ldx / kStepBK);
+    kloop(q.ldx / BK);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const float bi = q.b_ih[d][g * H + j];
@@ -362,7 +372,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
     pb = wb16;
     plb = H;
   }
-  if (!FX || !first) kloop(H / kStepBK);
+  if (!FX || !first) kloop(H / BK);
 
   // epilogue: C row (r&3) + 8 (r>>2) + 4 (lane>>5) of the wave's 32 rows, unit j = lane & 31.
   // Eight rows at a time, every load first and unconditional (rows past b read row b-1): a load
@@ -427,7 +437,10 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       } else {
         c.hp[o] = hpv[u];
       }
-      if (c.feat_mode == 1) c.feat[o] = act_forward(h, c.act);
+      if (c.feat_mode == 1) {
+        if (c.feat16) c.feat16[o] = static_cast<__bf16>(act_forward(h, c.act));
+        else c.feat[o] = act_forward(h, c.act);
+      }
       else if (c.feat_mode == 2 && t == W - 1) c.feat[bb * (2 * H) + d * H + j] = act_forward(h, c.act);
     }
   }
@@ -821,6 +834,7 @@ struct ppo_lstm_ctx {
   float *gh, *dhrec, *dcarry;        // [rows][8H], [rows][2H], [rows][2H]
   float *dy[2], *tmp;                // [rows*W][2H]
   float *feat_a, *feat_c;            // [rows][W*2H], [rows][2H]
+  __bf16 *feat16;                    // [rows][W*2H]: the actor features as bf16 (feat16_on())
   float *act_mu[PPO_MAX_LAYERS + 1], *act_ls[PPO_MAX_LAYERS + 1], *act_v[PPO_MAX_LAYERS + 1];
   float *dz[3][2];                   // ping-pong gradient buffers [rows][maxw]: mu, ls, critic
   float *slabs;                      // [kSplits][total] (the first `splits` used)
@@ -858,6 +872,17 @@ const int g_lstm_splits = [] {
 bool lstm_fusex_env() {
   const char *v = getenv("PPO_LSTM_FUSEX");
   return !(v && atoi(v) == 0);
+}
+
+// bf16 mode, ReLU: the actor's features (act(h), [B][W*2H]) are stored only as bf16 -- the two
+// actor MLPs' first-layer forward and weight-gradient GEMMs read them as RNE bf16 anyway, and the
+// input gradient's ReLU' needs only their sign, which RNE keeps -- so the step kernels write, and
+// those GEMMs read, half the bytes; bitwise the f32-stored form.  PPO_LSTM_FEAT16=0 keeps f32
+// (read per call: the bitwise test flips it).
+bool feat16_on(const ppo_lstm_ctx *x) {
+  const char *v = getenv("PPO_LSTM_FEAT16");
+  return x->prec == PPO_PREC_BF16 && x->cfg.activation == PPO_ACT_RELU &&
+         (x->cfg.window * 2 * x->cfg.latent) % 4 == 0 && !(v && atoi(v) == 0);
 }
 
 struct TimingScope {
@@ -985,7 +1010,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
     // step launch (the rollout's 1,024-row windows keep the GEMM: 5x the rows per launch fill the
     // GPU where one step's 1,024 rows do not)
     const bool fusex = fused_step && l == 0 && xin16 && x->w16 && !x->rollout &&
-                       (4 * H) % 128 == 0 && x->ldx16 % kStepBK == 0 && lstm_fusex_env();
+                       (4 * H) % 128 == 0 && x->ldx16 % 64 == 0 && lstm_fusex_env();
     if (fusex) {
       // no separate projection: lstm_step_fwdx_kernel below
     } else if (l == 0 && xin16 && x->w16 && (4 * H) % 128 == 0) {
@@ -1023,6 +1048,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         const bool top = l == N.layers - 1;
         a.cell.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
         a.cell.feat = z == 0 ? x->feat_a : x->feat_c;
+        a.cell.feat16 = (top && z == 0 && feat16_on(x)) ? x->feat16 : nullptr;
         a.cell.act = x->cfg.activation;
         a.cell.b = b;
         a.cell.w = W;
@@ -1106,6 +1132,7 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
       const bool top = l == N.layers - 1;
       a.feat_mode = top ? (z == 0 ? 1 : 2) : 0;
       a.feat = z == 0 ? x->feat_a : x->feat_c;
+      a.feat16 = (top && z == 0 && feat16_on(x)) ? x->feat16 : nullptr;
       a.act = x->cfg.activation;
       a.b = b;
       a.w = W;
@@ -1120,14 +1147,16 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
 }
 
 // MLP forward: m1 (and m2 on the same input, the actor's mean / logstd pair) over in [b][in0]
+// in16 (nullable): the input rows as bf16 (the bf16 actor features), read instead of in
 int mlp_forward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm, const float *in,
-                int b, hipStream_t st) {
+                int b, hipStream_t st, const __bf16 *in16 = nullptr) {
   const float *P = x->params;
   for (int l = 0; l < m[0]->n; ++l) {
     GemmProblem p[2] = {};
     for (int k = 0; k < nm; ++k) {
       const MlpLayer &L = m[k]->l[l];
       p[k].a = l == 0 ? in : acts[k][l - 1];
+      if (l == 0) p[k].a16 = in16;
       p[k].lda = L.in;
       p[k].b = P + L.w;
       p[k].ldb = L.in;
@@ -1145,9 +1174,11 @@ int mlp_forward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm,
 
 // MLP backward from dz (gradient of the output layer's pre-activation, [b][out]); weight grads
 // into the slabs, the input gradient (times act'(input) of the feature activation) into din.
+// in16 (nullable): the input rows as bf16 -- the first layer's weight-gradient B operand and the
+// input gradient's activation-derivative operand
 int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm, const float *in,
                  float *const *pp[2], float *din, int64_t ld_din, int feat_act, int b,
-                 hipStream_t st, bool sum_din = true) {
+                 hipStream_t st, bool sum_din = true, const __bf16 *in16 = nullptr) {
   // pp[k]: the problem's two ping-pong buffers; pp[k][0] holds the output-layer gradient
   const float *P = x->params;
   float *cur[2] = {pp[0][0], nm == 2 ? pp[1][0] : nullptr};
@@ -1158,6 +1189,7 @@ int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm
       p[k].a = cur[k];
       p[k].lda = L.out;
       p[k].b = l == 0 ? in : acts[k][l - 1];
+      if (l == 0) p[k].b16 = in16;
       p[k].ldb = L.in;
       p[k].c = x->slabs + L.w;
       p[k].ldc = L.in;
@@ -1185,6 +1217,7 @@ int mlp_backward(ppo_lstm_ctx *x, const Mlp *m[2], float *const *acts[2], int nm
         q[k].c = k == 0 ? din : x->tmp;
         q[k].ldc = ld_din;
         q[k].aux = in;
+        q[k].aux16 = in16;
       }
       q[k].m = b;
       q[k].n = L.in;
@@ -1383,7 +1416,8 @@ int forward_all(ppo_lstm_ctx *x, const float *xin, const __bf16 *xin16, int b, h
   if (int rc = lstm_forward(x, 1, xin, xin16, b, st)) return rc;
   const Mlp *am[2] = {&x->mu, &x->ls};
   float *const *aa[2] = {x->act_mu, x->act_ls};
-  if (int rc = mlp_forward(x, am, aa, 2, x->feat_a, b, st)) return rc;
+  if (int rc = mlp_forward(x, am, aa, 2, x->feat_a, b, st, feat16_on(x) ? x->feat16 : nullptr))
+    return rc;
   const Mlp *cm[2] = {&x->vc, nullptr};
   float *const *ca[2] = {x->act_v, nullptr};
   return mlp_forward(x, cm, ca, 1, x->feat_c, b, st);
@@ -1467,6 +1501,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   const int64_t o_dy0 = take(R * W * 2 * H), o_dy1 = take(R * W * 2 * H);
   const int64_t o_tmp = take(R * std::max<int64_t>(W * 2 * H, maxw));
   const int64_t o_fa = take(R * W * 2 * H), o_fc = take(R * 2 * H);
+  const int64_t o_f16 = take(R * W * H);
   int64_t o_mu[PPO_MAX_LAYERS + 1], o_ls[PPO_MAX_LAYERS + 1], o_v[PPO_MAX_LAYERS + 1];
   for (int l = 0; l <= c.n_hidden; ++l) {
     o_mu[l] = take(R * x->mu.l[l].out);
@@ -1512,6 +1547,7 @@ extern "C" int ppo_lstm_ctx_create(const ppo_lstm_cfg *cfg, int device, ppo_lstm
   x->tmp = w + o_tmp;
   x->feat_a = w + o_fa;
   x->feat_c = w + o_fc;
+  x->feat16 = reinterpret_cast<__bf16 *>(w + o_f16);
   for (int l = 0; l <= c.n_hidden; ++l) {
     x->act_mu[l] = w + o_mu[l];
     x->act_ls[l] = w + o_ls[l];
@@ -1793,7 +1829,8 @@ extern "C" int ppo_lstm_minibatch_grad(ppo_lstm_ctx *x, const float *states_d,
     float *const *aa[2] = {x->act_mu, x->act_ls};
     float *const *pp[2] = {x->dz[0], x->dz[1]};
     if (int rc = mlp_backward(x, am, aa, 2, x->feat_a, pp, x->dy[0],
-                              static_cast<int64_t>(W) * 2 * H, c.activation, b, st, false))
+                              static_cast<int64_t>(W) * 2 * H, c.activation, b, st, false,
+                              feat16_on(x) ? x->feat16 : nullptr))
       return rc;
     if (int rc = lstm_backward(x, 0, x->x, x16, b, st, x->tmp)) return rc;
   }

@@ -35,6 +35,8 @@ struct GemmProblem {
   int64_t ldc;
   const float *bias;   // EPI_FWD, nullable
   const float *aux;    // EPI_DX: layer input activations (same layout as c; c may alias it)
+  const __bf16 *aux16; // EPI_DX, bf16 kernel, nullable: the activations as bf16 instead of aux
+                       // (a ReLU net's: act'(y) depends only on the sign, which RNE keeps)
   float *colsum;       // EPI_PARTIAL: bias-gradient slab base, nullable
   float *colsum2;      // bf16 kernel: a second slab base receiving the same column sums, nullable
   int m, n;
@@ -180,11 +182,23 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[TM][TN], const
         // the elements it writes, so the order change is safe under aliasing
         float ax[16];
         if (EPI == EPI_DX) {
+          // one branch per block on the operand's width (a per-element select serialised the
+          // 16 loads behind it)
+          if (P.aux16) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            ax[r] = (!checked || (row < M && col < N)) ? P.aux[static_cast<int64_t>(row) * P.ldc + col]
-                                                       : 0.f;
+            for (int r = 0; r < 16; ++r) {
+              const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+              ax[r] = (!checked || (row < M && col < N))
+                          ? static_cast<float>(P.aux16[static_cast<int64_t>(row) * P.ldc + col])
+                          : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+              ax[r] = (!checked || (row < M && col < N)) ? P.aux[static_cast<int64_t>(row) * P.ldc + col]
+                                                         : 0.f;
+            }
           }
         }
 #pragma unroll
@@ -693,23 +707,29 @@ static bool vec4_ok16(const GemmBatch &gb, int nprob, bool operand_a) {
   return true;
 }
 
-// bf16 operands from global memory (the BiLSTM's dG, h_prev and gathered rows, and its bf16
-// weight copy): A alone or A and B (FWD, PARTIAL), vector loads for the bf16 operands -- the
-// producers keep those buffers 8-B aligned with ld % 4 == 0, which the host checks
+// bf16 operands from global memory (the BiLSTM's dG, h_prev, gathered rows and features, and its
+// bf16 weight copy): A alone, A and B, or B alone with an f32 A (FWD, PARTIAL), vector loads for
+// the bf16 operands -- the producers keep those buffers 8-B aligned with ld % 4 == 0, which the
+// host checks
 template <int TM, int TN, int WM, int WN, int AMODE, int BMODE, int EPI>
 static int launch_gemm_bf16_src(const GemmBatch &gb, int nprob, dim3 grid, hipStream_t st) {
   const bool a16 = gb.p[0].a16 != nullptr, b16 = gb.p[0].b16 != nullptr;
   for (int i = 1; i < nprob; ++i)
     PPO_REQUIRE((gb.p[i].a16 != nullptr) == a16 && (gb.p[i].b16 != nullptr) == b16,
                 "gemm: mixed bf16 / f32 operands in one batch");
-  PPO_REQUIRE(a16 && vec4_ok16(gb, nprob, true) && (!b16 || vec4_ok16(gb, nprob, false)),
-              "gemm: bf16-source operands need A in bf16 and 8-B aligned rows (ld %% 4 == 0)");
+  PPO_REQUIRE((!a16 || vec4_ok16(gb, nprob, true)) && (!b16 || vec4_ok16(gb, nprob, false)),
+              "gemm: bf16-source operands need 8-B aligned rows (ld %% 4 == 0)");
   // an f32 B operand (weights, or rows of an odd width) may need scalar loads
   const bool vb = b16 || vec4_ok(gb, nprob, false);
   if constexpr (EPI == EPI_DX) {
     PPO_REQUIRE(false, "gemm: no bf16-source DX variant");
   } else {
-    if (b16)
+    if (!a16) {  // f32 A (the wgrad's dY, its column sums taken before rounding), bf16 B
+      if (vec4_ok(gb, nprob, true))
+        launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, false, true>(gb, nprob, grid, st);
+      else
+        launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 1, 4, false, true>(gb, nprob, grid, st);
+    } else if (b16)
       launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, true>(gb, nprob, grid, st);
     else if (vb)
       launch_gemm_bf16_v<TM, TN, WM, WN, AMODE, BMODE, EPI, 4, 4, true, false>(gb, nprob, grid, st);

@@ -393,6 +393,32 @@ def test_fused_forward_step_bitwise_equals_layered(gpu, monkeypatch, fusex):
 
 
 @pytest.mark.parametrize("b", [200, 4096 + 72])
+def test_bf16_features_bitwise_equal_f32_stored(gpu, monkeypatch, b):
+    """bf16 mode, ReLU: the actor features stored only as bf16 (PPO_LSTM_FEAT16, the default) --
+    read as bf16 by the actor MLPs' first-layer forward and weight-gradient GEMMs and by the input
+    gradient's ReLU' -- reproduce the f32-stored features bitwise (the GEMMs rounded them to bf16
+    as they staged them; ReLU' needs only the sign): forward outputs, the whole minibatch gradient
+    and the losses on the main.py network, a partial last row tile at both sizes."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=41)
+    agent.engine.set_precision("bf16")
+    gen = torch.Generator().manual_seed(12)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    old_logp = torch.randn(b, generator=gen) - 10.0
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PPO_LSTM_FEAT16", mode)
+        out[mode] = (_forward(agent, x), _grad(agent, x, actions, old_logp, adv, vt))
+    for k in out["1"][0]:
+        assert torch.equal(out["1"][0][k], out["0"][0][k]), k
+    assert torch.equal(out["1"][1][0], out["0"][1][0])
+    assert torch.equal(out["1"][1][1], out["0"][1][1])
+
+
+@pytest.mark.parametrize("b", [200, 4096 + 72])
 def test_wide_recurrent_gradient_bitwise_equals_layered(gpu, monkeypatch, b):
     """bf16 mode: the backward steps' recurrent gradient dh_rec = dG W_hh on the wide path's
     LDS-DMA GEMM (W_hh^T images) reproduces gemm_bf16_kernel's bitwise -- the whole minibatch
