@@ -167,6 +167,14 @@ __global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(CellArgs q) {
 // accumulator), gh = acc + b_hh, then pre = gh + Gx and the same cell arithmetic.
 constexpr int kStepUnits = 64, kStepBK = 32;
 constexpr int kStepRowsMb = 128;  // rows per workgroup of the minibatch step launches
+// their k-loop pipeline (lstm_step_fwd_body PIPE): 2, the LDS-DMA ring (default; measured
+// against 1 on one box, alternating: forward steps 115.2 -> 100.5 ms per iteration, the main.py
+// line 399.0 / 398.3 -> 384.2 / 383.4 ms, profiles/r06/lstm_pipe_*), or PPO_LSTM_STEP_PIPE=1, two
+// register staging sets; read per call
+static int lstm_step_pipe_env() {
+  const char *v = getenv("PPO_LSTM_STEP_PIPE");
+  return (v && atoi(v) == 1) ? 1 : 2;
+}
 struct StepArgs {
   CellArgs cell;
   const float *whh[2];  // W_hh per direction, [4H][H] f32 (torch layout)
@@ -192,18 +200,27 @@ typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
 // ROWS rows x 64 units per workgroup, ROWS / 32 x 2 waves (a wave: 32 rows x 32 units x 4 gates).
 // Every workgroup streams the whole 256 x K weight panel of its 64 units, so the panel traffic
 // per launch is (b / ROWS) x 2 x 4H x K x 2 B: 128-row workgroups halve it against 64.
-template <bool W16, bool FX, int ROWS, bool PF2>
+//
+// PIPE: the k-loop's operand pipeline -- 0: one register staging set (load tile k+1 while tile k
+// multiplies); 1: two register sets, loads two tiles ahead; 2 (W16): LDS-DMA ring
+// (global_load_lds_dwordx4 straight into swizzled [rows][64] images, wide_gemm.h's RowImage
+// layout), 3 stages of 64-deep k-tiles, no register staging.
+template <bool W16, bool FX, int ROWS, int PIPE>
 __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   static_assert(ROWS == 64 || ROWS == 128, "step rows");
+  static_assert(PIPE < 2 || W16, "LDS-DMA from bf16 operands only");
+  constexpr bool DMA = PIPE == 2;
   constexpr int NT = 4 * ROWS, RT = ROWS / 32;    // threads, row tiles
-  // k-tile depth (64 for the prefetching loop measured: its two staging sets then need 123 VGPRs
-  // of spill in lstm_step_fwdx_kernel)
-  constexpr int BK = kStepBK;
+  // k-tile depth (64 for the register-prefetching loop measured: its two staging sets then need
+  // 123 VGPRs of spill in lstm_step_fwdx_kernel)
+  constexpr int BK = DMA ? 64 : kStepBK;
   constexpr int IPR = BK / 4;                     // 4-element staging items per operand row
   constexpr int NA = IPR * ROWS / NT, NB = 256 * IPR / NT;  // A / B staging items per thread
-  constexpr int AP = BK + 8;                      // bf16 image row pitch (16 B of padding)
+  constexpr int AP = DMA ? BK : BK + 8;           // bf16 image row pitch (16 B of padding unless
+                                                  // swizzled)
   constexpr int AIMG = ROWS * AP, BIMG = 4 * kStepUnits * AP;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * (AIMG + BIMG)];
+  constexpr int NSTG = DMA ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[NSTG * (AIMG + BIMG)];
   const CellArgs &c = q.cell;
   const int H = c.h, W = c.w;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -222,8 +239,8 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   // staging: A ROWS rows x 32 k (2 float4 per thread), B 256 rows (gate g: rows g*H + j0 .. +63)
   // x 32 k (NB float4 per thread); rows past b load row b-1 (clamped, results discarded).  W16:
   // the phase's bf16 operands (A rows at pa + row * pla, B rows at pb + n * plb)
-  float4 va[NA], vb[NB];
-  uint2 va16[NA], vb16[NB];
+  float4 va[DMA ? 1 : NA], vb[DMA ? 1 : NB];
+  uint2 va16[DMA ? 1 : NA], vb16[DMA ? 1 : NB];
   const __bf16 *wb16 = W16 ? q.whh16[d] : nullptr;
   const __bf16 *pa = arow16, *pb = wb16;
   int64_t pla = lda, plb = H;
@@ -284,8 +301,9 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   // W16: two register sets, tile i's loads in set i % 2 issued two tiles ahead of its LDS store
   // (one tile's MFMA + barrier more to land than a single set gives: the loop is load-latency
   // bound at two waves per SIMD); the same tiles in the same order
-  uint2 sa0[NA], sb0[NB], sa1[NA], sb1[NB];
-  auto gl16 = [&](int k0, uint2(&ra)[NA], uint2(&rb)[NB]) {
+  uint2 sa0[PIPE == 1 ? NA : 1], sb0[PIPE == 1 ? NB : 1], sa1[PIPE == 1 ? NA : 1],
+      sb1[PIPE == 1 ? NB : 1];
+  auto gl16 = [&](int k0, uint2(&ra)[PIPE == 1 ? NA : 1], uint2(&rb)[PIPE == 1 ? NB : 1]) {
 #pragma unroll
     for (int u = 0; u < NA; ++u) {
       const int e = tid + NT * u, rr = e / IPR, kk = (e % IPR) * 4;
@@ -299,7 +317,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       rb[u] = *reinterpret_cast<const uint2 *>(pb + static_cast<int64_t>(gate * H + j0 + jj) * plb + k0 + kk);
     }
   };
-  auto ls16 = [&](int buf, const uint2(&ra)[NA], const uint2(&rb)[NB]) {
+  auto ls16 = [&](int buf, const uint2(&ra)[PIPE == 1 ? NA : 1], const uint2(&rb)[PIPE == 1 ? NB : 1]) {
     __bf16 *ai = lds + buf * (AIMG + BIMG), *bi = ai + AIMG;
 #pragma unroll
     for (int u = 0; u < NA; ++u) {
@@ -312,8 +330,61 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
       *reinterpret_cast<uint2 *>(bi + nn * AP + kk) = rb[u];
     }
   };
+  // PIPE 2: one stage = the A image (ROWS / 8 wave-instructions of 8 rows x 128 B) and the four
+  // gates' 64-row B images (8 each); rows past b read row b-1 (clamped, results discarded)
+  constexpr int NWV = NT / 64, NIA = ROWS / 8, NIB = 32, PER = (NIA + NIB) / NWV;
+  static_assert((NIA + NIB) % NWV == 0, "uneven LDS-DMA split over the waves");
+  auto dma_fill = [&](int buf, int k0) {
+    __bf16 *ia = lds + buf * (AIMG + BIMG), *ib = ia + AIMG;
+#pragma unroll
+    for (int jj = 0; jj < PER; ++jj) {
+      const int i = wv + NWV * jj;
+      if (i < NIA) {
+        const int row = 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        const int grow = min(r0 + row, c.b - 1);
+        __builtin_amdgcn_global_load_lds(pa + grow * pla + k0 + 8 * lc,
+                                         (wide::lds_void *)(ia + 512 * i), 16, 0, 0);
+      } else {
+        const int ibb = i - NIA, gate = ibb >> 3, row = 8 * (ibb & 7) + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        __builtin_amdgcn_global_load_lds(pb + static_cast<int64_t>(gate * H + j0 + row) * plb + k0 + 8 * lc,
+                                         (wide::lds_void *)(ib + 512 * ibb), 16, 0, 0);
+      }
+    }
+  };
+  auto mfma_dma = [&](int buf) {
+    const __bf16 *ia = lds + buf * (AIMG + BIMG), *ib = ia + AIMG;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const lstm_bf16x8 a = wide::RowImage<ROWS, NWV>::frag(ia, 32 * mt, ks, lane);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const lstm_bf16x8 bv = wide::RowImage<64, NWV>::frag(ib + g * 64 * 64, 32 * ug, ks, lane);
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[g], 0, 0, 0);
+      }
+    }
+  };
   auto kloop = [&](int nk) {
-    if constexpr (W16 && PF2) {
+    if constexpr (DMA) {
+#pragma unroll
+      for (int s2 = 0; s2 < NSTG - 1; ++s2)
+        if (s2 < nk) dma_fill(s2, s2 * BK);
+      int buf = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        // this wave's DMA of tile kt has landed (the younger tile may stay in flight), then every
+        // wave's by the barrier; every wave is done reading buffer (kt - 1) % NSTG, refilled below
+        wide::vm_wait_le<PER, NSTG - 2>(min(NSTG - 2, nk - 1 - kt));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + NSTG - 1 < nk) dma_fill(buf == 0 ? NSTG - 1 : buf - 1, (kt + NSTG - 1) * BK);
+        mfma_dma(buf);
+        buf = buf + 1 == NSTG ? 0 : buf + 1;
+      }
+      __syncthreads();  // every wave's reads are done before the next phase refills the ring
+    } else if constexpr (W16 && PIPE == 1) {
       gl16(0, sa0, sb0);
       if (nk > 1) gl16(BK, sa1, sb1);
       ls16(0, sa0, sb0);
@@ -446,19 +517,20 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   }
 }
 
-template <bool W16>
+template <bool W16, int PIPE>
 __global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwd_kernel(StepArgs q) {
-  lstm_step_fwd_body<W16, false, kStepRowsMb, W16>(q);
+  lstm_step_fwd_body<W16, false, kStepRowsMb, PIPE>(q);
 }
 // the rollout's launches (1,024-row windows, 64-row workgroups: 8 x more of them than rows / 128
 // would give): the same body under its own name, so the traffic / roofline rows of the minibatch
 // kernel stay per-launch comparable
 __global__ __launch_bounds__(256) void lstm_step_fwd_rollout_kernel(StepArgs q) {
-  lstm_step_fwd_body<true, false, 64, false>(q);
+  lstm_step_fwd_body<true, false, 64, 0>(q);
 }
 // layer 0 with the input projection in the step (FX), minibatch launches
+template <int PIPE>
 __global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwdx_kernel(StepArgs q) {
-  lstm_step_fwd_body<true, true, kStepRowsMb, true>(q);
+  lstm_step_fwd_body<true, true, kStepRowsMb, PIPE>(q);
 }
 
 struct CellBwdArgs {
@@ -1067,7 +1139,8 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
           }
           a.x16 = xin16;
           a.ldx = ldx;
-          TimRec rec{KC_LSTM, "lstm_step_fwdx_kernel", 0.0, 0.0};
+          const int pipe = lstm_step_pipe_env();
+          TimRec rec{KC_LSTM, pipe == 2 ? "lstm_step_fwdx_kernel<2>" : "lstm_step_fwdx_kernel<1>", 0.0, 0.0};
           if (tim_active()) {
             const double kk = ldx + (s > 0 ? H : 0);
             rec.flops = 2.0 * 2 * b * 4.0 * H * kk;
@@ -1076,14 +1149,17 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
             rec.bytes = 2.0 * 4 * H * ldx * 2 + 2.0 * b * ldx * 2 + 2.0 * b * H * (4.0 * 6 + 2.0) +
                         (s > 0 ? 2.0 * 4 * H * H * 2 + 2.0 * b * H * (2.0 + 4.0) : 0.0);
           }
-          launch_k(rec, lstm_step_fwdx_kernel, grid, block, 0, st, a);
+          if (pipe == 2) launch_k(rec, lstm_step_fwdx_kernel<2>, grid, block, 0, st, a);
+          else launch_k(rec, lstm_step_fwdx_kernel<1>, grid, block, 0, st, a);
           PPO_LAUNCHED();
           continue;
         }
         // the launched instantiation's name (rocprof's, for the traffic table)
         TimRec rec{KC_LSTM,
-                   x->w16 ? (x->rollout ? "lstm_step_fwd_rollout_kernel" : "lstm_step_fwd_kernel<true>")
-                          : "lstm_step_fwd_kernel<false>",
+                   x->w16 ? (x->rollout ? "lstm_step_fwd_rollout_kernel"
+                                        : (lstm_step_pipe_env() == 2 ? "lstm_step_fwd_kernel<true, 2>"
+                                                                     : "lstm_step_fwd_kernel<true, 1>"))
+                          : "lstm_step_fwd_kernel<false, 0>",
                    0.0, 0.0};
         if (tim_active()) {
           rec.flops = 2.0 * 2 * b * 4.0 * H * H;
@@ -1097,9 +1173,10 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
           a.whh16[0] = x->w16 + L.w_hh[0];
           a.whh16[1] = x->w16 + L.w_hh[1];
           if (x->rollout) launch_k(rec, lstm_step_fwd_rollout_kernel, grid_r, dim3(256), 0, st, a);
-          else launch_k(rec, lstm_step_fwd_kernel<true>, grid, block, 0, st, a);
+          else if (lstm_step_pipe_env() == 2) launch_k(rec, lstm_step_fwd_kernel<true, 2>, grid, block, 0, st, a);
+          else launch_k(rec, lstm_step_fwd_kernel<true, 1>, grid, block, 0, st, a);
         } else {
-          launch_k(rec, lstm_step_fwd_kernel<false>, grid, block, 0, st, a);
+          launch_k(rec, lstm_step_fwd_kernel<false, 0>, grid, block, 0, st, a);
         }
         PPO_LAUNCHED();
         continue;

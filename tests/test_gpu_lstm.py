@@ -419,6 +419,32 @@ def test_bf16_features_bitwise_equal_f32_stored(gpu, monkeypatch, b):
 
 
 @pytest.mark.parametrize("b", [200, 4096 + 72])
+def test_step_pipelines_bitwise_equal(gpu, monkeypatch, b):
+    """bf16 forward steps: the LDS-DMA k-loop (PPO_LSTM_STEP_PIPE=2: global_load_lds into
+    swizzled 64-deep k-tile images, three stages) reproduces the register-staged one (1) bitwise --
+    the same k-steps in the same order over the same bf16 operands: forward outputs, the whole
+    minibatch gradient and the losses on the main.py network, partial last row tiles (rows past
+    b are clamped to row b-1 and discarded)."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=52)
+    agent.engine.set_precision("bf16")
+    gen = torch.Generator().manual_seed(13)
+    x = torch.randn(b, window, obs, generator=gen)
+    actions = torch.randn(b, act, generator=gen) * 0.3
+    old_logp = torch.randn(b, generator=gen) - 10.0
+    adv = torch.randn(b, 1, generator=gen)
+    vt = torch.randn(b, 1, generator=gen)
+    out = {}
+    for mode in ("2", "1"):
+        monkeypatch.setenv("PPO_LSTM_STEP_PIPE", mode)
+        out[mode] = (_forward(agent, x), _grad(agent, x, actions, old_logp, adv, vt))
+    for k in out["2"][0]:
+        assert torch.equal(out["2"][0][k], out["1"][0][k]), k
+    assert torch.equal(out["2"][1][0], out["1"][1][0])
+    assert torch.equal(out["2"][1][1], out["1"][1][1])
+
+
+@pytest.mark.parametrize("b", [200, 4096 + 72])
 def test_wide_recurrent_gradient_bitwise_equals_layered(gpu, monkeypatch, b):
     """bf16 mode: the backward steps' recurrent gradient dh_rec = dG W_hh on the wide path's
     LDS-DMA GEMM (W_hh^T images) reproduces gemm_bf16_kernel's bitwise -- the whole minibatch
