@@ -206,7 +206,7 @@ typedef float lstm_f32x16 __attribute__((ext_vector_type(16)));
 // (global_load_lds_dwordx4 straight into swizzled [rows][64] images, wide_gemm.h's RowImage
 // layout), 3 stages of 64-deep k-tiles, no register staging.
 template <bool W16, bool FX, int ROWS, int PIPE>
-__device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
+__device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q, int d) {
   static_assert(ROWS == 64 || ROWS == 128, "step rows");
   static_assert(PIPE < 2 || W16, "LDS-DMA from bf16 operands only");
   constexpr bool DMA = PIPE == 2;
@@ -225,7 +225,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
   const int H = c.h, W = c.w;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int mt = wv % RT, ug = wv / RT;
-  const int r0 = blockIdx.x * ROWS, j0 = blockIdx.y * kStepUnits, d = blockIdx.z;
+  const int r0 = blockIdx.x * ROWS, j0 = blockIdx.y * kStepUnits;
   const int t = d == 0 ? c.s : W - 1 - c.s;
   const int tp = d == 0 ? t - 1 : t + 1;
   const float *arow = c.y + static_cast<int64_t>(tp) * 2 * H + d * H;  // + row * W * 2H + k
@@ -519,18 +519,26 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q) {
 
 template <bool W16, int PIPE>
 __global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwd_kernel(StepArgs q) {
-  lstm_step_fwd_body<W16, false, kStepRowsMb, PIPE>(q);
+  lstm_step_fwd_body<W16, false, kStepRowsMb, PIPE>(q, blockIdx.z);
 }
 // the rollout's launches (1,024-row windows, 64-row workgroups: 8 x more of them than rows / 128
 // would give): the same body under its own name, so the traffic / roofline rows of the minibatch
 // kernel stay per-launch comparable
 __global__ __launch_bounds__(256) void lstm_step_fwd_rollout_kernel(StepArgs q) {
-  lstm_step_fwd_body<true, false, 64, 0>(q);
+  lstm_step_fwd_body<true, false, 64, 0>(q, blockIdx.z);
+}
+// the rollout's steps of BOTH nets in one launch (blockIdx.z = 2 net + direction): one step's
+// 1,024 rows give a net 128 workgroups, half the CUs
+struct StepArgs2 {
+  StepArgs n[2];
+};
+__global__ __launch_bounds__(256) void lstm_step_fwd_rollout2_kernel(StepArgs2 q) {
+  lstm_step_fwd_body<true, false, 64, 0>(q.n[blockIdx.z >> 1], blockIdx.z & 1);
 }
 // layer 0 with the input projection in the step (FX), minibatch launches
 template <int PIPE>
 __global__ __launch_bounds__(4 * kStepRowsMb) void lstm_step_fwdx_kernel(StepArgs q) {
-  lstm_step_fwd_body<true, true, kStepRowsMb, PIPE>(q);
+  lstm_step_fwd_body<true, true, kStepRowsMb, PIPE>(q, blockIdx.z);
 }
 
 struct CellBwdArgs {
@@ -915,6 +923,11 @@ struct ppo_lstm_ctx {
   int maxw;
   int fused_step;  // bf16 forward steps as lstm_step_fwd_kernel (ppo_lstm_fused_step)
   int rollout;     // inside forward_rollout: the step launches take the rollout kernel
+  // forward_all's paired rollout steps: lstm_forward queues each net's step arguments (s > 0)
+  // here instead of launching them, forward_all then launches both nets' step s together
+  int defer_steps;
+  int npend[2];
+  StepArgs pend[2][16];
   Timing tim;
 };
 
@@ -1172,6 +1185,11 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         if (x->w16) {
           a.whh16[0] = x->w16 + L.w_hh[0];
           a.whh16[1] = x->w16 + L.w_hh[1];
+          if (x->rollout && x->defer_steps) {  // forward_all launches it with the other net's
+            PPO_REQUIRE(x->npend[z] < 16, "ppo_lstm: too many deferred steps");
+            x->pend[z][x->npend[z]++] = a;
+            continue;
+          }
           if (x->rollout) launch_k(rec, lstm_step_fwd_rollout_kernel, grid_r, dim3(256), 0, st, a);
           else if (lstm_step_pipe_env() == 2) launch_k(rec, lstm_step_fwd_kernel<true, 2>, grid, block, 0, st, a);
           else launch_k(rec, lstm_step_fwd_kernel<true, 1>, grid, block, 0, st, a);
@@ -1489,8 +1507,34 @@ int check_rows(ppo_lstm_ctx *x, int b) {
 }
 
 int forward_all(ppo_lstm_ctx *x, const float *xin, const __bf16 *xin16, int b, hipStream_t st) {
+  // the rollout (one-layer nets, W16 step kernels): both nets' projections and first steps, then
+  // each step s of both nets as one launch (lstm_step_fwd_rollout2_kernel) -- the same per-net
+  // launches' work in stream order, so bitwise the same; PPO_LSTM_PAIR_STEPS=0 launches per net
+  const int H = x->cfg.latent, W = x->cfg.window;
+  const char *pv = getenv("PPO_LSTM_PAIR_STEPS");
+  const bool pair = x->rollout && x->w16 && x->fused_step && x->prec == PPO_PREC_BF16 &&
+                    H % kStepUnits == 0 && x->net[0].layers == 1 && x->net[1].layers == 1 &&
+                    W <= 16 && !(pv && atoi(pv) == 0);
+  struct DeferScope {
+    ppo_lstm_ctx *x;
+    ~DeferScope() { x->defer_steps = 0; }
+  } defer_scope{x};
+  x->defer_steps = pair ? 1 : 0;
+  x->npend[0] = x->npend[1] = 0;
   if (int rc = lstm_forward(x, 0, xin, xin16, b, st)) return rc;
   if (int rc = lstm_forward(x, 1, xin, xin16, b, st)) return rc;
+  x->defer_steps = 0;
+  PPO_REQUIRE(x->npend[0] == x->npend[1], "ppo_lstm: paired rollout steps %d / %d", x->npend[0],
+              x->npend[1]);
+  for (int i = 0; i < x->npend[0]; ++i) {
+    StepArgs2 a2{};
+    a2.n[0] = x->pend[0][i];
+    a2.n[1] = x->pend[1][i];
+    TimRec rec{KC_LSTM, "lstm_step_fwd_rollout2_kernel", 0.0, 0.0};
+    launch_k(rec, lstm_step_fwd_rollout2_kernel, dim3(ceil_div(b, 64), H / kStepUnits, 4),
+             dim3(256), 0, st, a2);
+    PPO_LAUNCHED();
+  }
   const Mlp *am[2] = {&x->mu, &x->ls};
   float *const *aa[2] = {x->act_mu, x->act_ls};
   if (int rc = mlp_forward(x, am, aa, 2, x->feat_a, b, st, feat16_on(x) ? x->feat16 : nullptr))

@@ -418,6 +418,23 @@ def test_bf16_features_bitwise_equal_f32_stored(gpu, monkeypatch, b):
     assert torch.equal(out["1"][1][1], out["0"][1][1])
 
 
+def test_rollout_paired_steps_bitwise_equal(gpu, monkeypatch):
+    """The rollout forward with both nets' step s in one launch (lstm_step_fwd_rollout2_kernel,
+    PPO_LSTM_PAIR_STEPS, the default) reproduces the per-net launches bitwise: mean, std, value and
+    both LSTM outputs on the main.py network, 200 rows (a partial last row block)."""
+    obs, window, act, latent, layers, hidden = 348, 5, 17, 256, 1, (256, 256, 128, 128)
+    b = 200
+    agent = _agent(gpu, obs, window, act, latent, layers, hidden, "relu", b, seed=61)
+    agent.engine.set_precision("bf16")
+    x = torch.randn(b, window, obs, generator=torch.Generator().manual_seed(14))
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PPO_LSTM_PAIR_STEPS", mode)
+        out[mode] = _forward(agent, x)
+    for k in out["1"]:
+        assert torch.equal(out["1"][k], out["0"][k]), k
+
+
 @pytest.mark.parametrize("b", [200, 4096 + 72])
 def test_step_pipelines_bitwise_equal(gpu, monkeypatch, b):
     """bf16 forward steps: the LDS-DMA k-loop (PPO_LSTM_STEP_PIPE=2: global_load_lds into
