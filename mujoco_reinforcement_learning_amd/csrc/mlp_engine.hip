@@ -163,9 +163,12 @@ __device__ __forceinline__ float4 rb4(float4 v, int bf16) {
 // H_L) is not launched.  Waves combine in a fixed order; one partial per block.
 constexpr int kFusedHeadAct = 8;
 template <int NJ, bool FW>
-__global__ __launch_bounds__(256) void update_head_q4_kernel(UpdateHeadArgs q) {
+// two workgroups per CU where the registers allow it (NJ <= 16: 512 blocks then run in one round)
+__global__ __launch_bounds__(256, NJ <= 16 ? 2 : 1) void update_head_q4_kernel(UpdateHeadArgs q) {
   constexpr int D = 16 * NJ;
-  constexpr int KA = kMaxAct / 4;
+  // action groups of 4 per lane: the fused-wgrad instantiation runs only for A <= kFusedHeadAct,
+  // so it sizes its per-action registers for that (kMaxAct / 4 groups cost it 30 VGPRs)
+  constexpr int KA = FW ? kFusedHeadAct / 4 : kMaxAct / 4;
   constexpr int CH = (4 * NJ + 63) / 64;  // float4 column chunks per lane (fused wgrad)
   constexpr int AF = FW ? kFusedHeadAct : 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
