@@ -278,7 +278,7 @@ struct SliceTable {
 // std==0 -> 1; row_stats.h, the fused rollout step's exact arithmetic), cast to f32, write
 // permuted (N, W, O).  running_gym_sequential_vectorized.py:61-92.  O <= 32 (wider rows take
 // obs_normalize_wide_kernel).
-__global__ void obs_normalize_kernel(const double *__restrict__ window, float *__restrict__ state,
+__global__ __launch_bounds__(128) void obs_normalize_kernel(const double *__restrict__ window, float *__restrict__ state,
                                      int n, int o, int w, SliceTable tab, int normalize) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // (env, slot)
   if (i >= static_cast<int64_t>(n) * w) return;
