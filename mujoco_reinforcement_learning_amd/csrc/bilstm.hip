@@ -82,7 +82,7 @@ struct CellArgs {
   const float *gh;     // [B][2][4H] recurrent projection incl. b_hh (nullptr at the first step)
   const float *b_hh[2];
   float *c;            // [B*W][2H] cell states
-  float *y;            // [B*W][2H] layer output h
+  float *y;            // [B*W][2H] layer output h (step kernels: nullable, W16 only)
   float *hp;           // [B*W][2H] h_prev (zeros at each direction's first step)
   __bf16 *hp16;        // bf16 mode: h_prev as bf16 instead (the dW_hh GEMM's only operand use)
   float *feat;         // optional act(h): mode 1 -> [B*W][2H] (actor), mode 2 -> [B][2H] at t=W-1
@@ -228,7 +228,8 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q, int d) {
   const int r0 = blockIdx.x * ROWS, j0 = blockIdx.y * kStepUnits;
   const int t = d == 0 ? c.s : W - 1 - c.s;
   const int tp = d == 0 ? t - 1 : t + 1;
-  const float *arow = c.y + static_cast<int64_t>(tp) * 2 * H + d * H;  // + row * W * 2H + k
+  // f32 h_prev rows (+ row * W * 2H + k; the f32-staged instantiation only)
+  const float *arow = W16 ? nullptr : c.y + static_cast<int64_t>(tp) * 2 * H + d * H;
   // W16: h_prev as bf16 from hp16's row t (the previous step wrote it there: bf16(h(tp)), the
   // rounding the f32 staging applies)
   const __bf16 *arow16 = W16 ? c.hp16 + static_cast<int64_t>(t) * 2 * H + d * H : nullptr;
@@ -495,7 +496,7 @@ __device__ __forceinline__ void lstm_step_fwd_body(const StepArgs &q, int d) {
       g[2 * H + j] = gg;
       g[3 * H + j] = og;
       c.c[o] = cn;
-      c.y[o] = h;
+      if (c.y) c.y[o] = h;  // null: a one-layer net's minibatch step, where nothing reads h in f32
       if constexpr (W16) {
         // row t's h_prev is already there (FX, first step: zeros); h goes to the next step's row
         if (FX && first) c.hp16[o] = static_cast<__bf16>(0.f);
@@ -1127,7 +1128,9 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
         a.cell.b_hh[0] = P + L.b_hh[0];
         a.cell.b_hh[1] = P + L.b_hh[1];
         a.cell.c = x->c[z][l];
-        a.cell.y = x->y[z][l];
+        // the layer output h in f32 feeds only a stacked layer and the rollout's LSTM-output copy
+        // (ppo_lstm_forward): a one-layer net's minibatch step (fusex) does not write it
+        a.cell.y = (fusex && N.layers == 1) ? nullptr : x->y[z][l];
         a.cell.hp = x->hp[z][l];
         a.cell.hp16 = b16 ? x->hp16[z][l] : nullptr;
         const bool top = l == N.layers - 1;
