@@ -1160,9 +1160,10 @@ int lstm_forward(ppo_lstm_ctx *x, int z, const float *xin, const __bf16 *xin16, 
           if (tim_active()) {
             const double kk = ldx + (s > 0 ? H : 0);
             rec.flops = 2.0 * 2 * b * 4.0 * H * kk;
-            // W_ih (and W_hh) images and the bf16 rows in; gates / c / h out (f32) and the next
+            // W_ih (and W_hh) images and the bf16 rows in; gates / c (/ h unless one-layer) out (f32) and the next
             // row's bf16 h_prev; s > 0: the staged bf16 h_prev and c_prev in
-            rec.bytes = 2.0 * 4 * H * ldx * 2 + 2.0 * b * ldx * 2 + 2.0 * b * H * (4.0 * 6 + 2.0) +
+            rec.bytes = 2.0 * 4 * H * ldx * 2 + 2.0 * b * ldx * 2 +
+                        2.0 * b * H * (4.0 * (a.cell.y ? 6 : 5) + 2.0) +
                         (s > 0 ? 2.0 * 4 * H * H * 2 + 2.0 * b * H * (2.0 + 4.0) : 0.0);
           }
           if (pipe == 2) launch_k(rec, lstm_step_fwdx_kernel<2>, grid, block, 0, st, a);
