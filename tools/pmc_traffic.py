@@ -27,7 +27,16 @@ def kernel_key(name: str) -> str:
         elif ch == "(" and depth == 0:
             name = name[:i]
             break
-    return name[5:] if name.startswith("ppo::") else name
+    # drop every namespace qualifier outside the template arguments (ppo::, ppo::lstm::, ...)
+    depth, cut = 0, 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif depth == 0 and name.startswith("::", i):
+            cut = i + 2
+    return name[cut:]
 
 
 _LAYER = {"32, 20,": "L2", "64, 9,": "L3"}
